@@ -1,0 +1,187 @@
+/*
+ * scann_mi355x.h — C ABI of the MI355X tree-AH / LUT16 query path.
+ *
+ * This is the drop-in boundary for the reference's batched search seam
+ * (SURVEY.md §8b).  One call replaces, for a whole query batch:
+ *   TreeAHHybridResidual::FindNeighborsBatchedImpl
+ *       (scann/tree_x_hybrid/tree_ah_hybrid_residual.cc:631-846)
+ *   TreeXHybridSMMD::FindNeighborsBatchedImpl for non-residual indexes
+ *       (scann/tree_x_hybrid/tree_x_hybrid_smmd.cc:565-669, 718-790)
+ *   followed by the exact reorder and SortAndDropResults of
+ *   SingleMachineSearcherBase<float>::FindNeighborsBatched
+ *       (scann/base/single_machine_base.cc:570-587, 849-901)
+ * and is what ScannInterface::SearchBatched (scann/scann_ops/cc/scann.cc:463-475)
+ * would call in place of scann_->FindNeighborsBatched.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Host buffers passed in are borrowed and
+ *    copied; device buffers are owned by the index handle.
+ *  - Every function returns SMX_OK (0) or a negative smx_status; the message
+ *    of the last failure on the calling thread is smx_last_error().  Nothing
+ *    throws across the ABI (the reference maps Status to RuntimeError at its
+ *    pybind layer, scann_npy.cc:41-55; the Python mirror does the same).
+ *  - Distances are returned in the reference's internal convention (smaller
+ *    is better; -dot for dot product).  The x(-1) of ReshapeBatchedNNResult
+ *    (scann/scann_ops/cc/scann.h:162-180) is applied by the caller.
+ *  - Calls on one handle may come from several host threads; they are
+ *    serialised on the handle's stream (re-entrant per the reference's
+ *    const FindNeighbors*Impl, SURVEY.md §8b "Threading").
+ *  - Device code targets gfx950 (MI355X) only.
+ */
+#ifndef SCANN_MI355X_H_
+#define SCANN_MI355X_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum smx_status {
+  SMX_OK = 0,
+  SMX_INVALID_ARGUMENT = -1,   /* InvalidArgumentError  */
+  SMX_FAILED_PRECONDITION = -2,/* FailedPreconditionError */
+  SMX_DEVICE_ERROR = -3,       /* HIP runtime failure   */
+  SMX_OUT_OF_MEMORY = -4,
+  SMX_INTERNAL = -5
+} smx_status;
+
+enum { SMX_METRIC_DOT = 0, SMX_METRIC_SQUARED_L2 = 1 };
+
+/* Index description.  Replaces the state TreeAHHybridResidual builds in
+ * BuildLeafSearchers (tree_ah_hybrid_residual.cc:325-495) / the assets
+ * ScannInterface::LoadArtifacts reads (scann.cc:105-264):
+ *   centers        <- the k-means tree leaf centers (serialized_partitioner.pb)
+ *   codebook       <- ah_codebook.pb, [num_blocks][16][dims_per_block]
+ *   leaf_offsets/leaf_members <- datapoints_by_token_ (ascending ids per leaf)
+ *   member_codes   <- hashed_dataset(.npy / _soar.npy), one row per member
+ *   dataset        <- dataset.npy (exact reordering), may be NULL
+ * A datapoint may be a member of several leaves (SOAR spilling); results are
+ * then de-duplicated as in DeduplicateDatabaseSpilledResults
+ * (tree_x_hybrid/internal/utils.cc:135-162). */
+typedef struct smx_index_desc {
+  int32_t metric;           /* SMX_METRIC_*                                   */
+  int32_t dim;
+  int32_t num_leaves;
+  int32_t num_blocks;       /* AH subspaces; LUT16 requires <= 64 here        */
+  int32_t dims_per_block;   /* last block covers dim-(num_blocks-1)*dpb dims  */
+  int32_t residual;         /* 1: residual tree-AH, global top-N (pipeline A) */
+  const float* centers;     /* [num_leaves][dim]                              */
+  const float* codebook;    /* [num_blocks][16][dims_per_block]               */
+  const uint64_t* leaf_offsets; /* [num_leaves+1]                             */
+  const uint32_t* leaf_members; /* [leaf_offsets[num_leaves]]                 */
+  const uint8_t* member_codes;  /* [members][num_blocks], values 0..15         */
+  uint32_t num_datapoints;
+  const float* dataset;     /* [num_datapoints][dim] or NULL                  */
+  float spilling_overretrieve_factor; /* tree_ah_hybrid_residual.h:320 (2.0) */
+  int32_t reserved;
+} smx_index_desc;
+
+typedef struct smx_index smx_index;
+
+/* Per-call search parameters.  Mirrors SearchParameters as produced by
+ * ScannInterface::GetSearchParametersBatched (scann.cc:406-430):
+ * leaves_to_search -> TreeXOptionalParameters::num_partitions_to_search_override,
+ * pre_reorder_nn / final_nn -> pre/post_reordering_num_neighbors.
+ * All three must be > 0 (defaults are resolved by the caller, as
+ * SetUnspecifiedParametersToDefaults does, single_machine_base.cc:120). */
+typedef struct smx_search_params {
+  int32_t leaves_to_search;
+  int32_t pre_reorder_nn;   /* ignored (= final_nn) when reorder is off       */
+  int32_t final_nn;
+  int32_t reorder;          /* 1: exact reorder with the float dataset        */
+} smx_search_params;
+
+/* Stage timings of the last search on a handle (ms, HIP events recorded on
+ * the handle's stream around each launch; filled only when profiling was
+ * enabled with smx_set_profiling). */
+typedef struct smx_timings {
+  float partition_ms;
+  float lut_ms;
+  float invert_ms;
+  float seed_scan_ms;
+  float seed_select_ms;
+  float scan_ms;            /* main LUT16 scan kernel                        */
+  float select_ms;          /* final top-k + SOAR dedupe + reorder + sort    */
+  float total_ms;
+  double scan_code_bytes;   /* algorithmic bytes of the main scan launch:
+                               sum over its (query, leaf) pairs of
+                               16 * num_blocks * ceil(leaf_size / 32)        */
+  double seed_code_bytes;
+  int32_t scan_pairs;       /* (query, leaf) pairs in the main launch        */
+  int32_t seed_pairs;
+  int32_t overflow_retries; /* candidate-buffer tightening passes            */
+  int32_t max_candidates;   /* largest per-query survivor count              */
+} smx_timings;
+
+/* Index lifecycle (ScannNumpy ctor / destructor; scann_npy.cc:57-77). */
+int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out);
+int smx_index_destroy(smx_index* index);
+int smx_index_info(const smx_index* index, int32_t* dim, int32_t* num_leaves,
+                   uint32_t* num_datapoints, int32_t* global_topn_shift);
+
+/* Batched search with host buffers (ScannNumpy::SearchBatched,
+ * scann_npy.cc:233-270).  queries: [nq][dim] float32 row-major (host).
+ * out_idx / out_dist: [nq][final_nn] (host), padded with id 0 / NaN as
+ * ReshapeBatchedNNResult does; out_count: [nq] (host, may be NULL). */
+int smx_search_batched(smx_index* index, const float* queries, int32_t nq,
+                       int32_t dim, const smx_search_params* params,
+                       uint32_t* out_idx, float* out_dist, int32_t* out_count);
+
+/* Same with device buffers, enqueued on `stream` (hipStream_t; NULL = the
+ * handle's own stream).  Synchronises only to check the candidate-buffer
+ * overflow flag.  d_out_count may be NULL. */
+int smx_search_batched_device(smx_index* index, const float* d_queries, int32_t nq,
+                              int32_t dim, const smx_search_params* params,
+                              uint32_t* d_out_idx, float* d_out_dist,
+                              int32_t* d_out_count, void* stream);
+
+/* ---- stage entry points (used by the parity tests; host buffers) ------- */
+
+/* Query tokenization: top-L leaves per query by partition distance, sorted by
+ * (distance, leaf id) — KMeansTreePartitioner::TokensForDatapointWithSpillingBatched
+ * (scann/partitioning/kmeans_tree_partitioner.cc:643-730) with the transposed
+ * many-to-many numerics (many_to_many_impl.inc:522-560).  [nq][L] outputs. */
+int smx_partition_topl(smx_index* index, const float* queries, int32_t nq,
+                       int32_t L, int32_t* out_leaf, float* out_dist);
+
+/* Per-query LUT16 tables — AsymmetricQueryer::CreateLookupTable
+ * (scann/hashes/asymmetric_hashing2/querying.h:284-329) +
+ * ConvertLookupToFixedPoint<uint8_t> (asymmetric_hashing_impl.cc:571-645).
+ * out_lut: [nq][num_blocks][16] uint8 (biased by 128); out_mult: [nq]. */
+int smx_create_lookup_tables(smx_index* index, const float* queries, int32_t nq,
+                             uint8_t* out_lut, float* out_mult);
+
+/* Pre-reorder candidates (global ids) — the NNResultsVector
+ * FindNeighborsBatchedNoSortNoExactReorder produces, sorted by (distance,
+ * id).  k' = pre_nn (x overretrieve factor before SOAR dedupe).
+ * Outputs [nq][pre_nn] padded with 0 / NaN. */
+int smx_search_pre_reorder(smx_index* index, const float* queries, int32_t nq,
+                           int32_t leaves, int32_t pre_nn, uint32_t* out_idx,
+                           float* out_dist, int32_t* out_count);
+
+/* Exact distances of given rows (the reorder kernel alone;
+ * one_to_many_symmetric.h:373-503).  ids: [nq][k]; out [nq][k]. */
+int smx_exact_distances(smx_index* index, const float* queries, int32_t nq,
+                        const uint32_t* ids, int32_t k, float* out_dist);
+
+/* Raw LUT16 accumulation on one leaf: Sum_b (lut[b][code]-128) for every
+ * member of `leaf` against one uint8 LUT [num_blocks][16] — the integer core
+ * of LUT16Avx2::GetTopFloatDistances (lut16_avx2.inc:55-124).  out: [leaf size]. */
+int smx_lut16_leaf_scores(smx_index* index, int32_t leaf, const uint8_t* lut,
+                          int32_t* out_scores);
+
+/* ---- diagnostics ---------------------------------------------------------- */
+int smx_set_profiling(smx_index* index, int32_t enabled);
+int smx_get_timings(const smx_index* index, smx_timings* out);
+/* Candidate buffer capacity per query and seed leaves (tuning knobs). */
+int smx_set_tuning(smx_index* index, int32_t candidates_per_query, int32_t seed_leaves);
+
+const char* smx_last_error(void);
+const char* smx_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SCANN_MI355X_H_ */

@@ -1,0 +1,126 @@
+// lut16_avx2_port.cc — AVX2 port of the reference's batched tree-AH query
+// path, used ONLY as bench.py's cpu_baseline ("kind": "port").
+//
+// TEST INFRASTRUCTURE (see scann_oracle.h).  Semantics equal
+// orc_search(..., ORC_MODE_EMULATE, ...) exactly; the difference is the
+// execution strategy, which mirrors the reference:
+//   * SearchBatchedParallel chunking over a thread pool (scann.cc:478-501);
+//   * per chunk: partition top-L, per-query LUTs, queries inverted by leaf,
+//     leaves visited in leaf_tokens_by_norm_ order, batches of <=3 queries
+//     per LUT16 call (tree_ah_hybrid_residual.cc:631-786);
+//   * the LUT16 inner loop as pshufb lookups over the reference packed layout
+//     with 16-bit accumulation (lut16_avx2.inc:55-124, 403-526).
+// Partition scoring and LUT construction reuse the scalar restatement's
+// numerics (same translation unit family, compiled -ffp-contract=off).
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <numeric>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "scann_oracle.h"
+
+#if defined(__AVX2__)
+#include <immintrin.h>
+
+namespace {
+
+// 32 exact int16 accumulators for one 32-datapoint group of the reference
+// packed layout (16*nb bytes) and one LUT (u8 [nb][16]).
+inline void Lut16Group(const uint8_t* group, int nb, const uint8_t* lut,
+                       int16_t out[32]) {
+  const __m256i low4 = _mm256_set1_epi8(0x0F);
+  const __m256i lowbyte = _mm256_set1_epi16(0x00FF);
+  __m256i e0 = _mm256_setzero_si256(), o0 = e0, e1 = e0, o1 = e0;
+  int b = 0;
+  for (; b + 2 <= nb; b += 2) {
+    const __m256i codes = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(group + b * 16));
+    const __m256i lo = _mm256_and_si256(codes, low4);
+    const __m256i hi = _mm256_and_si256(_mm256_srli_epi16(codes, 4), low4);
+    const __m256i tbl = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(lut + b * 16));
+    const __m256i r0 = _mm256_shuffle_epi8(tbl, lo);
+    const __m256i r1 = _mm256_shuffle_epi8(tbl, hi);
+    e0 = _mm256_add_epi16(e0, _mm256_and_si256(r0, lowbyte));
+    o0 = _mm256_add_epi16(o0, _mm256_srli_epi16(r0, 8));
+    e1 = _mm256_add_epi16(e1, _mm256_and_si256(r1, lowbyte));
+    o1 = _mm256_add_epi16(o1, _mm256_srli_epi16(r1, 8));
+  }
+  // Fold the two 128-bit lanes (blocks b and b+1 of each pair).
+  __m128i E0 = _mm_add_epi16(_mm256_castsi256_si128(e0), _mm256_extracti128_si256(e0, 1));
+  __m128i O0 = _mm_add_epi16(_mm256_castsi256_si128(o0), _mm256_extracti128_si256(o0, 1));
+  __m128i E1 = _mm_add_epi16(_mm256_castsi256_si128(e1), _mm256_extracti128_si256(e1, 1));
+  __m128i O1 = _mm_add_epi16(_mm256_castsi256_si128(o1), _mm256_extracti128_si256(o1, 1));
+  __m128i d0 = _mm_unpacklo_epi16(E0, O0);  // dps 0..7
+  __m128i d1 = _mm_unpackhi_epi16(E0, O0);  // dps 8..15
+  __m128i d2 = _mm_unpacklo_epi16(E1, O1);  // dps 16..23
+  __m128i d3 = _mm_unpackhi_epi16(E1, O1);  // dps 24..31
+  if (b < nb) {  // odd trailing block (lut16_avx2.inc:102-116)
+    const __m128i codes = _mm_loadu_si128(reinterpret_cast<const __m128i*>(group + b * 16));
+    const __m128i l4 = _mm_set1_epi8(0x0F);
+    const __m128i lo = _mm_and_si128(codes, l4);
+    const __m128i hi = _mm_and_si128(_mm_srli_epi16(codes, 4), l4);
+    const __m128i tbl = _mm_loadu_si128(reinterpret_cast<const __m128i*>(lut + b * 16));
+    const __m128i v0 = _mm_shuffle_epi8(tbl, lo);
+    const __m128i v1 = _mm_shuffle_epi8(tbl, hi);
+    const __m128i z = _mm_setzero_si128();
+    d0 = _mm_add_epi16(d0, _mm_unpacklo_epi8(v0, z));
+    d1 = _mm_add_epi16(d1, _mm_unpackhi_epi8(v0, z));
+    d2 = _mm_add_epi16(d2, _mm_unpacklo_epi8(v1, z));
+    d3 = _mm_add_epi16(d3, _mm_unpackhi_epi8(v1, z));
+  }
+  const __m128i bias = _mm_set1_epi16(int16_t(nb * 128));
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(out + 0), _mm_sub_epi16(d0, bias));
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(out + 8), _mm_sub_epi16(d1, bias));
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(out + 16), _mm_sub_epi16(d2, bias));
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(out + 24), _mm_sub_epi16(d3, bias));
+}
+
+inline uint32_t PushMask(const int16_t acc[32], int16_t thr) {
+  const __m256i t = _mm256_set1_epi16(thr);
+  const __m256i a0 = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(acc));
+  const __m256i a1 = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(acc + 16));
+  const __m256i c0 = _mm256_cmpgt_epi16(t, a0);
+  const __m256i c1 = _mm256_cmpgt_epi16(t, a1);
+  const __m256i packed = _mm256_permute4x64_epi64(_mm256_packs_epi16(c0, c1), 0xD8);
+  return uint32_t(_mm256_movemask_epi8(packed));
+}
+
+}  // namespace
+#endif  // __AVX2__
+
+// Driver shared with the scalar restatement (defined in scann_oracle.cc so it
+// reuses the same partition / LUT / FastTopNeighbors code).
+namespace orc_port {
+using GroupFn = void (*)(const uint8_t*, int, const uint8_t*, int16_t*);
+using MaskFn = uint32_t (*)(const int16_t*, int16_t);
+void* Prepare(const orc_index* ix);
+void Release(void* p);
+int Run(void* prepared, const float* queries, int nq, int leaves, int pre_nn,
+        int final_nn, int do_reorder, int nthreads, uint32_t* out_idx,
+        float* out_dist, int32_t* out_count, GroupFn group_fn, MaskFn mask_fn);
+}  // namespace orc_port
+
+extern "C" {
+void* orc_avx2_prepare(const orc_index* idx) { return orc_port::Prepare(idx); }
+void orc_avx2_release(void* p) { orc_port::Release(p); }
+int orc_search_avx2(void* prepared, const float* queries, int32_t nq,
+                    int32_t leaves, int32_t pre_nn, int32_t final_nn,
+                    int32_t do_reorder, int32_t nthreads, uint32_t* out_idx,
+                    float* out_dist, int32_t* out_count) {
+#if defined(__AVX2__)
+  return orc_port::Run(prepared, queries, nq, leaves, pre_nn, final_nn,
+                       do_reorder, nthreads, out_idx, out_dist, out_count,
+                       &Lut16Group, &PushMask);
+#else
+  (void)prepared; (void)queries; (void)nq; (void)leaves; (void)pre_nn;
+  (void)final_nn; (void)do_reorder; (void)nthreads; (void)out_idx;
+  (void)out_dist; (void)out_count;
+  return -2;
+#endif
+}
+}  // extern "C"

@@ -1,0 +1,204 @@
+"""ctypes binding of libscann_mi355x.so (include/scann_mi355x.h).
+
+This is the reference-side binding a maintainer would add in place of the
+``scann_pybind`` extension (scann/scann_ops/cc/python/scann_pybind.cc).
+There is no CPU fallback: if the library is missing or fails to load, import
+raises, and every search runs the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .index import IndexDesc
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libscann_mi355x.so")
+
+SMX_OK = 0
+
+
+class SearchParams(ctypes.Structure):
+    _fields_ = [("leaves_to_search", ctypes.c_int32), ("pre_reorder_nn", ctypes.c_int32),
+                ("final_nn", ctypes.c_int32), ("reorder", ctypes.c_int32)]
+
+
+class Timings(ctypes.Structure):
+    _fields_ = [("partition_ms", ctypes.c_float), ("lut_ms", ctypes.c_float),
+                ("invert_ms", ctypes.c_float), ("seed_scan_ms", ctypes.c_float),
+                ("seed_select_ms", ctypes.c_float), ("scan_ms", ctypes.c_float),
+                ("select_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
+                ("scan_code_bytes", ctypes.c_double), ("seed_code_bytes", ctypes.c_double),
+                ("scan_pairs", ctypes.c_int32), ("seed_pairs", ctypes.c_int32),
+                ("overflow_retries", ctypes.c_int32), ("max_candidates", ctypes.c_int32)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+# name -> (restype, argtypes); must cover every function of include/scann_mi355x.h
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+SIGNATURES = {
+    "smx_index_create": (ctypes.c_int, [ctypes.POINTER(IndexDesc), _i32, ctypes.POINTER(_vp)]),
+    "smx_index_destroy": (ctypes.c_int, [_vp]),
+    "smx_index_info": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "smx_search_batched": (ctypes.c_int, [_vp, _vp, _i32, _i32, ctypes.POINTER(SearchParams), _vp, _vp, _vp]),
+    "smx_search_batched_device": (ctypes.c_int, [_vp, _vp, _i32, _i32, ctypes.POINTER(SearchParams), _vp, _vp, _vp, _vp]),
+    "smx_partition_topl": (ctypes.c_int, [_vp, _vp, _i32, _i32, _vp, _vp]),
+    "smx_create_lookup_tables": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp]),
+    "smx_search_pre_reorder": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp]),
+    "smx_exact_distances": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp]),
+    "smx_lut16_leaf_scores": (ctypes.c_int, [_vp, _i32, _vp, _vp]),
+    "smx_set_profiling": (ctypes.c_int, [_vp, _i32]),
+    "smx_get_timings": (ctypes.c_int, [_vp, ctypes.POINTER(Timings)]),
+    "smx_set_tuning": (ctypes.c_int, [_vp, _i32, _i32]),
+    "smx_last_error": (ctypes.c_char_p, []),
+    "smx_version": (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load the HIP library; raises ImportError (loudly) if it is unusable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (the MI355X search path has no CPU fallback)")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class SmxError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str) -> None:
+    if rc != SMX_OK:
+        msg = load().smx_last_error().decode(errors="replace")
+        raise SmxError(f"{what}: {msg} (status {rc})")
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+class NativeIndex:
+    """Owns one smx_index handle (device-resident index)."""
+
+    def __init__(self, index, device: int = 0):
+        self.lib = load()
+        self.index = index
+        self.dim = index.dim
+        desc = index.desc()
+        h = _vp()
+        check(self.lib.smx_index_create(ctypes.byref(desc), device, ctypes.byref(h)),
+              "smx_index_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.lib.smx_index_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self):
+        d, l, s = _i32(), _i32(), _i32()
+        n = ctypes.c_uint32()
+        check(self.lib.smx_index_info(self.h, ctypes.byref(d), ctypes.byref(l), ctypes.byref(n),
+                                      ctypes.byref(s)), "smx_index_info")
+        return dict(dim=d.value, num_leaves=l.value, num_datapoints=n.value,
+                    global_topn_shift=s.value)
+
+    def search_batched(self, queries, leaves, pre_nn, final_nn, reorder=True):
+        q = _c(queries, np.float32)
+        if q.ndim != 2:
+            raise ValueError("Queries must be in two-dimensional array")
+        nq = q.shape[0]
+        p = SearchParams(int(leaves), int(pre_nn), int(final_nn), int(bool(reorder)))
+        idx = np.zeros((nq, final_nn), np.uint32)
+        dist = np.zeros((nq, final_nn), np.float32)
+        cnt = np.zeros(nq, np.int32)
+        check(self.lib.smx_search_batched(self.h, q.ctypes.data, nq, q.shape[1], ctypes.byref(p),
+                                          idx.ctypes.data, dist.ctypes.data, cnt.ctypes.data),
+              "Error during search")
+        return idx, dist, cnt
+
+    def search_batched_device(self, q_ptr, nq, leaves, pre_nn, final_nn, reorder,
+                              out_idx_ptr, out_dist_ptr, out_count_ptr=None, stream=None):
+        p = SearchParams(int(leaves), int(pre_nn), int(final_nn), int(bool(reorder)))
+        check(self.lib.smx_search_batched_device(self.h, q_ptr, nq, self.dim, ctypes.byref(p),
+                                                 out_idx_ptr, out_dist_ptr, out_count_ptr, stream),
+              "Error during search")
+
+    def search_pre_reorder(self, queries, leaves, pre_nn):
+        q = _c(queries, np.float32)
+        nq = q.shape[0]
+        idx = np.zeros((nq, pre_nn), np.uint32)
+        dist = np.zeros((nq, pre_nn), np.float32)
+        cnt = np.zeros(nq, np.int32)
+        check(self.lib.smx_search_pre_reorder(self.h, q.ctypes.data, nq, leaves, pre_nn,
+                                              idx.ctypes.data, dist.ctypes.data, cnt.ctypes.data),
+              "smx_search_pre_reorder")
+        return idx, dist, cnt
+
+    def partition_topl(self, queries, L):
+        q = _c(queries, np.float32)
+        leaf = np.zeros((q.shape[0], L), np.int32)
+        dist = np.zeros((q.shape[0], L), np.float32)
+        check(self.lib.smx_partition_topl(self.h, q.ctypes.data, q.shape[0], L, leaf.ctypes.data,
+                                          dist.ctypes.data), "smx_partition_topl")
+        return leaf, dist
+
+    def create_lookup_tables(self, queries):
+        q = _c(queries, np.float32)
+        nb = self.index.num_blocks
+        lut = np.zeros((q.shape[0], nb, 16), np.uint8)
+        mult = np.zeros(q.shape[0], np.float32)
+        check(self.lib.smx_create_lookup_tables(self.h, q.ctypes.data, q.shape[0], lut.ctypes.data,
+                                                mult.ctypes.data), "smx_create_lookup_tables")
+        return lut, mult
+
+    def exact_distances(self, queries, ids):
+        q = _c(queries, np.float32)
+        ids = _c(ids, np.uint32)
+        out = np.zeros(ids.shape, np.float32)
+        check(self.lib.smx_exact_distances(self.h, q.ctypes.data, q.shape[0], ids.ctypes.data,
+                                           ids.shape[1], out.ctypes.data), "smx_exact_distances")
+        return out
+
+    def leaf_scores(self, leaf, lut_u8):
+        lut_u8 = _c(lut_u8, np.uint8)
+        n = int(self.index.leaf_offsets[leaf + 1] - self.index.leaf_offsets[leaf])
+        out = np.zeros(max(n, 1), np.int32)
+        check(self.lib.smx_lut16_leaf_scores(self.h, int(leaf), lut_u8.ctypes.data, out.ctypes.data),
+              "smx_lut16_leaf_scores")
+        return out[:n]
+
+    def set_profiling(self, on: bool):
+        check(self.lib.smx_set_profiling(self.h, int(bool(on))), "smx_set_profiling")
+
+    def timings(self):
+        t = Timings()
+        check(self.lib.smx_get_timings(self.h, ctypes.byref(t)), "smx_get_timings")
+        return t.as_dict()
+
+    def set_tuning(self, candidates_per_query: int, seed_leaves: int):
+        check(self.lib.smx_set_tuning(self.h, int(candidates_per_query), int(seed_leaves)),
+              "smx_set_tuning")

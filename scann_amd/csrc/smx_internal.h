@@ -1,0 +1,124 @@
+// smx_internal.h — device-side index layout, kernel argument blocks and the
+// launcher entry points shared by smx_kernels.hip and smx_searcher.hip.
+#ifndef SMX_INTERNAL_H_
+#define SMX_INTERNAL_H_
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace smx {
+
+// Query-tile width of the LUT16 scan: one MFMA i32_32x32x32_i8 covers 32
+// datapoints x 32 queries x 2 AH blocks.
+constexpr int kQueriesPerTile = 32;
+constexpr int kDpPerTile = 32;
+constexpr int kMaxBlocks = 64;           // LUT16 blocks supported (K <= 32)
+constexpr uint64_t kNoThreshold = ~0ull;
+
+// Bytes of code data one lane holds per 32-datapoint tile: lane (r, h) keeps
+// the nibbles of datapoint r for blocks h, h+2, h+4, ... (K = ceil(B/2)).
+inline int LaneBytes(int ksteps) { return 4 * ((((ksteps + 1) / 2) + 3) / 4); }
+
+// Index resident in HBM (owned by the handle).
+struct DeviceIndex {
+  int metric = 0, dim = 0, nl = 0, nb = 0, dpb = 0, residual = 0;
+  int ksteps = 0;        // ceil(nb / 2)
+  int lane_bytes = 0;    // LaneBytes(ksteps)
+  int shift = 0;         // global top-N shift, 0 = tie by global id
+  uint32_t num_datapoints = 0;
+  uint64_t num_members = 0;
+  uint64_t num_tiles = 0;
+  uint32_t max_leaf = 0;
+  bool disjoint = true;
+  float spill = 2.0f;
+  float* centers = nullptr;     // [nl][dim]
+  float* centers_t = nullptr;   // [dim][nl]
+  float* cnorm = nullptr;       // [nl], squared L2 only
+  float* codebook = nullptr;    // [nb][16][dpb]
+  uint8_t* tiles = nullptr;     // [num_tiles][64 lanes][lane_bytes]
+  uint64_t* tile_off = nullptr; // [nl+1]
+  uint32_t* leaf_size = nullptr;// [nl]
+  uint64_t* member_off = nullptr; // [nl+1]
+  uint32_t* members = nullptr;  // [num_members]
+  float* dataset = nullptr;     // [num_datapoints][dim] or null
+};
+
+struct ScanArgs {
+  const uint8_t* tiles;
+  const uint64_t* tile_off;
+  const uint32_t* leaf_size;
+  const uint64_t* member_off;
+  const uint32_t* members;
+  const int8_t* lut;          // [nq][2K][16]
+  const float* inv;           // [nq]
+  const uint32_t* pair_q;     // queries grouped by leaf
+  const float* pair_bias;     // partition distance per pair (residual)
+  const uint32_t* pair_off;   // [nl+1]
+  const uint32_t* tile_prefix;// [nl+1] query tiles per leaf, prefix
+  const uint32_t* tile_leaf;  // [work items] leaf of each query tile
+  const uint64_t* tau_key;    // [nq] emission threshold, or null (emit all)
+  uint64_t* cand;             // [nq][cap]
+  uint32_t* cand_count;       // [nq]
+  uint32_t* work_counter;
+  uint32_t cap;
+  int nl;
+  int nb;
+  int shift;
+  int residual;
+};
+
+struct SelectArgs {
+  const uint64_t* cand;
+  const uint32_t* cand_count;
+  uint32_t cap;
+  int kk;                     // k' kept before dedupe
+  int pre_nn;                 // kept after SOAR dedupe
+  int final_nn;
+  int reorder;
+  int disjoint;
+  int pre_only;               // output the pre-reorder set (stage entry)
+  int shift;
+  int metric;
+  int dim;
+  const uint64_t* member_off;
+  const uint32_t* members;
+  const float* dataset;
+  const float* queries;
+  uint32_t* out_idx;
+  float* out_dist;
+  int32_t* out_count;
+  int out_width;
+  uint32_t* overflow;         // [2]: flag, max count
+};
+
+// ---- launchers (smx_kernels.hip) ------------------------------------------
+hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int nq,
+                               int L, int32_t* out_leaf, float* out_dist,
+                               hipStream_t s);
+hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq,
+                          int8_t* lut, float* mult, float* inv, uint8_t* lut_u8,
+                          hipStream_t s);
+hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf,
+                       const float* topl_dist, int nq, int L, int seed_leaves,
+                       uint32_t* cnt /*[2][nl]*/, uint32_t* fill /*[2][nl]*/,
+                       uint32_t* pair_off /*[2][nl+1]*/,
+                       uint32_t* tile_prefix /*[2][nl+1]*/,
+                       uint32_t* pair_q /*[2][nq*L]*/, float* pair_bias /*[2][nq*L]*/,
+                       uint32_t* tile_leaf /*[2][max_items]*/, uint32_t max_items,
+                       unsigned long long* code_bytes /*[2]*/, hipStream_t s);
+hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, hipStream_t s);
+hipError_t LaunchSeedSelect(const uint64_t* seed_cand, const uint32_t* seed_count,
+                            uint32_t seed_cap, int nq, int kk, uint64_t* tau_key,
+                            hipStream_t s);
+hipError_t LaunchTighten(const uint64_t* cand, const uint32_t* cand_count, uint32_t cap,
+                         int nq, int kk, uint64_t* tau_key, hipStream_t s);
+hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s);
+hipError_t LaunchExactDistances(const DeviceIndex& ix, const float* queries, int nq,
+                                const uint32_t* ids, int k, float* out, hipStream_t s);
+hipError_t LaunchLeafScores(const DeviceIndex& ix, int leaf, const int8_t* lut,
+                            int32_t* out, hipStream_t s);
+hipError_t LaunchFill64(uint64_t* p, uint64_t v, size_t n, hipStream_t s);
+
+}  // namespace smx
+
+#endif  // SMX_INTERNAL_H_

@@ -1,0 +1,796 @@
+// smx_kernels.hip — HIP kernels (gfx950 / CDNA4) of the tree-AH LUT16 query
+// path.  Every float operation whose rounding the reference fixes is spelled
+// with an explicit round-to-nearest intrinsic; the library is also built with
+// -ffp-contract=off.
+//
+//   partition_topl_kernel   query tokenization: per-query FMA chains over all
+//                           leaf centers (many_to_many_impl.inc:522-560) and an
+//                           exact top-L by (distance, leaf) in LDS
+//                           (kmeans_tree_partitioner.cc:703-728)
+//   lut_build_kernel        raw float LUT + uint8 fixed point
+//                           (asymmetric_hashing_impl.cc:505-645)
+//   pairs_* kernels         InvertCentersToSearch on the GPU
+//                           (tree_ah_hybrid_residual.cc:610-622)
+//   lut16_scan_kernel<K>    THE hot loop (lut16_avx2.inc:403-526): LUT16 sums
+//                           on MFMA i32_32x32x32_i8 (one-hot codes x int8 LUT),
+//                           fused distance + threshold + candidate emission
+//   seed/tighten/final      exact top-k by the reference's total order
+//                           (fast_top_neighbors.h:175-228), SOAR dedupe
+//                           (internal/utils.cc:135-162), exact reorder
+//                           (one_to_many_symmetric.h:373-503) and SortAndDrop
+//                           (single_machine_base.cc:872-901)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "smx_internal.h"
+
+namespace smx {
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+// sqrtf(FLT_EPSILON) as the reference computes it on the host
+// (asymmetric_hashing_impl.cc:575): 3.4526698e-04f.
+__device__ __forceinline__ float SqrtFltEps() { return __uint_as_float(0x39b504f3u); }
+
+// Order-preserving map float -> uint32 (total order of the reference's
+// comparator for non-NaN values; -0 canonicalised to +0 first).
+__device__ __forceinline__ uint32_t OrderedBits(float f) {
+  f = __fadd_rn(f, 0.0f);
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float FromOrdered(uint32_t o) {
+  const uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+  return __uint_as_float(u);
+}
+
+__device__ __forceinline__ uint32_t NextPow2(uint32_t x) {
+  return x <= 1 ? 1u : 1u << (32 - __clz(x - 1));
+}
+
+// Block-wide bitonic sort (ascending) of n (power of two) keys in LDS.
+__device__ void BitonicSort(uint64_t* keys, uint32_t n) {
+  for (uint32_t k = 2; k <= n; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t a = keys[i], b = keys[ixj];
+          const bool up = (i & k) == 0;
+          if ((a > b) == up) {
+            keys[i] = b;
+            keys[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Query tokenization.
+// Dot: acc <- fma(-q_d, c_d, acc) from 0, d ascending.
+// Squared L2: acc starts at ||c||^2 + ||q||^2, then acc <- fma(-q_d, 2c_d, acc);
+// ||q||^2 accumulated in double, sequentially (thread 0).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) partition_topl_kernel(
+    const float* __restrict__ queries, int dim, const float* __restrict__ centers_t,
+    const float* __restrict__ cnorm, int nl, int metric, int L, uint32_t npow2,
+    int32_t* __restrict__ out_leaf, float* __restrict__ out_dist) {
+  extern __shared__ uint64_t lds64[];
+  uint64_t* keys = lds64;
+  float* q = reinterpret_cast<float*>(lds64 + npow2);
+  const int qi = blockIdx.x;
+  const float* qg = queries + size_t(qi) * dim;
+  for (int d = threadIdx.x; d < dim; d += blockDim.x) q[d] = qg[d];
+  __shared__ float qnorm;
+  __syncthreads();
+  if (metric == 1 && threadIdx.x == 0) {
+    double acc = 0.0;
+    for (int d = 0; d < dim; ++d) acc += double(q[d]) * double(q[d]);
+    qnorm = float(acc);
+  }
+  __syncthreads();
+  for (uint32_t c = threadIdx.x; c < npow2; c += blockDim.x) {
+    uint64_t key = ~0ull;
+    if (c < uint32_t(nl)) {
+      float acc;
+      if (metric == 0) {
+        acc = 0.0f;
+        for (int d = 0; d < dim; ++d) acc = __fmaf_rn(-q[d], centers_t[size_t(d) * nl + c], acc);
+      } else {
+        acc = __fadd_rn(cnorm[c], qnorm);
+        for (int d = 0; d < dim; ++d)
+          acc = __fmaf_rn(-q[d], __fmul_rn(centers_t[size_t(d) * nl + c], 2.0f), acc);
+      }
+      key = (uint64_t(OrderedBits(acc)) << 32) | c;
+    }
+    keys[c] = key;
+  }
+  __syncthreads();
+  BitonicSort(keys, npow2);
+  const int Lc = L < nl ? L : nl;
+  for (int i = threadIdx.x; i < L; i += blockDim.x) {
+    const bool has = i < Lc;
+    out_leaf[size_t(qi) * L + i] = has ? int32_t(keys[i] & 0xFFFFFFFFu) : -1;
+    out_dist[size_t(qi) * L + i] = has ? FromOrdered(uint32_t(keys[i] >> 32)) : __int_as_float(0x7fc00000);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LUT build: raw[b][c] = -(fl(q0*c0) + fl(q1*c1)) (dot) or
+// fl(t0*t0) + fl(t1*t1), t = q - c (squared L2); multiplier
+// 127 / max(sqrt(FLT_EPSILON), max|raw|); int8 = round(raw * m) (the uint8
+// table minus its bias 128); inv = (float)(1.0/(double)m) for residual
+// indexes (lut16_avx2.inc:427-430), 1.0f/m otherwise (querying.h:450-454).
+// LUT rows are padded to 2*K blocks with zeros.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) lut_build_kernel(
+    const float* __restrict__ queries, int dim, const float* __restrict__ codebook,
+    int nb, int dpb, int padded_blocks, int metric, int residual,
+    int8_t* __restrict__ lut, float* __restrict__ mult, float* __restrict__ inv,
+    uint8_t* __restrict__ lut_u8) {
+  __shared__ float raw[kMaxBlocks * 16];
+  __shared__ float red[256];
+  const int qi = blockIdx.x;
+  const float* q = queries + size_t(qi) * dim;
+  const int nent = nb * 16;
+  const int last = dim - dpb * (nb - 1);
+  float local_max = 0.0f;
+  for (int e = threadIdx.x; e < nent; e += blockDim.x) {
+    const int b = e >> 4, c = e & 15;
+    const int nd = (b == nb - 1) ? last : dpb;
+    const float* qb = q + size_t(b) * dpb;
+    const float* cb = codebook + (size_t(b) * 16 + c) * dpb;
+    float v;
+    if (metric == 0) {
+      float s = __fmul_rn(qb[0], cb[0]);
+      for (int i = 1; i < nd; ++i) s = __fadd_rn(s, __fmul_rn(qb[i], cb[i]));
+      v = -s;
+    } else {
+      float t = __fsub_rn(qb[0], cb[0]);
+      float s = __fmul_rn(t, t);
+      for (int i = 1; i < nd; ++i) {
+        const float u = __fsub_rn(qb[i], cb[i]);
+        s = __fadd_rn(s, __fmul_rn(u, u));
+      }
+      v = s;
+    }
+    raw[e] = v;
+    local_max = fmaxf(local_max, fabsf(v));
+  }
+  red[threadIdx.x] = local_max;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  const float m = __fdiv_rn(127.0f, fmaxf(SqrtFltEps(), red[0]));
+  const int tot = padded_blocks * 16;
+  for (int e = threadIdx.x; e < tot; e += blockDim.x) {
+    int8_t v8 = 0;
+    if (e < nent) {
+      const float r = roundf(__fmul_rn(raw[e], m));
+      v8 = int8_t(int(r));
+      if (lut_u8) lut_u8[size_t(qi) * nent + e] = uint8_t(int(r) + 128);
+    }
+    lut[size_t(qi) * tot + e] = v8;
+  }
+  if (threadIdx.x == 0) {
+    mult[qi] = m;
+    inv[qi] = residual ? float(1.0 / double(m)) : __fdiv_rn(1.0f, m);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Invert (query -> leaves) into (leaf -> queries), split into the seed set
+// (rank < seed_leaves) and the main set.
+// ---------------------------------------------------------------------------
+__global__ void pairs_count_kernel(const int32_t* __restrict__ topl_leaf, int nq, int L,
+                                   int seed_leaves, int nl, uint32_t* __restrict__ cnt,
+                                   const uint32_t* __restrict__ leaf_size, int nb,
+                                   unsigned long long* __restrict__ code_bytes) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq * L) return;
+  const int leaf = topl_leaf[i];
+  if (leaf < 0) return;
+  const unsigned long long bytes = 16ull * nb * ((leaf_size[leaf] + 31u) / 32u);
+  atomicAdd(&cnt[nl + leaf], 1u);           // main set: every pair
+  atomicAdd(&code_bytes[1], bytes);
+  if ((i % L) < seed_leaves) {              // seed set: the first ranks
+    atomicAdd(&cnt[leaf], 1u);
+    atomicAdd(&code_bytes[0], bytes);
+  }
+}
+
+__global__ void __launch_bounds__(1024) pairs_scan_kernel(const uint32_t* __restrict__ cnt,
+                                                          int nl, uint32_t* __restrict__ pair_off,
+                                                          uint32_t* __restrict__ tile_prefix) {
+  __shared__ uint32_t s_pairs[1024];
+  __shared__ uint32_t s_tiles[1024];
+  const int set = blockIdx.x;
+  const uint32_t* c = cnt + size_t(set) * nl;
+  uint32_t* po = pair_off + size_t(set) * (nl + 1);
+  uint32_t* tp = tile_prefix + size_t(set) * (nl + 1);
+  const int per = (nl + blockDim.x - 1) / blockDim.x;
+  const int beg = threadIdx.x * per;
+  const int end = min(nl, beg + per);
+  uint32_t sp = 0, st = 0;
+  for (int l = beg; l < end; ++l) {
+    sp += c[l];
+    st += (c[l] + kQueriesPerTile - 1) / kQueriesPerTile;
+  }
+  s_pairs[threadIdx.x] = sp;
+  s_tiles[threadIdx.x] = st;
+  __syncthreads();
+  // Hillis-Steele inclusive scan over 1024 partial sums.
+  for (int off = 1; off < int(blockDim.x); off <<= 1) {
+    uint32_t a = 0, b = 0;
+    if (int(threadIdx.x) >= off) {
+      a = s_pairs[threadIdx.x - off];
+      b = s_tiles[threadIdx.x - off];
+    }
+    __syncthreads();
+    s_pairs[threadIdx.x] += a;
+    s_tiles[threadIdx.x] += b;
+    __syncthreads();
+  }
+  uint32_t rp = threadIdx.x ? s_pairs[threadIdx.x - 1] : 0;
+  uint32_t rt = threadIdx.x ? s_tiles[threadIdx.x - 1] : 0;
+  for (int l = beg; l < end; ++l) {
+    po[l] = rp;
+    tp[l] = rt;
+    rp += c[l];
+    rt += (c[l] + kQueriesPerTile - 1) / kQueriesPerTile;
+  }
+  if (threadIdx.x == blockDim.x - 1) {
+    po[nl] = s_pairs[blockDim.x - 1];
+    tp[nl] = s_tiles[blockDim.x - 1];
+  }
+}
+
+__global__ void pairs_scatter_kernel(const int32_t* __restrict__ topl_leaf,
+                                     const float* __restrict__ topl_dist, int nq, int L,
+                                     int seed_leaves, int nl, const uint32_t* __restrict__ pair_off,
+                                     uint32_t* __restrict__ fill, uint32_t* __restrict__ pair_q,
+                                     float* __restrict__ pair_bias) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq * L) return;
+  const int leaf = topl_leaf[i];
+  if (leaf < 0) return;
+  const int nsets = (i % L) < seed_leaves ? 2 : 1;
+  for (int k = 0; k < nsets; ++k) {
+    const int set = 1 - k;  // main first, then seed
+    const uint32_t pos = pair_off[size_t(set) * (nl + 1) + leaf] +
+                         atomicAdd(&fill[set * nl + leaf], 1u);
+    const size_t base = size_t(set) * nq * L;
+    pair_q[base + pos] = uint32_t(i / L);
+    pair_bias[base + pos] = topl_dist[i];
+  }
+}
+
+// Work item (query tile) -> leaf map for both sets.
+__global__ void pairs_tiles_kernel(const uint32_t* __restrict__ tile_prefix, int nl,
+                                   uint32_t* __restrict__ tile_leaf, uint32_t max_items) {
+  const int set = blockIdx.y;
+  const int leaf = blockIdx.x * blockDim.x + threadIdx.x;
+  if (leaf >= nl) return;
+  const uint32_t* tp = tile_prefix + size_t(set) * (nl + 1);
+  uint32_t* tl = tile_leaf + size_t(set) * max_items;
+  for (uint32_t t = tp[leaf]; t < tp[leaf + 1]; ++t) tl[t] = uint32_t(leaf);
+}
+
+// ---------------------------------------------------------------------------
+// LUT16 scan on MFMA.
+//
+// One wave owns a work item = (leaf, 32 queries of that leaf).  For every
+// 32-datapoint tile of the leaf it computes the 32x32 matrix of LUT16 sums
+//     S[dp][q] = sum_b int8LUT_q[b][code(dp, b)]
+// as K = ceil(B/2) MFMA i32_32x32x32_i8 steps: A = one-hot codes (row = dp,
+// 16 bytes per lane-half = one block's 16 centers), B = the queries' int8
+// LUT rows (held in VGPRs for the whole leaf).  The i32 sums are exact
+// (|S| <= 127*B).  Lane (c, h) of the accumulator holds 16 datapoints of
+// query c, so the epilogue converts, thresholds and emits per lane:
+//     d = fl(fl(float(S) * inv_q) + bias_{q,leaf})
+// and appends (ordered(d) << 32 | tie) to the query's candidate list when
+// (d, tie) <= the query's threshold key.  Only S <= amax (the largest sum
+// whose distance can pass, found by bisection: d is monotone in S) is
+// converted.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ v4i OneHot16(uint32_t t) {
+  const uint32_t one = 1u << ((t & 3u) << 3);
+  const uint32_t g = t >> 2;
+  v4i r;
+  r[0] = g == 0 ? int(one) : 0;
+  r[1] = g == 1 ? int(one) : 0;
+  r[2] = g == 2 ? int(one) : 0;
+  r[3] = g == 3 ? int(one) : 0;
+  return r;
+}
+
+__device__ __forceinline__ float DistOf(int s, float inv, float bias) {
+  return __fadd_rn(__fmul_rn(float(s), inv), bias);
+}
+
+// Largest sum in [lo, hi] whose distance is <= td (lo - 1 if none).
+__device__ int SumLimit(float td, float inv, float bias, int lo, int hi) {
+  if (!(DistOf(lo, inv, bias) <= td)) return lo - 1;
+  if (DistOf(hi, inv, bias) <= td) return hi;
+  while (hi - lo > 1) {
+    const int mid = lo + ((hi - lo) >> 1);
+    if (DistOf(mid, inv, bias) <= td) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+template <int K>
+__device__ __forceinline__ v16i TileSums(const uint32_t* codes, const v4i* frag) {
+  v16i acc = {0};
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    const uint32_t nib = (codes[s >> 3] >> ((s & 7) * 4)) & 15u;
+    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(OneHot16(nib), frag[s], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+template <int K>
+__device__ __forceinline__ void LoadCodes(const uint8_t* p, uint32_t* codes) {
+  constexpr int NW = ((((K + 1) / 2) + 3) / 4);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+  if constexpr (NW == 4) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    codes[0] = v.x; codes[1] = v.y; codes[2] = v.z; codes[3] = v.w;
+  } else if constexpr (NW == 2) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    codes[0] = v.x; codes[1] = v.y;
+  } else {
+#pragma unroll
+    for (int i = 0; i < NW; ++i) codes[i] = w[i];
+  }
+}
+
+template <int K>
+__global__ void __launch_bounds__(256) lut16_scan_kernel(ScanArgs a) {
+  constexpr int NW = ((((K + 1) / 2) + 3) / 4);
+  constexpr int W = 4 * NW;
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 31;
+  const int h = lane >> 5;
+  const uint32_t total = a.tile_prefix[a.nl];
+  const int smin = -128 * a.nb, smax = 128 * a.nb;
+  for (;;) {
+    uint32_t w = 0;
+    if (lane == 0) w = atomicAdd(a.work_counter, 1u);
+    w = __builtin_amdgcn_readfirstlane(__shfl(w, 0));
+    if (w >= total) break;
+    const int leaf = int(a.tile_leaf[w]);
+    const uint32_t t = w - a.tile_prefix[leaf];
+    const uint32_t pbeg = a.pair_off[leaf] + t * kQueriesPerTile;
+    const uint32_t pend = a.pair_off[leaf + 1];
+    const int nvalid = int(min(uint32_t(kQueriesPerTile), pend - pbeg));
+    const bool valid = c < nvalid;
+    const uint32_t pidx = pbeg + uint32_t(valid ? c : 0);
+    const uint32_t qid = a.pair_q[pidx];
+    const float bias = a.residual ? a.pair_bias[pidx] : 0.0f;
+    const float inv = a.inv[qid];
+    v4i frag[K];
+    const v4i* lrow = reinterpret_cast<const v4i*>(a.lut + size_t(qid) * (2 * K) * 16);
+#pragma unroll
+    for (int s = 0; s < K; ++s) frag[s] = lrow[2 * s + h];
+    const uint64_t T = a.tau_key ? a.tau_key[qid] : kNoThreshold;
+    const int amax = (T == kNoThreshold)
+                         ? smax
+                         : SumLimit(FromOrdered(uint32_t(T >> 32)), inv, bias, smin, smax);
+    const uint32_t n = a.leaf_size[leaf];
+    const uint32_t ntile = (n + kDpPerTile - 1) / kDpPerTile;
+    const uint8_t* tb = a.tiles + a.tile_off[leaf] * 64ull * W + size_t(lane) * W;
+    const uint64_t moff = a.member_off[leaf];
+    uint32_t codes[NW], next[NW];
+    if (ntile) LoadCodes<K>(tb, codes);
+    for (uint32_t j = 0; j < ntile; ++j) {
+      if (j + 1 < ntile) LoadCodes<K>(tb + size_t(j + 1) * 64 * W, next);
+      const v16i acc = TileSums<K>(codes, frag);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t row = (i & 3) + 8 * (i >> 2) + 4 * h;
+        const uint32_t dp = j * kDpPerTile + row;
+        if (valid && dp < n && acc[i] <= amax) {
+          const float d = DistOf(acc[i], inv, bias);
+          const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp)
+                                           : a.members[moff + dp];
+          const uint64_t key = (uint64_t(OrderedBits(d)) << 32) | tie;
+          if (key <= T) {
+            const uint32_t slot = atomicAdd(&a.cand_count[qid], 1u);
+            if (slot < a.cap) a.cand[size_t(qid) * a.cap + slot] = key;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NW; ++i) codes[i] = next[i];
+    }
+  }
+}
+
+// One-query variant for the stage entry point: raw sums of one leaf.
+template <int K>
+__global__ void __launch_bounds__(64) leaf_scores_kernel(const uint8_t* __restrict__ tiles,
+                                                         uint64_t tile0, uint32_t n,
+                                                         const int8_t* __restrict__ lut,
+                                                         int32_t* __restrict__ out) {
+  constexpr int NW = ((((K + 1) / 2) + 3) / 4);
+  constexpr int W = 4 * NW;
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 31;
+  const int h = lane >> 5;
+  v4i frag[K];
+  const v4i* lrow = reinterpret_cast<const v4i*>(lut);
+#pragma unroll
+  for (int s = 0; s < K; ++s) frag[s] = lrow[2 * s + h];
+  const uint32_t ntile = (n + 31) / 32;
+  for (uint32_t j = 0; j < ntile; ++j) {
+    uint32_t codes[NW];
+    LoadCodes<K>(tiles + (tile0 + j) * 64ull * W + size_t(lane) * W, codes);
+    const v16i acc = TileSums<K>(codes, frag);
+    if (c == 0) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t dp = j * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (dp < n) out[dp] = acc[i];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Seed selection: the k'-th best key among a query's seed-leaf candidates is
+// a valid threshold for the whole scan (every stored key is a genuine
+// candidate, so the k'-th of any subset bounds the final k'-th from above).
+// The main pass rescans the seed leaves, so nothing here must be complete.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) seed_select_kernel(
+    const uint64_t* __restrict__ seed_cand, const uint32_t* __restrict__ seed_count,
+    uint32_t seed_cap, int kk, uint64_t* __restrict__ tau_key) {
+  extern __shared__ uint64_t keys[];
+  const int qi = blockIdx.x;
+  const uint32_t n = min(seed_count[qi], seed_cap);
+  if (kk <= 0 || n < uint32_t(kk)) return;
+  const uint32_t np2 = NextPow2(n);
+  for (uint32_t i = threadIdx.x; i < np2; i += blockDim.x)
+    keys[i] = i < n ? seed_cand[size_t(qi) * seed_cap + i] : ~0ull;
+  __syncthreads();
+  BitonicSort(keys, np2);
+  if (threadIdx.x == 0 && keys[kk - 1] < tau_key[qi]) tau_key[qi] = keys[kk - 1];
+}
+
+// Overflow recovery: the k'-th smallest stored key is a valid (tighter)
+// threshold because every stored key is a genuine candidate.
+__global__ void __launch_bounds__(256) tighten_kernel(const uint64_t* __restrict__ cand,
+                                                      const uint32_t* __restrict__ cand_count,
+                                                      uint32_t cap, int kk,
+                                                      uint64_t* __restrict__ tau_key) {
+  extern __shared__ uint64_t keys[];
+  const int qi = blockIdx.x;
+  if (cand_count[qi] <= cap || kk <= 0) return;
+  const uint32_t np2 = NextPow2(cap);
+  for (uint32_t i = threadIdx.x; i < np2; i += blockDim.x)
+    keys[i] = i < cap ? cand[size_t(qi) * cap + i] : ~0ull;
+  __syncthreads();
+  BitonicSort(keys, np2);
+  if (threadIdx.x == 0 && keys[kk - 1] < tau_key[qi]) tau_key[qi] = keys[kk - 1];
+}
+
+// Exact reorder distance (A.8): 8 fused accumulators over dims 0..8m-1,
+// folded (l, l+4), a 4-wide and a 2-wide (lanes 2,3) tail, then
+// (s0+s2)+(s1+s3) and a fused scalar tail.
+__device__ float ExactDistance(const float* __restrict__ q, const float* __restrict__ x,
+                               int dim, int metric) {
+  auto term = [metric](float acc, float a, float b) {
+    if (metric == 0) return __fmaf_rn(-a, b, acc);
+    const float t = __fsub_rn(a, b);
+    return __fmaf_rn(t, t, acc);
+  };
+  float a8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int j = 0;
+  for (; j + 8 <= dim; j += 8) {
+#pragma unroll
+    for (int l = 0; l < 8; ++l) a8[l] = term(a8[l], q[j + l], x[j + l]);
+  }
+  float s[4];
+#pragma unroll
+  for (int l = 0; l < 4; ++l) s[l] = __fadd_rn(a8[l + 4], a8[l]);
+  if (j + 4 <= dim) {
+#pragma unroll
+    for (int l = 0; l < 4; ++l) s[l] = term(s[l], q[j + l], x[j + l]);
+    j += 4;
+  }
+  if (j + 2 <= dim) {
+    s[2] = term(s[2], q[j], x[j]);
+    s[3] = term(s[3], q[j + 1], x[j + 1]);
+    j += 2;
+  }
+  float r = __fadd_rn(__fadd_rn(s[0], s[2]), __fadd_rn(s[1], s[3]));
+  if (j < dim) r = term(r, q[j], x[j]);
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// Final selection per query: exact k' best by (distance, tie id) among the
+// candidates, tie -> global id, SOAR de-duplication, exact reorder, and the
+// (distance, id) sort of SortAndDropResults.
+// LDS: keys[cap_pow2] u64 | q[dim] f32 | gid/dist scratch.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) final_select_kernel(SelectArgs a) {
+  extern __shared__ uint64_t lds[];
+  const int qi = blockIdx.x;
+  const uint32_t raw_n = a.cand_count[qi];
+  if (raw_n > a.cap && threadIdx.x == 0) {
+    atomicOr(&a.overflow[0], 1u);
+    atomicMax(&a.overflow[1], raw_n);
+  }
+  if (threadIdx.x == 0) atomicMax(&a.overflow[2], raw_n);
+  const uint32_t n = min(raw_n, a.cap);
+  const uint32_t np2 = NextPow2(n);
+  uint64_t* keys = lds;
+  const uint32_t kcap = NextPow2(a.cap);
+  uint64_t* aux = lds + kcap;
+  float* q = reinterpret_cast<float*>(aux + NextPow2(uint32_t(a.kk)));
+  uint32_t* gid = reinterpret_cast<uint32_t*>(q + a.dim);
+  float* dist = reinterpret_cast<float*>(gid + a.kk);
+  __shared__ uint32_t s_m;
+  for (uint32_t i = threadIdx.x; i < np2; i += blockDim.x)
+    keys[i] = i < n ? a.cand[size_t(qi) * a.cap + i] : ~0ull;
+  if (a.reorder)
+    for (int d = threadIdx.x; d < a.dim; d += blockDim.x) q[d] = a.queries[size_t(qi) * a.dim + d];
+  __syncthreads();
+  BitonicSort(keys, np2);
+  uint32_t m = min(n, uint32_t(a.kk));
+  // tie -> global id
+  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+    const uint64_t k = keys[i];
+    uint32_t tie = uint32_t(k & 0xFFFFFFFFu);
+    if (a.shift > 0) {
+      const uint32_t leaf = tie >> a.shift;
+      const uint32_t local = tie & ((1u << a.shift) - 1u);
+      tie = a.members[a.member_off[leaf] + local];
+    }
+    gid[i] = tie;
+    dist[i] = FromOrdered(uint32_t(k >> 32));
+  }
+  __syncthreads();
+  if (!a.disjoint) {
+    // Group duplicates by id: sort (gid << 32 | rank).
+    const uint32_t mp2 = NextPow2(m);
+    for (uint32_t i = threadIdx.x; i < mp2; i += blockDim.x)
+      keys[i] = i < m ? ((uint64_t(gid[i]) << 32) | i) : ~0ull;
+    __syncthreads();
+    BitonicSort(keys, mp2);
+    // For each run start: averaged distance 0.5a + 0.5b (two copies at most).
+    // (ordered(d) << 32 | gid) for run starts, MAX for the rest.
+    for (uint32_t i = threadIdx.x; i < mp2; i += blockDim.x) {
+      uint64_t out = ~0ull;
+      if (i < m) {
+        const uint32_t g = uint32_t(keys[i] >> 32);
+        const bool start = (i == 0) || uint32_t(keys[i - 1] >> 32) != g;
+        if (start) {
+          float d = dist[uint32_t(keys[i] & 0xFFFFFFFFu)];
+          if (i + 1 < m && uint32_t(keys[i + 1] >> 32) == g) {
+            const float d2 = dist[uint32_t(keys[i + 1] & 0xFFFFFFFFu)];
+            d = __fadd_rn(__fmul_rn(0.5f, d), __fmul_rn(0.5f, d2));
+          }
+          out = (uint64_t(OrderedBits(d)) << 32) | g;
+        }
+      }
+      aux[i] = out;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < mp2; i += blockDim.x) keys[i] = aux[i];
+    __syncthreads();
+    BitonicSort(keys, mp2);
+    if (threadIdx.x == 0) {
+      uint32_t u = 0;
+      while (u < m && keys[u] != ~0ull) ++u;
+      s_m = min(u, uint32_t(a.pre_nn));
+    }
+    __syncthreads();
+    m = s_m;
+    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+      gid[i] = uint32_t(keys[i] & 0xFFFFFFFFu);
+      dist[i] = FromOrdered(uint32_t(keys[i] >> 32));
+    }
+    __syncthreads();
+  }
+  if (a.reorder && !a.pre_only) {
+    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
+      dist[i] = ExactDistance(q, a.dataset + size_t(gid[i]) * a.dim, a.dim, a.metric);
+    __syncthreads();
+  }
+  // Sort by (distance, global id) and keep the output width.
+  const uint32_t mp2 = NextPow2(m);
+  for (uint32_t i = threadIdx.x; i < mp2; i += blockDim.x)
+    keys[i] = i < m ? ((uint64_t(OrderedBits(dist[i])) << 32) | gid[i]) : ~0ull;
+  __syncthreads();
+  BitonicSort(keys, mp2);
+  const uint32_t keep = min(m, uint32_t(a.out_width));
+  for (int i = threadIdx.x; i < a.out_width; i += blockDim.x) {
+    const bool has = uint32_t(i) < keep;
+    a.out_idx[size_t(qi) * a.out_width + i] = has ? uint32_t(keys[i] & 0xFFFFFFFFu) : 0u;
+    a.out_dist[size_t(qi) * a.out_width + i] =
+        has ? FromOrdered(uint32_t(keys[i] >> 32)) : __int_as_float(0x7fc00000);
+  }
+  if (threadIdx.x == 0 && a.out_count) a.out_count[qi] = int32_t(keep);
+}
+
+__global__ void exact_distances_kernel(const float* __restrict__ queries, const float* __restrict__ dataset,
+                                       int dim, int metric, const uint32_t* __restrict__ ids,
+                                       int k, float* __restrict__ out) {
+  const int qi = blockIdx.x;
+  for (int i = threadIdx.x; i < k; i += blockDim.x) {
+    const uint32_t g = ids[size_t(qi) * k + i];
+    out[size_t(qi) * k + i] = ExactDistance(queries + size_t(qi) * dim, dataset + size_t(g) * dim, dim, metric);
+  }
+}
+
+__global__ void fill64_kernel(uint64_t* p, uint64_t v, size_t n) {
+  const size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Launchers.
+// ---------------------------------------------------------------------------
+hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int nq, int L,
+                               int32_t* out_leaf, float* out_dist, hipStream_t s) {
+  if (nq == 0) return hipSuccess;
+  uint32_t np2 = 1;
+  while (np2 < uint32_t(ix.nl)) np2 <<= 1;
+  const size_t lds = size_t(np2) * 8 + size_t(ix.dim) * 4;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(partition_topl_kernel, dim3(nq), dim3(256), lds, s, queries, ix.dim,
+                     ix.centers_t, ix.cnorm, ix.nl, ix.metric, L, np2, out_leaf, out_dist);
+  return hipGetLastError();
+}
+
+hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq, int8_t* lut,
+                          float* mult, float* inv, uint8_t* lut_u8, hipStream_t s) {
+  if (nq == 0) return hipSuccess;
+  hipLaunchKernelGGL(lut_build_kernel, dim3(nq), dim3(256), 0, s, queries, ix.dim, ix.codebook,
+                     ix.nb, ix.dpb, 2 * ix.ksteps, ix.metric, ix.residual, lut, mult, inv, lut_u8);
+  return hipGetLastError();
+}
+
+hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf, const float* topl_dist,
+                       int nq, int L, int seed_leaves, uint32_t* cnt, uint32_t* fill,
+                       uint32_t* pair_off, uint32_t* tile_prefix, uint32_t* pair_q,
+                       float* pair_bias, uint32_t* tile_leaf, uint32_t max_items,
+                       unsigned long long* code_bytes, hipStream_t s) {
+  const int n = nq * L;
+  const int blocks = (n + 255) / 256;
+  if (n > 0) {
+    hipLaunchKernelGGL(pairs_count_kernel, dim3(blocks), dim3(256), 0, s, topl_leaf, nq, L,
+                       seed_leaves, ix.nl, cnt, ix.leaf_size, ix.nb,
+                       code_bytes);
+  }
+  hipLaunchKernelGGL(pairs_scan_kernel, dim3(2), dim3(1024), 0, s, cnt, ix.nl, pair_off,
+                     tile_prefix);
+  if (n > 0) {
+    hipLaunchKernelGGL(pairs_scatter_kernel, dim3(blocks), dim3(256), 0, s, topl_leaf,
+                       topl_dist, nq, L, seed_leaves, ix.nl, pair_off, fill, pair_q, pair_bias);
+  }
+  hipLaunchKernelGGL(pairs_tiles_kernel, dim3((ix.nl + 255) / 256, 2), dim3(256), 0, s,
+                     tile_prefix, ix.nl, tile_leaf, max_items);
+  return hipGetLastError();
+}
+
+#define SMX_SCAN_CASE(KV)                                                        \
+  case KV:                                                                       \
+    hipLaunchKernelGGL(lut16_scan_kernel<KV>, dim3(grid), dim3(256), 0, s, a);   \
+    break;
+
+hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, hipStream_t s) {
+  switch (ix.ksteps) {
+    SMX_SCAN_CASE(4)
+    SMX_SCAN_CASE(8)
+    SMX_SCAN_CASE(12)
+    SMX_SCAN_CASE(16)
+    SMX_SCAN_CASE(20)
+    SMX_SCAN_CASE(24)
+    SMX_SCAN_CASE(25)
+    SMX_SCAN_CASE(28)
+    SMX_SCAN_CASE(32)
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+#define SMX_LEAF_CASE(KV)                                                                  \
+  case KV:                                                                                 \
+    hipLaunchKernelGGL(leaf_scores_kernel<KV>, dim3(1), dim3(64), 0, s, ix.tiles, tile0, n, \
+                       lut, out);                                                          \
+    break;
+
+hipError_t LaunchLeafScores(const DeviceIndex& ix, int leaf, const int8_t* lut, int32_t* out,
+                            hipStream_t s) {
+  uint64_t tile0 = 0;
+  uint32_t n = 0;
+  hipError_t e = hipMemcpyAsync(&tile0, ix.tile_off + leaf, 8, hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return e;
+  e = hipMemcpyAsync(&n, ix.leaf_size + leaf, 4, hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return e;
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return e;
+  if (n == 0) return hipSuccess;
+  switch (ix.ksteps) {
+    SMX_LEAF_CASE(4)
+    SMX_LEAF_CASE(8)
+    SMX_LEAF_CASE(12)
+    SMX_LEAF_CASE(16)
+    SMX_LEAF_CASE(20)
+    SMX_LEAF_CASE(24)
+    SMX_LEAF_CASE(25)
+    SMX_LEAF_CASE(28)
+    SMX_LEAF_CASE(32)
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t LaunchSeedSelect(const uint64_t* seed_cand, const uint32_t* seed_count,
+                            uint32_t seed_cap, int nq, int kk, uint64_t* tau_key,
+                            hipStream_t s) {
+  if (nq == 0) return hipSuccess;
+  uint32_t np2 = 1;
+  while (np2 < seed_cap) np2 <<= 1;
+  const size_t lds = size_t(np2) * 8;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(seed_select_kernel, dim3(nq), dim3(256), lds, s, seed_cand, seed_count,
+                     seed_cap, kk, tau_key);
+  return hipGetLastError();
+}
+
+hipError_t LaunchTighten(const uint64_t* cand, const uint32_t* cand_count, uint32_t cap, int nq,
+                         int kk, uint64_t* tau_key, hipStream_t s) {
+  if (nq == 0) return hipSuccess;
+  uint32_t np2 = 1;
+  while (np2 < cap) np2 <<= 1;
+  const size_t lds = size_t(np2) * 8;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(tighten_kernel, dim3(nq), dim3(256), lds, s, cand, cand_count, cap, kk,
+                     tau_key);
+  return hipGetLastError();
+}
+
+hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s) {
+  if (nq == 0) return hipSuccess;
+  uint32_t kcap = 1;
+  while (kcap < a.cap) kcap <<= 1;
+  uint32_t kkp2 = 1;
+  while (kkp2 < uint32_t(a.kk)) kkp2 <<= 1;
+  const size_t lds = size_t(kcap) * 8 + size_t(kkp2) * 8 + size_t(a.dim) * 4 + size_t(a.kk) * 8;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(final_select_kernel, dim3(nq), dim3(256), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t LaunchExactDistances(const DeviceIndex& ix, const float* queries, int nq,
+                                const uint32_t* ids, int k, float* out, hipStream_t s) {
+  if (nq == 0 || k == 0) return hipSuccess;
+  hipLaunchKernelGGL(exact_distances_kernel, dim3(nq), dim3(128), 0, s, queries, ix.dataset,
+                     ix.dim, ix.metric, ids, k, out);
+  return hipGetLastError();
+}
+
+hipError_t LaunchFill64(uint64_t* p, uint64_t v, size_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(fill64_kernel, dim3((n + 255) / 256), dim3(256), 0, s, p, v, n);
+  return hipGetLastError();
+}
+
+}  // namespace smx

@@ -1,0 +1,756 @@
+// smx_searcher.hip — host side of the MI355X tree-AH searcher: index upload
+// into the device layout, the batched search pipeline and the C ABI of
+// include/scann_mi355x.h.
+//
+// Pipeline of one search_batched call (all on one HIP stream):
+//   1 partition_topl      query tokenization (top-L leaves + biases)
+//   2 lut_build           per-query int8 LUT16 tables, multipliers
+//   3 pairs               invert query->leaves into leaf->queries (seed/main)
+//   4 seed scan + select  per-query threshold from its first `seed_leaves`
+//                         leaves (k'-th best key there)
+//   5 main scan           every (leaf, query tile): MFMA LUT16 sums, fused
+//                         distance, emission of keys <= threshold
+//   6 final select        exact top-k' -> global ids -> SOAR dedupe -> exact
+//                         reorder -> (distance, id) sort -> outputs
+// A candidate list that overflows its capacity triggers the tightening loop
+// (threshold <- k'-th stored key, rescan), which always makes progress.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/scann_mi355x.h"
+#include "smx_internal.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int Fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define SMX_HIP(expr)                                                              \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess)                                                          \
+      return Fail(_e == hipErrorOutOfMemory ? SMX_OUT_OF_MEMORY : SMX_DEVICE_ERROR, \
+                  std::string("HIP error in ") + #expr + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+template <typename T>
+int DAlloc(T** p, size_t n) {
+  *p = nullptr;
+  if (n == 0) return SMX_OK;
+  SMX_HIP(hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T)));
+  return SMX_OK;
+}
+
+template <typename T>
+void DFree(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+int Log2Ceil(uint32_t n) {
+  int f = 31 - __builtin_clz(n);
+  return ((n & (n - 1)) == 0) ? f : f + 1;
+}
+
+// K values with a compiled scan kernel; others round up (zero padding).
+int EffectiveKSteps(int nb) {
+  static const int kList[] = {4, 8, 12, 16, 20, 24, 25, 28, 32};
+  const int k = (nb + 1) / 2;
+  for (int v : kList)
+    if (v >= k) return v;
+  return -1;
+}
+
+struct Workspace {
+  int nq = 0, L = 0, kk = 0, dim = 0, width = 0;
+  uint32_t cap = 0, seed_cap = 0, max_items = 0;
+  float* queries = nullptr;
+  int32_t* topl_leaf = nullptr;
+  float* topl_dist = nullptr;
+  int8_t* lut = nullptr;
+  uint8_t* lut_u8 = nullptr;
+  float* mult = nullptr;
+  float* inv = nullptr;
+  uint32_t* counters = nullptr;     // cnt[2][nl] | fill[2][nl] | work[2] | overflow[3]
+  uint32_t* pair_off = nullptr;     // [2][nl+1]
+  uint32_t* tile_prefix = nullptr;  // [2][nl+1]
+  uint32_t* pair_q = nullptr;       // [2][nq*L]
+  float* pair_bias = nullptr;       // [2][nq*L]
+  uint32_t* tile_leaf = nullptr;    // [2][max_items]
+  unsigned long long* code_bytes = nullptr;  // [2]
+  uint64_t* tau = nullptr;          // [nq]
+  uint64_t* seed_cand = nullptr;    // [nq][seed_cap]
+  uint32_t* seed_count = nullptr;   // [nq]
+  uint64_t* cand = nullptr;         // [nq][cap]
+  uint32_t* cand_count = nullptr;   // [nq]
+  uint32_t* out_idx = nullptr;
+  float* out_dist = nullptr;
+  int32_t* out_count = nullptr;
+
+  void Release() {
+    DFree(queries); DFree(topl_leaf); DFree(topl_dist); DFree(lut); DFree(lut_u8);
+    DFree(mult); DFree(inv); DFree(counters); DFree(pair_off); DFree(tile_prefix);
+    DFree(pair_q); DFree(pair_bias); DFree(tile_leaf); DFree(code_bytes); DFree(tau);
+    DFree(seed_cand); DFree(seed_count); DFree(cand); DFree(cand_count);
+    DFree(out_idx); DFree(out_dist); DFree(out_count);
+    nq = L = kk = dim = width = 0;
+    cap = seed_cap = max_items = 0;
+  }
+};
+
+}  // namespace
+
+struct smx_index {
+  smx::DeviceIndex ix;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  Workspace ws;
+  uint32_t cap_per_query = 4096;   // candidate list capacity
+  int seed_leaves = 1;
+  int grid = 0;                    // scan grid (blocks of 4 waves)
+  bool profiling = false;
+  smx_timings timings{};
+  hipEvent_t ev[16] = {};
+};
+
+namespace {
+
+int UploadIndex(const smx_index_desc* d, smx_index* h) {
+  smx::DeviceIndex& ix = h->ix;
+  ix.metric = d->metric;
+  ix.dim = d->dim;
+  ix.nl = d->num_leaves;
+  ix.nb = d->num_blocks;
+  ix.dpb = d->dims_per_block;
+  ix.residual = d->residual ? 1 : 0;
+  ix.num_datapoints = d->num_datapoints;
+  ix.spill = d->spilling_overretrieve_factor > 0 ? d->spilling_overretrieve_factor : 2.0f;
+  ix.ksteps = EffectiveKSteps(ix.nb);
+  ix.lane_bytes = smx::LaneBytes(ix.ksteps);
+  const int nl = ix.nl, dim = ix.dim, nb = ix.nb, K = ix.ksteps, W = ix.lane_bytes;
+  const uint64_t M = d->leaf_offsets[nl];
+  ix.num_members = M;
+
+  // Per-leaf sizes, tile offsets, max leaf, disjointness.
+  std::vector<uint32_t> size(nl);
+  std::vector<uint64_t> toff(nl + 1, 0);
+  for (int l = 0; l < nl; ++l) {
+    const uint64_t n = d->leaf_offsets[l + 1] - d->leaf_offsets[l];
+    size[l] = uint32_t(n);
+    ix.max_leaf = std::max<uint32_t>(ix.max_leaf, uint32_t(n));
+    toff[l + 1] = toff[l] + (n + 31) / 32;
+  }
+  ix.num_tiles = toff[nl];
+  ix.disjoint = (M == d->num_datapoints);
+  if (ix.disjoint) {
+    std::vector<uint8_t> seen(d->num_datapoints, 0);
+    for (uint64_t i = 0; i < M; ++i) {
+      const uint32_t g = d->leaf_members[i];
+      if (seen[g]) { ix.disjoint = false; break; }
+      seen[g] = 1;
+    }
+  }
+  // Global top-N shift (tree_ah_hybrid_residual.h:234-247).
+  ix.shift = 0;
+  if (ix.residual && nl > 1) {
+    const int inner = 32 - Log2Ceil(uint32_t(nl));
+    if (uint64_t(ix.max_leaf) <= (1ull << inner)) ix.shift = inner;
+  }
+
+  // Code tiles: lane l = h*32 + r of tile j of a leaf holds, as nibbles
+  // s = 0..K-1 (low nibble first), the codes of datapoint 32j + r for blocks
+  // 2s + h.  Missing datapoints / blocks are code 0 against a zero LUT row or
+  // are masked in the epilogue.
+  std::vector<uint8_t> tiles(size_t(ix.num_tiles) * 64 * W, 0);
+  for (int l = 0; l < nl; ++l) {
+    const uint64_t beg = d->leaf_offsets[l];
+    const uint32_t n = size[l];
+    for (uint32_t dp = 0; dp < n; ++dp) {
+      const uint8_t* code = d->member_codes + (beg + dp) * nb;
+      const uint64_t tile = toff[l] + dp / 32;
+      const uint32_t r = dp % 32;
+      for (int b = 0; b < nb; ++b) {
+        const int h = b & 1, s = b >> 1;
+        uint8_t* lane = &tiles[(tile * 64 + size_t(h) * 32 + r) * W];
+        lane[s >> 1] |= uint8_t((code[b] & 15) << ((s & 1) * 4));
+      }
+    }
+  }
+  (void)K;
+
+  // Transposed centers and squared norms (A.10 database side).
+  std::vector<float> ct(size_t(dim) * nl);
+  std::vector<float> cn(nl);
+  for (int l = 0; l < nl; ++l) {
+    float acc = 0.0f;
+    for (int k = 0; k < dim; ++k) {
+      const float v = d->centers[size_t(l) * dim + k];
+      ct[size_t(k) * nl + l] = v;
+      acc = std::fma(-v, v, acc);
+    }
+    cn[l] = acc * -1.0f;
+  }
+  int rc;
+  if ((rc = DAlloc(&ix.centers, size_t(nl) * dim)) ||
+      (rc = DAlloc(&ix.centers_t, size_t(nl) * dim)) || (rc = DAlloc(&ix.cnorm, nl)) ||
+      (rc = DAlloc(&ix.codebook, size_t(nb) * 16 * ix.dpb)) ||
+      (rc = DAlloc(&ix.tiles, tiles.size())) || (rc = DAlloc(&ix.tile_off, nl + 1)) ||
+      (rc = DAlloc(&ix.leaf_size, nl)) || (rc = DAlloc(&ix.member_off, nl + 1)) ||
+      (rc = DAlloc(&ix.members, M)))
+    return rc;
+  if (d->dataset && (rc = DAlloc(&ix.dataset, size_t(d->num_datapoints) * dim))) return rc;
+  SMX_HIP(hipMemcpy(ix.centers, d->centers, sizeof(float) * nl * dim, hipMemcpyHostToDevice));
+  SMX_HIP(hipMemcpy(ix.centers_t, ct.data(), sizeof(float) * nl * dim, hipMemcpyHostToDevice));
+  SMX_HIP(hipMemcpy(ix.cnorm, cn.data(), sizeof(float) * nl, hipMemcpyHostToDevice));
+  SMX_HIP(hipMemcpy(ix.codebook, d->codebook, sizeof(float) * nb * 16 * ix.dpb, hipMemcpyHostToDevice));
+  if (!tiles.empty())
+    SMX_HIP(hipMemcpy(ix.tiles, tiles.data(), tiles.size(), hipMemcpyHostToDevice));
+  SMX_HIP(hipMemcpy(ix.tile_off, toff.data(), 8 * (nl + 1), hipMemcpyHostToDevice));
+  SMX_HIP(hipMemcpy(ix.leaf_size, size.data(), 4 * nl, hipMemcpyHostToDevice));
+  SMX_HIP(hipMemcpy(ix.member_off, d->leaf_offsets, 8 * (nl + 1), hipMemcpyHostToDevice));
+  if (M) SMX_HIP(hipMemcpy(ix.members, d->leaf_members, 4 * M, hipMemcpyHostToDevice));
+  if (d->dataset)
+    SMX_HIP(hipMemcpy(ix.dataset, d->dataset, sizeof(float) * size_t(d->num_datapoints) * dim,
+                      hipMemcpyHostToDevice));
+  return SMX_OK;
+}
+
+void FreeIndex(smx::DeviceIndex& ix) {
+  DFree(ix.centers); DFree(ix.centers_t); DFree(ix.cnorm); DFree(ix.codebook);
+  DFree(ix.tiles); DFree(ix.tile_off); DFree(ix.leaf_size); DFree(ix.member_off);
+  DFree(ix.members); DFree(ix.dataset);
+}
+
+int ValidateDesc(const smx_index_desc* d) {
+  if (!d) return Fail(SMX_INVALID_ARGUMENT, "null index description");
+  if (d->metric != SMX_METRIC_DOT && d->metric != SMX_METRIC_SQUARED_L2)
+    return Fail(SMX_INVALID_ARGUMENT, "metric must be dot product or squared L2");
+  if (d->dim <= 0 || d->num_leaves <= 0 || d->num_blocks <= 0 || d->dims_per_block <= 0)
+    return Fail(SMX_INVALID_ARGUMENT, "dim, num_leaves, num_blocks, dims_per_block must be > 0");
+  if (d->num_blocks > smx::kMaxBlocks)
+    return Fail(SMX_INVALID_ARGUMENT, "LUT16 path supports at most 64 AH blocks");
+  const int last = d->dim - d->dims_per_block * (d->num_blocks - 1);
+  if (last <= 0 || last > d->dims_per_block)
+    return Fail(SMX_INVALID_ARGUMENT, "num_blocks x dims_per_block does not tile dim");
+  if (!d->centers || !d->codebook || !d->leaf_offsets)
+    return Fail(SMX_INVALID_ARGUMENT, "centers, codebook and leaf_offsets are required");
+  if (d->leaf_offsets[0] != 0) return Fail(SMX_INVALID_ARGUMENT, "leaf_offsets[0] must be 0");
+  for (int l = 0; l < d->num_leaves; ++l)
+    if (d->leaf_offsets[l + 1] < d->leaf_offsets[l])
+      return Fail(SMX_INVALID_ARGUMENT, "leaf_offsets must be non-decreasing");
+  const uint64_t M = d->leaf_offsets[d->num_leaves];
+  if (M && (!d->leaf_members || !d->member_codes))
+    return Fail(SMX_INVALID_ARGUMENT, "leaf_members and member_codes are required");
+  if (M > 0xFFFFFFFFull) return Fail(SMX_INVALID_ARGUMENT, "too many members for 32-bit ids");
+  for (uint64_t i = 0; i < M; ++i) {
+    if (d->leaf_members[i] >= d->num_datapoints)
+      return Fail(SMX_INVALID_ARGUMENT, "leaf member id out of range");
+  }
+  for (uint64_t i = 0; i < M * uint64_t(d->num_blocks); ++i)
+    if (d->member_codes[i] > 15) return Fail(SMX_INVALID_ARGUMENT, "LUT16 codes must be < 16");
+  return SMX_OK;
+}
+
+int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
+  Workspace& w = h->ws;
+  const smx::DeviceIndex& ix = h->ix;
+  const uint32_t cap = std::max<uint32_t>(h->cap_per_query, uint32_t(kk));
+  const uint32_t seed_cap = std::min<uint32_t>(
+      16384u, std::max<uint32_t>(uint32_t(kk), uint32_t(h->seed_leaves) * ix.max_leaf));
+  if (nq <= w.nq && L <= w.L && kk <= w.kk && width <= w.width && cap == w.cap &&
+      seed_cap == w.seed_cap && ix.dim == w.dim)
+    return SMX_OK;
+  w.Release();
+  const int nl = ix.nl;
+  const size_t pairs = size_t(nq) * L;
+  const uint32_t max_items = uint32_t(pairs / smx::kQueriesPerTile + nl + 1);
+  int rc;
+  if ((rc = DAlloc(&w.queries, size_t(nq) * ix.dim)) || (rc = DAlloc(&w.topl_leaf, pairs)) ||
+      (rc = DAlloc(&w.topl_dist, pairs)) ||
+      (rc = DAlloc(&w.lut, size_t(nq) * 2 * ix.ksteps * 16)) ||
+      (rc = DAlloc(&w.lut_u8, size_t(nq) * ix.nb * 16)) || (rc = DAlloc(&w.mult, nq)) ||
+      (rc = DAlloc(&w.inv, nq)) || (rc = DAlloc(&w.counters, size_t(4) * nl + 8)) ||
+      (rc = DAlloc(&w.pair_off, size_t(2) * (nl + 1))) ||
+      (rc = DAlloc(&w.tile_prefix, size_t(2) * (nl + 1))) ||
+      (rc = DAlloc(&w.pair_q, 2 * pairs)) || (rc = DAlloc(&w.pair_bias, 2 * pairs)) ||
+      (rc = DAlloc(&w.tile_leaf, size_t(2) * max_items)) || (rc = DAlloc(&w.code_bytes, 2)) ||
+      (rc = DAlloc(&w.tau, nq)) || (rc = DAlloc(&w.seed_cand, size_t(nq) * seed_cap)) ||
+      (rc = DAlloc(&w.seed_count, nq)) || (rc = DAlloc(&w.cand, size_t(nq) * cap)) ||
+      (rc = DAlloc(&w.cand_count, nq)) || (rc = DAlloc(&w.out_idx, size_t(nq) * width)) ||
+      (rc = DAlloc(&w.out_dist, size_t(nq) * width)) || (rc = DAlloc(&w.out_count, nq))) {
+    w.Release();
+    return rc;
+  }
+  w.nq = nq; w.L = L; w.kk = kk; w.width = width; w.dim = ix.dim;
+  w.cap = cap; w.seed_cap = seed_cap; w.max_items = max_items;
+  return SMX_OK;
+}
+
+int32_t SpillK(const smx::DeviceIndex& ix, int32_t k) {
+  if (ix.disjoint) return k;
+  const double r = double(k) * double(ix.spill);
+  return r > 2147483647.0 ? 2147483647 : int32_t(r);
+}
+
+void Mark(smx_index* h, int i, hipStream_t s) {
+  if (h->profiling) (void)hipEventRecord(h->ev[i], s);
+}
+
+float Elapsed(smx_index* h, int a, int b) {
+  float ms = 0.0f;
+  if (hipEventElapsedTime(&ms, h->ev[a], h->ev[b]) != hipSuccess) return 0.0f;
+  return ms;
+}
+
+// The search pipeline.  queries: device [nq][dim].  pre_only: stop before
+// reorder and output the pre-reorder set (width pre_nn).
+int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int final_nn,
+              bool reorder, bool pre_only, uint32_t* out_idx, float* out_dist,
+              int32_t* out_count, hipStream_t s) {
+  smx::DeviceIndex& ix = h->ix;
+  if (nq == 0) return SMX_OK;
+  L = std::min(L, ix.nl);
+  const int pnn = reorder ? pre_nn : final_nn;
+  const int kk = std::max(1, SpillK(ix, pnn));
+  const int width = pre_only ? pnn : final_nn;
+  int rc = EnsureWorkspace(h, nq, L, kk, width);
+  if (rc) return rc;
+  Workspace& w = h->ws;
+  const int nl = ix.nl;
+  uint32_t* cnt = w.counters;
+  uint32_t* fill = w.counters + 2 * nl;
+  uint32_t* work = w.counters + 4 * nl;
+  uint32_t* overflow = work + 2;
+  const int seed = std::min(h->seed_leaves, L);
+
+  Mark(h, 0, s);
+  SMX_HIP(hipMemsetAsync(w.counters, 0, sizeof(uint32_t) * (4 * nl + 8), s));
+  SMX_HIP(hipMemsetAsync(w.code_bytes, 0, sizeof(unsigned long long) * 2, s));
+  SMX_HIP(hipMemsetAsync(w.seed_count, 0, sizeof(uint32_t) * nq, s));
+  SMX_HIP(hipMemsetAsync(w.cand_count, 0, sizeof(uint32_t) * nq, s));
+  SMX_HIP(smx::LaunchFill64(w.tau, smx::kNoThreshold, nq, s));
+  SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, s));
+  Mark(h, 1, s);
+  SMX_HIP(smx::LaunchLutBuild(ix, queries, nq, w.lut, w.mult, w.inv, nullptr, s));
+  Mark(h, 2, s);
+  SMX_HIP(smx::LaunchPairs(ix, w.topl_leaf, w.topl_dist, nq, L, seed, cnt, fill, w.pair_off,
+                           w.tile_prefix, w.pair_q, w.pair_bias, w.tile_leaf, w.max_items,
+                           w.code_bytes, s));
+  Mark(h, 3, s);
+
+  const size_t pairs = size_t(nq) * L;
+  auto scan_args = [&](int set, const uint64_t* tau, uint64_t* cand, uint32_t* count,
+                       uint32_t capq) {
+    smx::ScanArgs a{};
+    a.tiles = ix.tiles;
+    a.tile_off = ix.tile_off;
+    a.leaf_size = ix.leaf_size;
+    a.member_off = ix.member_off;
+    a.members = ix.members;
+    a.lut = w.lut;
+    a.inv = w.inv;
+    a.pair_q = w.pair_q + size_t(set) * pairs;
+    a.pair_bias = w.pair_bias + size_t(set) * pairs;
+    a.pair_off = w.pair_off + size_t(set) * (nl + 1);
+    a.tile_prefix = w.tile_prefix + size_t(set) * (nl + 1);
+    a.tile_leaf = w.tile_leaf + size_t(set) * w.max_items;
+    a.tau_key = tau;
+    a.cand = cand;
+    a.cand_count = count;
+    a.work_counter = work + set;
+    a.cap = capq;
+    a.nl = nl;
+    a.nb = ix.nb;
+    a.shift = ix.shift;
+    a.residual = ix.residual;
+    return a;
+  };
+  // Seed pass: everything of the first `seed` leaves per query.
+  if (seed > 0) {
+    const smx::ScanArgs sa = scan_args(0, nullptr, w.seed_cand, w.seed_count, w.seed_cap);
+    SMX_HIP(smx::LaunchScan(ix, sa, h->grid, s));
+    Mark(h, 4, s);
+    SMX_HIP(smx::LaunchSeedSelect(w.seed_cand, w.seed_count, w.seed_cap, nq, kk, w.tau, s));
+  } else {
+    Mark(h, 4, s);
+  }
+  Mark(h, 5, s);
+
+  smx::SelectArgs sel{};
+  sel.cand = w.cand;
+  sel.cand_count = w.cand_count;
+  sel.cap = w.cap;
+  sel.kk = kk;
+  sel.pre_nn = pnn;
+  sel.final_nn = final_nn;
+  sel.reorder = reorder ? 1 : 0;
+  sel.disjoint = ix.disjoint ? 1 : 0;
+  sel.pre_only = pre_only ? 1 : 0;
+  sel.shift = ix.shift;
+  sel.metric = ix.metric;
+  sel.dim = ix.dim;
+  sel.member_off = ix.member_off;
+  sel.members = ix.members;
+  sel.dataset = ix.dataset;
+  sel.queries = queries;
+  sel.out_idx = out_idx;
+  sel.out_dist = out_dist;
+  sel.out_count = out_count;
+  sel.out_width = width;
+  sel.overflow = overflow;
+
+  int retries = 0;
+  uint32_t ovf[3] = {0, 0, 0};
+  for (;;) {
+    const smx::ScanArgs ma = scan_args(1, w.tau, w.cand, w.cand_count, w.cap);
+    SMX_HIP(smx::LaunchScan(ix, ma, h->grid, s));
+    Mark(h, 6, s);
+    SMX_HIP(smx::LaunchFinalSelect(sel, nq, s));
+    Mark(h, 7, s);
+    SMX_HIP(hipMemcpyAsync(ovf, overflow, sizeof(ovf), hipMemcpyDeviceToHost, s));
+    SMX_HIP(hipStreamSynchronize(s));
+    if (!ovf[0]) break;
+    if (++retries > 64) return Fail(SMX_INTERNAL, "candidate tightening did not converge");
+    SMX_HIP(smx::LaunchTighten(w.cand, w.cand_count, w.cap, nq, kk, w.tau, s));
+    SMX_HIP(hipMemsetAsync(w.cand_count, 0, sizeof(uint32_t) * nq, s));
+    SMX_HIP(hipMemsetAsync(overflow, 0, sizeof(uint32_t) * 3, s));
+    SMX_HIP(hipMemsetAsync(work + 1, 0, sizeof(uint32_t), s));
+  }
+  if (h->profiling) {
+    smx_timings& t = h->timings;
+    t.partition_ms = Elapsed(h, 0, 1);
+    t.lut_ms = Elapsed(h, 1, 2);
+    t.invert_ms = Elapsed(h, 2, 3);
+    t.seed_scan_ms = Elapsed(h, 3, 4);
+    t.seed_select_ms = Elapsed(h, 4, 5);
+    t.scan_ms = Elapsed(h, 5, 6);
+    t.select_ms = Elapsed(h, 6, 7);
+    t.total_ms = Elapsed(h, 0, 7);
+    unsigned long long cb[2] = {0, 0};
+    (void)hipMemcpy(cb, w.code_bytes, sizeof(cb), hipMemcpyDeviceToHost);
+    uint32_t cnts[2] = {0, 0};
+    (void)hipMemcpy(&cnts[0], w.pair_off + nl, 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(&cnts[1], w.pair_off + (nl + 1) + nl, 4, hipMemcpyDeviceToHost);
+    t.seed_code_bytes = double(cb[0]);
+    t.scan_code_bytes = double(cb[1]);
+    t.seed_pairs = int32_t(cnts[0]);
+    t.scan_pairs = int32_t(cnts[1]);
+  }
+  h->timings.overflow_retries = retries;
+  h->timings.max_candidates = int32_t(ovf[2]);
+  return SMX_OK;
+}
+
+int CheckSearchArgs(smx_index* h, int nq, int dim, const smx_search_params* p) {
+  if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
+  if (!p) return Fail(SMX_INVALID_ARGUMENT, "null search params");
+  if (nq < 0) return Fail(SMX_INVALID_ARGUMENT, "negative batch size");
+  if (dim != h->ix.dim)
+    return Fail(SMX_INVALID_ARGUMENT, "Query doesn't match dataset dimsensionality");
+  if (p->leaves_to_search <= 0) return Fail(SMX_INVALID_ARGUMENT, "leaves_to_search must be > 0");
+  if (p->final_nn <= 0) return Fail(SMX_INVALID_ARGUMENT, "final_num_neighbors must be > 0");
+  if (p->reorder && p->pre_reorder_nn <= 0)
+    return Fail(SMX_INVALID_ARGUMENT, "pre_reorder_num_neighbors must be > 0");
+  if (p->reorder && !h->ix.dataset)
+    return Fail(SMX_FAILED_PRECONDITION, "exact reordering requested but index has no dataset");
+  const int pnn = p->reorder ? p->pre_reorder_nn : p->final_nn;
+  if (SpillK(h->ix, pnn) > 8192)
+    return Fail(SMX_INVALID_ARGUMENT, "pre-reorder neighbors above 8192 are not supported");
+  return SMX_OK;
+}
+
+int CheckFinite(const float* q, size_t n) {
+  for (size_t i = 0; i < n; ++i)
+    if (!std::isfinite(q[i])) return Fail(SMX_INVALID_ARGUMENT, "queries must be finite");
+  return SMX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* smx_last_error(void) { return g_last_error.c_str(); }
+const char* smx_version(void) { return "scann_mi355x 0.1 (gfx950)"; }
+
+int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out) {
+  if (!out) return Fail(SMX_INVALID_ARGUMENT, "null output handle");
+  *out = nullptr;
+  int rc = ValidateDesc(desc);
+  if (rc) return rc;
+  if (EffectiveKSteps(desc->num_blocks) < 0)
+    return Fail(SMX_INVALID_ARGUMENT, "unsupported number of AH blocks");
+  int ndev = 0;
+  SMX_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return Fail(SMX_INVALID_ARGUMENT, "no such HIP device");
+  SMX_HIP(hipSetDevice(device));
+  auto* h = new smx_index;
+  h->device = device;
+  rc = UploadIndex(desc, h);
+  if (rc) {
+    FreeIndex(h->ix);
+    delete h;
+    return rc;
+  }
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    FreeIndex(h->ix);
+    delete h;
+    return Fail(SMX_DEVICE_ERROR, "hipStreamCreate failed");
+  }
+  for (auto& e : h->ev) (void)hipEventCreate(&e);
+  hipDeviceProp_t prop;
+  SMX_HIP(hipGetDeviceProperties(&prop, device));
+  h->grid = prop.multiProcessorCount * 4;
+  *out = h;
+  return SMX_OK;
+}
+
+int smx_index_destroy(smx_index* h) {
+  if (!h) return SMX_OK;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  h->ws.Release();
+  FreeIndex(h->ix);
+  for (auto& e : h->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return SMX_OK;
+}
+
+int smx_index_info(const smx_index* h, int32_t* dim, int32_t* num_leaves,
+                   uint32_t* num_datapoints, int32_t* shift) {
+  if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
+  if (dim) *dim = h->ix.dim;
+  if (num_leaves) *num_leaves = h->ix.nl;
+  if (num_datapoints) *num_datapoints = h->ix.num_datapoints;
+  if (shift) *shift = h->ix.shift;
+  return SMX_OK;
+}
+
+int smx_search_batched_device(smx_index* h, const float* d_queries, int32_t nq, int32_t dim,
+                              const smx_search_params* p, uint32_t* d_out_idx,
+                              float* d_out_dist, int32_t* d_out_count, void* stream) {
+  int rc = CheckSearchArgs(h, nq, dim, p);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lock(h->mu);
+  SMX_HIP(hipSetDevice(h->device));
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+  return RunSearch(h, d_queries, nq, p->leaves_to_search, p->pre_reorder_nn, p->final_nn,
+                   p->reorder != 0, false, d_out_idx, d_out_dist, d_out_count, s);
+}
+
+int smx_search_batched(smx_index* h, const float* queries, int32_t nq, int32_t dim,
+                       const smx_search_params* p, uint32_t* out_idx, float* out_dist,
+                       int32_t* out_count) {
+  int rc = CheckSearchArgs(h, nq, dim, p);
+  if (rc) return rc;
+  if ((rc = CheckFinite(queries, size_t(nq) * dim))) return rc;
+  if (nq == 0) return SMX_OK;
+  std::lock_guard<std::mutex> lock(h->mu);
+  SMX_HIP(hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  const int width = p->final_nn;
+  const int pnn = p->reorder ? p->pre_reorder_nn : p->final_nn;
+  rc = EnsureWorkspace(h, nq, std::min(p->leaves_to_search, h->ix.nl),
+                       std::max(1, SpillK(h->ix, pnn)), width);
+  if (rc) return rc;
+  Workspace& w = h->ws;
+  SMX_HIP(hipMemcpyAsync(w.queries, queries, sizeof(float) * size_t(nq) * dim,
+                         hipMemcpyHostToDevice, s));
+  rc = RunSearch(h, w.queries, nq, p->leaves_to_search, p->pre_reorder_nn, p->final_nn,
+                 p->reorder != 0, false, w.out_idx, w.out_dist, w.out_count, s);
+  if (rc) return rc;
+  SMX_HIP(hipMemcpyAsync(out_idx, w.out_idx, sizeof(uint32_t) * size_t(nq) * width,
+                         hipMemcpyDeviceToHost, s));
+  SMX_HIP(hipMemcpyAsync(out_dist, w.out_dist, sizeof(float) * size_t(nq) * width,
+                         hipMemcpyDeviceToHost, s));
+  if (out_count)
+    SMX_HIP(hipMemcpyAsync(out_count, w.out_count, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, s));
+  SMX_HIP(hipStreamSynchronize(s));
+  return SMX_OK;
+}
+
+int smx_search_pre_reorder(smx_index* h, const float* queries, int32_t nq, int32_t leaves,
+                           int32_t pre_nn, uint32_t* out_idx, float* out_dist,
+                           int32_t* out_count) {
+  if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
+  if (leaves <= 0 || pre_nn <= 0) return Fail(SMX_INVALID_ARGUMENT, "leaves and pre_nn must be > 0");
+  if (SpillK(h->ix, pre_nn) > 8192) return Fail(SMX_INVALID_ARGUMENT, "pre_nn too large");
+  int rc = CheckFinite(queries, size_t(nq) * h->ix.dim);
+  if (rc) return rc;
+  if (nq == 0) return SMX_OK;
+  std::lock_guard<std::mutex> lock(h->mu);
+  SMX_HIP(hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  rc = EnsureWorkspace(h, nq, std::min(leaves, h->ix.nl), std::max(1, SpillK(h->ix, pre_nn)),
+                       pre_nn);
+  if (rc) return rc;
+  Workspace& w = h->ws;
+  SMX_HIP(hipMemcpyAsync(w.queries, queries, sizeof(float) * size_t(nq) * h->ix.dim,
+                         hipMemcpyHostToDevice, s));
+  rc = RunSearch(h, w.queries, nq, leaves, pre_nn, pre_nn, true, true, w.out_idx, w.out_dist,
+                 w.out_count, s);
+  if (rc) return rc;
+  SMX_HIP(hipMemcpyAsync(out_idx, w.out_idx, sizeof(uint32_t) * size_t(nq) * pre_nn,
+                         hipMemcpyDeviceToHost, s));
+  SMX_HIP(hipMemcpyAsync(out_dist, w.out_dist, sizeof(float) * size_t(nq) * pre_nn,
+                         hipMemcpyDeviceToHost, s));
+  if (out_count)
+    SMX_HIP(hipMemcpyAsync(out_count, w.out_count, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, s));
+  SMX_HIP(hipStreamSynchronize(s));
+  return SMX_OK;
+}
+
+int smx_partition_topl(smx_index* h, const float* queries, int32_t nq, int32_t L,
+                       int32_t* out_leaf, float* out_dist) {
+  if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
+  if (nq < 0 || L <= 0) return Fail(SMX_INVALID_ARGUMENT, "bad nq / L");
+  if (nq == 0) return SMX_OK;
+  std::lock_guard<std::mutex> lock(h->mu);
+  SMX_HIP(hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  float* dq = nullptr;
+  int32_t* dl = nullptr;
+  float* dd = nullptr;
+  int rc;
+  if ((rc = DAlloc(&dq, size_t(nq) * h->ix.dim)) || (rc = DAlloc(&dl, size_t(nq) * L)) ||
+      (rc = DAlloc(&dd, size_t(nq) * L))) {
+    DFree(dq); DFree(dl); DFree(dd);
+    return rc;
+  }
+  hipError_t e = hipMemcpyAsync(dq, queries, sizeof(float) * size_t(nq) * h->ix.dim,
+                                hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = smx::LaunchPartitionTopL(h->ix, dq, nq, L, dl, dd, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(out_leaf, dl, 4 * size_t(nq) * L, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(out_dist, dd, 4 * size_t(nq) * L, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  DFree(dq); DFree(dl); DFree(dd);
+  if (e != hipSuccess) return Fail(SMX_DEVICE_ERROR, hipGetErrorString(e));
+  return SMX_OK;
+}
+
+int smx_create_lookup_tables(smx_index* h, const float* queries, int32_t nq, uint8_t* out_lut,
+                             float* out_mult) {
+  if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
+  if (nq <= 0) return nq == 0 ? SMX_OK : Fail(SMX_INVALID_ARGUMENT, "bad nq");
+  std::lock_guard<std::mutex> lock(h->mu);
+  SMX_HIP(hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  const smx::DeviceIndex& ix = h->ix;
+  float *dq = nullptr, *dm = nullptr, *di = nullptr;
+  int8_t* dl = nullptr;
+  uint8_t* du = nullptr;
+  int rc;
+  if ((rc = DAlloc(&dq, size_t(nq) * ix.dim)) || (rc = DAlloc(&dm, nq)) || (rc = DAlloc(&di, nq)) ||
+      (rc = DAlloc(&dl, size_t(nq) * 2 * ix.ksteps * 16)) || (rc = DAlloc(&du, size_t(nq) * ix.nb * 16))) {
+    DFree(dq); DFree(dm); DFree(di); DFree(dl); DFree(du);
+    return rc;
+  }
+  hipError_t e = hipMemcpyAsync(dq, queries, sizeof(float) * size_t(nq) * ix.dim,
+                                hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = smx::LaunchLutBuild(ix, dq, nq, dl, dm, di, du, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(out_lut, du, size_t(nq) * ix.nb * 16, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(out_mult, dm, 4 * size_t(nq), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  DFree(dq); DFree(dm); DFree(di); DFree(dl); DFree(du);
+  if (e != hipSuccess) return Fail(SMX_DEVICE_ERROR, hipGetErrorString(e));
+  return SMX_OK;
+}
+
+int smx_exact_distances(smx_index* h, const float* queries, int32_t nq, const uint32_t* ids,
+                        int32_t k, float* out_dist) {
+  if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
+  if (!h->ix.dataset) return Fail(SMX_FAILED_PRECONDITION, "index has no dataset");
+  if (nq < 0 || k < 0) return Fail(SMX_INVALID_ARGUMENT, "bad sizes");
+  for (size_t i = 0; i < size_t(nq) * k; ++i)
+    if (ids[i] >= h->ix.num_datapoints) return Fail(SMX_INVALID_ARGUMENT, "id out of range");
+  if (nq == 0 || k == 0) return SMX_OK;
+  std::lock_guard<std::mutex> lock(h->mu);
+  SMX_HIP(hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  float *dq = nullptr, *dout = nullptr;
+  uint32_t* dids = nullptr;
+  int rc;
+  if ((rc = DAlloc(&dq, size_t(nq) * h->ix.dim)) || (rc = DAlloc(&dids, size_t(nq) * k)) ||
+      (rc = DAlloc(&dout, size_t(nq) * k))) {
+    DFree(dq); DFree(dids); DFree(dout);
+    return rc;
+  }
+  hipError_t e = hipMemcpyAsync(dq, queries, sizeof(float) * size_t(nq) * h->ix.dim,
+                                hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(dids, ids, 4 * size_t(nq) * k, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = smx::LaunchExactDistances(h->ix, dq, nq, dids, k, dout, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(out_dist, dout, 4 * size_t(nq) * k, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  DFree(dq); DFree(dids); DFree(dout);
+  if (e != hipSuccess) return Fail(SMX_DEVICE_ERROR, hipGetErrorString(e));
+  return SMX_OK;
+}
+
+int smx_lut16_leaf_scores(smx_index* h, int32_t leaf, const uint8_t* lut, int32_t* out_scores) {
+  if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
+  if (leaf < 0 || leaf >= h->ix.nl) return Fail(SMX_INVALID_ARGUMENT, "leaf out of range");
+  std::lock_guard<std::mutex> lock(h->mu);
+  SMX_HIP(hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  const smx::DeviceIndex& ix = h->ix;
+  const int rows = 2 * ix.ksteps;
+  std::vector<int8_t> l8(size_t(rows) * 16, 0);
+  for (int i = 0; i < ix.nb * 16; ++i) l8[i] = int8_t(int(lut[i]) - 128);
+  uint64_t n64 = 0;
+  SMX_HIP(hipMemcpy(&n64, ix.member_off + leaf + 1, 8, hipMemcpyDeviceToHost));
+  uint64_t b64 = 0;
+  SMX_HIP(hipMemcpy(&b64, ix.member_off + leaf, 8, hipMemcpyDeviceToHost));
+  const size_t n = size_t(n64 - b64);
+  int8_t* dl = nullptr;
+  int32_t* dout = nullptr;
+  int rc;
+  if ((rc = DAlloc(&dl, l8.size())) || (rc = DAlloc(&dout, std::max<size_t>(n, 1)))) {
+    DFree(dl); DFree(dout);
+    return rc;
+  }
+  hipError_t e = hipMemcpyAsync(dl, l8.data(), l8.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = smx::LaunchLeafScores(ix, leaf, dl, dout, s);
+  if (e == hipSuccess && n) e = hipMemcpyAsync(out_scores, dout, 4 * n, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  DFree(dl); DFree(dout);
+  if (e != hipSuccess) return Fail(SMX_DEVICE_ERROR, hipGetErrorString(e));
+  return SMX_OK;
+}
+
+int smx_set_profiling(smx_index* h, int32_t enabled) {
+  if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
+  h->profiling = enabled != 0;
+  return SMX_OK;
+}
+
+int smx_get_timings(const smx_index* h, smx_timings* out) {
+  if (!h || !out) return Fail(SMX_INVALID_ARGUMENT, "null argument");
+  *out = h->timings;
+  return SMX_OK;
+}
+
+int smx_set_tuning(smx_index* h, int32_t candidates_per_query, int32_t seed_leaves) {
+  if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
+  if (candidates_per_query < 32 || candidates_per_query > 16384)
+    return Fail(SMX_INVALID_ARGUMENT, "candidates_per_query must be in [32, 16384]");
+  if (seed_leaves < 0) return Fail(SMX_INVALID_ARGUMENT, "seed_leaves must be >= 0");
+  std::lock_guard<std::mutex> lock(h->mu);
+  h->cap_per_query = uint32_t(candidates_per_query);
+  h->seed_leaves = seed_leaves;
+  return SMX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,161 @@
+"""Host-side representation of a tree-AH (LUT16) index.
+
+This is the data the query path consumes: leaf centers,
+the AH codebook, per-leaf member lists with their 4-bit codes, and the float
+rows used for exact reordering.  It corresponds to what the reference keeps
+inside ``TreeAHHybridResidual`` (``datapoints_by_token_``, the leaf
+searchers' packed codes and the partitioner's centers;
+scann/tree_x_hybrid/tree_ah_hybrid_residual.h:293-320) and to the assets
+``load_searcher`` reads (scann/scann_ops/cc/scann.cc:105-233).
+
+``IndexDesc`` is the ctypes mirror of ``smx_index_desc``
+(include/scann_mi355x.h); the oracle's ``orc_index`` has the same layout.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+from typing import Optional
+
+import numpy as np
+
+METRIC_DOT = 0
+METRIC_SQUARED_L2 = 1
+METRIC_NAMES = {"dot_product": METRIC_DOT, "squared_l2": METRIC_SQUARED_L2}
+
+
+class IndexDesc(ctypes.Structure):
+    """ctypes mirror of smx_index_desc / orc_index (identical layout)."""
+
+    _fields_ = [
+        ("metric", ctypes.c_int32),
+        ("dim", ctypes.c_int32),
+        ("num_leaves", ctypes.c_int32),
+        ("num_blocks", ctypes.c_int32),
+        ("dims_per_block", ctypes.c_int32),
+        ("residual", ctypes.c_int32),
+        ("centers", ctypes.c_void_p),
+        ("codebook", ctypes.c_void_p),
+        ("leaf_offsets", ctypes.c_void_p),
+        ("leaf_members", ctypes.c_void_p),
+        ("member_codes", ctypes.c_void_p),
+        ("num_datapoints", ctypes.c_uint32),
+        ("dataset", ctypes.c_void_p),
+        ("spilling_overretrieve_factor", ctypes.c_float),
+        ("pad_", ctypes.c_int32),
+    ]
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data
+
+
+@dataclasses.dataclass
+class TreeAHIndex:
+    metric: int
+    dim: int
+    num_blocks: int
+    dims_per_block: int
+    residual: bool
+    centers: np.ndarray          # float32 [L, D]
+    codebook: np.ndarray         # float32 [B, 16, dims_per_block]
+    leaf_offsets: np.ndarray     # uint64 [L+1]
+    leaf_members: np.ndarray     # uint32 [M], ascending within each leaf
+    member_codes: np.ndarray     # uint8 [M, B]
+    num_datapoints: int
+    dataset: Optional[np.ndarray] = None   # float32 [N, D] (exact reorder)
+    spilling_overretrieve_factor: float = 2.0
+
+    def __post_init__(self):
+        self.centers = np.ascontiguousarray(self.centers, dtype=np.float32)
+        self.codebook = np.ascontiguousarray(self.codebook, dtype=np.float32)
+        self.leaf_offsets = np.ascontiguousarray(self.leaf_offsets, dtype=np.uint64)
+        self.leaf_members = np.ascontiguousarray(self.leaf_members, dtype=np.uint32)
+        self.member_codes = np.ascontiguousarray(self.member_codes, dtype=np.uint8)
+        if self.dataset is not None:
+            self.dataset = np.ascontiguousarray(self.dataset, dtype=np.float32)
+        self.validate()
+
+    @property
+    def num_leaves(self) -> int:
+        return int(self.centers.shape[0])
+
+    @property
+    def num_members(self) -> int:
+        return int(self.leaf_members.shape[0])
+
+    @property
+    def disjoint(self) -> bool:
+        return self.num_members == self.num_datapoints
+
+    def leaf_sizes(self) -> np.ndarray:
+        return np.diff(self.leaf_offsets).astype(np.int64)
+
+    def validate(self) -> None:
+        L, D = self.centers.shape
+        if D != self.dim:
+            raise ValueError(f"centers dim {D} != dim {self.dim}")
+        B, dpb = self.num_blocks, self.dims_per_block
+        last = self.dim - dpb * (B - 1)
+        if not (0 < last <= dpb):
+            raise ValueError(f"{B} blocks of {dpb} dims do not tile dim {self.dim}")
+        if self.codebook.shape != (B, 16, dpb):
+            raise ValueError(f"codebook shape {self.codebook.shape} != {(B, 16, dpb)}")
+        if self.leaf_offsets.shape != (L + 1,) or self.leaf_offsets[0] != 0:
+            raise ValueError("leaf_offsets must have num_leaves+1 entries starting at 0")
+        if np.any(np.diff(self.leaf_offsets.astype(np.int64)) < 0):
+            raise ValueError("leaf_offsets must be non-decreasing")
+        M = int(self.leaf_offsets[-1])
+        if self.leaf_members.shape != (M,):
+            raise ValueError("leaf_members size mismatch")
+        if self.member_codes.shape != (M, B):
+            raise ValueError("member_codes shape mismatch")
+        if M and int(self.member_codes.max()) > 15:
+            raise ValueError("codes must be 4-bit (LUT16)")
+        if M and int(self.leaf_members.max()) >= self.num_datapoints:
+            raise ValueError("member id out of range")
+        if self.dataset is not None and self.dataset.shape != (self.num_datapoints, self.dim):
+            raise ValueError("dataset shape mismatch")
+
+    def desc(self) -> IndexDesc:
+        """Borrowed-pointer descriptor; keep ``self`` alive while it is used."""
+        return IndexDesc(
+            metric=self.metric, dim=self.dim, num_leaves=self.num_leaves,
+            num_blocks=self.num_blocks, dims_per_block=self.dims_per_block,
+            residual=int(bool(self.residual)),
+            centers=_ptr(self.centers), codebook=_ptr(self.codebook),
+            leaf_offsets=_ptr(self.leaf_offsets), leaf_members=_ptr(self.leaf_members),
+            member_codes=_ptr(self.member_codes), num_datapoints=self.num_datapoints,
+            dataset=_ptr(self.dataset),
+            spilling_overretrieve_factor=float(self.spilling_overretrieve_factor), pad_=0)
+
+    # -- serialization (own format; reference proto assets are SURVEY §8f-2) --
+    def save(self, directory: str) -> None:
+        import json
+        import os
+        os.makedirs(directory, exist_ok=True)
+        meta = dict(metric=self.metric, dim=self.dim, num_blocks=self.num_blocks,
+                    dims_per_block=self.dims_per_block, residual=bool(self.residual),
+                    num_datapoints=self.num_datapoints,
+                    spilling_overretrieve_factor=self.spilling_overretrieve_factor,
+                    has_dataset=self.dataset is not None)
+        with open(os.path.join(directory, "smx_index.json"), "w") as f:
+            json.dump(meta, f)
+        for name in ("centers", "codebook", "leaf_offsets", "leaf_members", "member_codes"):
+            np.save(os.path.join(directory, f"{name}.npy"), getattr(self, name))
+        if self.dataset is not None:
+            np.save(os.path.join(directory, "dataset.npy"), self.dataset)
+
+    @classmethod
+    def load(cls, directory: str) -> "TreeAHIndex":
+        import json
+        import os
+        with open(os.path.join(directory, "smx_index.json")) as f:
+            meta = json.load(f)
+        arr = {n: np.load(os.path.join(directory, f"{n}.npy"))
+               for n in ("centers", "codebook", "leaf_offsets", "leaf_members", "member_codes")}
+        ds = np.load(os.path.join(directory, "dataset.npy")) if meta["has_dataset"] else None
+        return cls(metric=meta["metric"], dim=meta["dim"], num_blocks=meta["num_blocks"],
+                   dims_per_block=meta["dims_per_block"], residual=meta["residual"],
+                   num_datapoints=meta["num_datapoints"], dataset=ds,
+                   spilling_overretrieve_factor=meta["spilling_overretrieve_factor"], **arr)

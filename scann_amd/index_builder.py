@@ -1,0 +1,155 @@
+"""Index construction for the tree-AH (LUT16) searcher.
+
+Build time is outside the hot path of this tier (SURVEY.md §8f-3 ranks the
+GPU index builder as a "next" row).  This module trains what the query path
+needs so that the searcher can be used end to end from the reference's
+builder API:
+
+* the k-means partitioner (squared-L2 partitioning distance, random
+  initialisation, ``training_iterations`` rounds on a ``training_sample_size``
+  sample; reference: scann/utils/gmm_utils.cc, kmeans_tree_partitioner.cc);
+* database tokenization by squared-L2 top-1 with ``datapoints_by_token``
+  sorted by global id (kmeans_tree_partitioner.cc:477-620, 532-535);
+* residuals against the assigned center for tree + dot product
+  (tree_ah_hybrid_residual.cc:185-224, scann_builder.py:429-431);
+* one 16-center k-means codebook per block (asymmetric_hashing_impl.cc:41-198)
+  and nearest-center encoding.  Anisotropic (AVQ) noise shaping and SOAR
+  spilling are NOT reproduced; the searcher accepts indexes that use them
+  (spilled members, any codes) but this builder does not produce them.
+
+Uses torch on the GPU when one is visible (dense distance blocks), numpy
+otherwise; results differ only in training floating-point noise, which no
+parity claim depends on.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import numpy as np
+
+from .index import METRIC_DOT, TreeAHIndex
+
+
+def _torch_device():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return torch, torch.device("cuda")
+    except Exception:  # pragma: no cover - torch is optional for building
+        pass
+    return None, None
+
+
+def _assign_l2(x: np.ndarray, centers: np.ndarray, chunk: int = 1 << 16) -> np.ndarray:
+    """argmin_c ||x - c||^2 for every row of x (ties -> lowest index)."""
+    torch, dev = _torch_device()
+    out = np.empty(x.shape[0], dtype=np.int64)
+    if torch is not None:
+        c = torch.from_numpy(centers).to(dev)
+        cn = (c * c).sum(1)
+        for s in range(0, x.shape[0], chunk):
+            xb = torch.from_numpy(x[s:s + chunk]).to(dev)
+            d = cn[None, :] - 2.0 * (xb @ c.T)
+            out[s:s + chunk] = d.argmin(1).cpu().numpy()
+        return out
+    cn = (centers * centers).sum(1)
+    for s in range(0, x.shape[0], chunk):
+        d = cn[None, :] - 2.0 * (x[s:s + chunk] @ centers.T)
+        out[s:s + chunk] = d.argmin(1)
+    return out
+
+
+def kmeans(x: np.ndarray, k: int, iterations: int, seed: int,
+           sample_size: Optional[int] = None) -> np.ndarray:
+    """Lloyd's k-means with random initialisation; empty clusters re-seeded."""
+    rng = np.random.default_rng(seed)
+    n = x.shape[0]
+    if sample_size is not None and n > sample_size:
+        x = x[np.sort(rng.choice(n, sample_size, replace=False))]
+        n = sample_size
+    if k >= n:
+        c = np.zeros((k, x.shape[1]), np.float32)
+        c[:n] = x
+        return c
+    centers = x[rng.choice(n, k, replace=False)].astype(np.float32, copy=True)
+    for _ in range(iterations):
+        lab = _assign_l2(x, centers)
+        sums = np.zeros_like(centers, dtype=np.float64)
+        np.add.at(sums, lab, x)
+        cnt = np.bincount(lab, minlength=k)
+        nz = cnt > 0
+        centers[nz] = (sums[nz] / cnt[nz, None]).astype(np.float32)
+        if (~nz).any():
+            centers[~nz] = x[rng.choice(n, int((~nz).sum()), replace=False)]
+    return centers
+
+
+def _block_view(v: np.ndarray, num_blocks: int, dpb: int) -> np.ndarray:
+    """[n, D] -> [n, B, dpb] with the last block zero-padded."""
+    n, d = v.shape
+    pad = num_blocks * dpb - d
+    if pad:
+        v = np.concatenate([v, np.zeros((n, pad), v.dtype)], axis=1)
+    return v.reshape(n, num_blocks, dpb)
+
+
+def train_codebook(residuals: np.ndarray, num_blocks: int, dpb: int,
+                   iterations: int, seed: int) -> np.ndarray:
+    blocks = _block_view(residuals, num_blocks, dpb)
+    cb = np.zeros((num_blocks, 16, dpb), np.float32)
+    for b in range(num_blocks):
+        cb[b] = kmeans(np.ascontiguousarray(blocks[:, b, :]), 16, iterations, seed + 7919 * b)
+    return cb
+
+
+def encode(residuals: np.ndarray, codebook: np.ndarray, chunk: int = 1 << 15) -> np.ndarray:
+    """Nearest codebook center per block (squared L2), uint8 [n, B]."""
+    num_blocks, _, dpb = codebook.shape
+    n = residuals.shape[0]
+    out = np.empty((n, num_blocks), np.uint8)
+    torch, dev = _torch_device()
+    if torch is not None:
+        cb = torch.from_numpy(codebook).to(dev)
+        for s in range(0, n, chunk):
+            r = torch.from_numpy(_block_view(residuals[s:s + chunk], num_blocks, dpb)).to(dev)
+            d = ((r[:, :, None, :] - cb[None]) ** 2).sum(-1)
+            out[s:s + chunk] = d.argmin(-1).to(torch.uint8).cpu().numpy()
+        return out
+    for s in range(0, n, chunk):
+        r = _block_view(residuals[s:s + chunk], num_blocks, dpb)
+        d = ((r[:, :, None, :] - codebook[None]) ** 2).sum(-1)
+        out[s:s + chunk] = d.argmin(-1)
+    return out
+
+
+def build_tree_ah(db: np.ndarray, metric: int, num_leaves: int,
+                  dims_per_block: int = 2, *, training_sample_size: int = 100000,
+                  training_iterations: int = 12, ah_training_iterations: int = 10,
+                  ah_training_sample_size: int = 100000, residual: Optional[bool] = None,
+                  keep_dataset: bool = True, seed: int = 0) -> TreeAHIndex:
+    db = np.ascontiguousarray(db, dtype=np.float32)
+    n, dim = db.shape
+    if residual is None:
+        residual = metric == METRIC_DOT
+    num_leaves = max(1, min(num_leaves, n))
+    centers = kmeans(db, num_leaves, training_iterations, seed, training_sample_size)
+    labels = _assign_l2(db, centers)
+    order = np.argsort(labels, kind="stable")   # members ascending by id per leaf
+    counts = np.bincount(labels, minlength=num_leaves)
+    offsets = np.zeros(num_leaves + 1, np.uint64)
+    offsets[1:] = np.cumsum(counts)
+    members = order.astype(np.uint32)
+    num_blocks = int(math.ceil(dim / dims_per_block))
+    resid = db[members] - centers[labels[members]] if residual else db[members]
+    rng = np.random.default_rng(seed + 1)
+    samp = resid
+    if resid.shape[0] > ah_training_sample_size:
+        samp = resid[np.sort(rng.choice(resid.shape[0], ah_training_sample_size, replace=False))]
+    codebook = train_codebook(samp, num_blocks, dims_per_block, ah_training_iterations, seed + 2)
+    codes = encode(resid, codebook)
+    return TreeAHIndex(metric=metric, dim=dim, num_blocks=num_blocks,
+                       dims_per_block=dims_per_block, residual=bool(residual),
+                       centers=centers, codebook=codebook, leaf_offsets=offsets,
+                       leaf_members=members, member_codes=codes, num_datapoints=n,
+                       dataset=db if keep_dataset else None)
