@@ -40,6 +40,7 @@ struct DeviceIndex {
   uint32_t* leaf_size = nullptr;// [nl]
   uint64_t* member_off = nullptr; // [nl+1]
   uint32_t* members = nullptr;  // [num_members]
+  uint32_t* leaf_order = nullptr; // [nl] leaves by descending size
   float* dataset = nullptr;     // [num_datapoints][dim] or null
 };
 
@@ -53,10 +54,11 @@ struct ScanArgs {
   const float* inv;           // [nq]
   const uint32_t* pair_q;     // queries grouped by leaf
   const float* pair_bias;     // partition distance per pair (residual)
-  const uint32_t* pair_off;   // [nl+1]
-  const uint32_t* tile_prefix;// [nl+1] query tiles per leaf, prefix
-  const uint32_t* tile_leaf;  // [work items] leaf of each query tile
-  const uint64_t* tau_key;    // [nq] emission threshold, or null (emit all)
+  const uint32_t* pair_off;   // [nl] first pair of each leaf
+  const uint32_t* leaf_count; // [nl] pairs of each leaf
+  const uint32_t* tile_prefix;// [nl+1] work items, largest leaf first
+  const uint2* work;          // [work items] (leaf, query tile within leaf)
+  const uint64_t* tau_key;    // [nq] emission threshold keys
   uint64_t* cand;             // [nq][cap]
   uint32_t* cand_count;       // [nq]
   uint32_t* work_counter;
@@ -64,6 +66,21 @@ struct ScanArgs {
   int nl;
   int nb;
   int shift;
+  int residual;
+};
+
+struct SeedArgs {
+  const int32_t* topl_leaf;   // [nq][L]
+  const float* topl_dist;     // [nq][L]
+  const int8_t* lut;          // [nq][2K][16]
+  const float* inv;
+  const uint8_t* tiles;
+  const uint64_t* tile_off;
+  const uint32_t* leaf_size;
+  uint64_t* tau_key;
+  int L;
+  int seed;
+  int kk;
   int residual;
 };
 
@@ -99,17 +116,14 @@ hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq,
                           int8_t* lut, float* mult, float* inv, uint8_t* lut_u8,
                           hipStream_t s);
 hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf,
-                       const float* topl_dist, int nq, int L, int seed_leaves,
-                       uint32_t* cnt /*[2][nl]*/, uint32_t* fill /*[2][nl]*/,
-                       uint32_t* pair_off /*[2][nl+1]*/,
-                       uint32_t* tile_prefix /*[2][nl+1]*/,
-                       uint32_t* pair_q /*[2][nq*L]*/, float* pair_bias /*[2][nq*L]*/,
-                       uint32_t* tile_leaf /*[2][max_items]*/, uint32_t max_items,
-                       unsigned long long* code_bytes /*[2]*/, hipStream_t s);
+                       const float* topl_dist, int nq, int L, uint32_t* cnt /*[nl]*/,
+                       uint32_t* fill /*[nl]*/, uint32_t* pair_off /*[nl+1]*/,
+                       uint32_t* tile_prefix /*[nl+1]*/, uint32_t* pair_q /*[nq*L]*/,
+                       float* pair_bias /*[nq*L]*/, uint2* work /*[max items]*/,
+                       uint32_t* totals /*[2] pairs, items*/,
+                       unsigned long long* code_bytes /*[1]*/, hipStream_t s);
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, hipStream_t s);
-hipError_t LaunchSeedSelect(const uint64_t* seed_cand, const uint32_t* seed_count,
-                            uint32_t seed_cap, int nq, int kk, uint64_t* tau_key,
-                            hipStream_t s);
+hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s);
 hipError_t LaunchTighten(const uint64_t* cand, const uint32_t* cand_count, uint32_t cap,
                          int nq, int kk, uint64_t* tau_key, hipStream_t s);
 hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s);

@@ -186,47 +186,41 @@ __global__ void __launch_bounds__(256) lut_build_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Invert (query -> leaves) into (leaf -> queries), split into the seed set
-// (rank < seed_leaves) and the main set.
+// Invert (query -> leaves) into (leaf -> queries) and cut every leaf's query
+// list into 32-query work items, listed largest leaf first (longest items
+// dequeued first).
 // ---------------------------------------------------------------------------
-__global__ void pairs_count_kernel(const int32_t* __restrict__ topl_leaf, int nq, int L,
-                                   int seed_leaves, int nl, uint32_t* __restrict__ cnt,
+__global__ void pairs_count_kernel(const int32_t* __restrict__ topl_leaf, int n,
+                                   uint32_t* __restrict__ cnt,
                                    const uint32_t* __restrict__ leaf_size, int nb,
                                    unsigned long long* __restrict__ code_bytes) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nq * L) return;
+  if (i >= n) return;
   const int leaf = topl_leaf[i];
   if (leaf < 0) return;
-  const unsigned long long bytes = 16ull * nb * ((leaf_size[leaf] + 31u) / 32u);
-  atomicAdd(&cnt[nl + leaf], 1u);           // main set: every pair
-  atomicAdd(&code_bytes[1], bytes);
-  if ((i % L) < seed_leaves) {              // seed set: the first ranks
-    atomicAdd(&cnt[leaf], 1u);
-    atomicAdd(&code_bytes[0], bytes);
-  }
+  atomicAdd(&cnt[leaf], 1u);
+  atomicAdd(code_bytes, 16ull * nb * ((leaf_size[leaf] + 31u) / 32u));
 }
 
 __global__ void __launch_bounds__(1024) pairs_scan_kernel(const uint32_t* __restrict__ cnt,
+                                                          const uint32_t* __restrict__ order,
                                                           int nl, uint32_t* __restrict__ pair_off,
-                                                          uint32_t* __restrict__ tile_prefix) {
+                                                          uint32_t* __restrict__ tile_prefix,
+                                                          uint32_t* __restrict__ totals) {
   __shared__ uint32_t s_pairs[1024];
   __shared__ uint32_t s_tiles[1024];
-  const int set = blockIdx.x;
-  const uint32_t* c = cnt + size_t(set) * nl;
-  uint32_t* po = pair_off + size_t(set) * (nl + 1);
-  uint32_t* tp = tile_prefix + size_t(set) * (nl + 1);
   const int per = (nl + blockDim.x - 1) / blockDim.x;
   const int beg = threadIdx.x * per;
   const int end = min(nl, beg + per);
   uint32_t sp = 0, st = 0;
-  for (int l = beg; l < end; ++l) {
-    sp += c[l];
-    st += (c[l] + kQueriesPerTile - 1) / kQueriesPerTile;
+  for (int p = beg; p < end; ++p) {
+    const uint32_t c = cnt[order[p]];
+    sp += c;
+    st += (c + kQueriesPerTile - 1) / kQueriesPerTile;
   }
   s_pairs[threadIdx.x] = sp;
   s_tiles[threadIdx.x] = st;
   __syncthreads();
-  // Hillis-Steele inclusive scan over 1024 partial sums.
   for (int off = 1; off < int(blockDim.x); off <<= 1) {
     uint32_t a = 0, b = 0;
     if (int(threadIdx.x) >= off) {
@@ -240,47 +234,43 @@ __global__ void __launch_bounds__(1024) pairs_scan_kernel(const uint32_t* __rest
   }
   uint32_t rp = threadIdx.x ? s_pairs[threadIdx.x - 1] : 0;
   uint32_t rt = threadIdx.x ? s_tiles[threadIdx.x - 1] : 0;
-  for (int l = beg; l < end; ++l) {
-    po[l] = rp;
-    tp[l] = rt;
-    rp += c[l];
-    rt += (c[l] + kQueriesPerTile - 1) / kQueriesPerTile;
+  for (int p = beg; p < end; ++p) {
+    const uint32_t leaf = order[p];
+    const uint32_t c = cnt[leaf];
+    pair_off[leaf] = rp;
+    tile_prefix[p] = rt;
+    rp += c;
+    rt += (c + kQueriesPerTile - 1) / kQueriesPerTile;
   }
   if (threadIdx.x == blockDim.x - 1) {
-    po[nl] = s_pairs[blockDim.x - 1];
-    tp[nl] = s_tiles[blockDim.x - 1];
+    tile_prefix[nl] = s_tiles[blockDim.x - 1];
+    totals[0] = s_pairs[blockDim.x - 1];
+    totals[1] = s_tiles[blockDim.x - 1];
   }
 }
 
 __global__ void pairs_scatter_kernel(const int32_t* __restrict__ topl_leaf,
-                                     const float* __restrict__ topl_dist, int nq, int L,
-                                     int seed_leaves, int nl, const uint32_t* __restrict__ pair_off,
+                                     const float* __restrict__ topl_dist, int n, int L,
+                                     const uint32_t* __restrict__ pair_off,
                                      uint32_t* __restrict__ fill, uint32_t* __restrict__ pair_q,
                                      float* __restrict__ pair_bias) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nq * L) return;
+  if (i >= n) return;
   const int leaf = topl_leaf[i];
   if (leaf < 0) return;
-  const int nsets = (i % L) < seed_leaves ? 2 : 1;
-  for (int k = 0; k < nsets; ++k) {
-    const int set = 1 - k;  // main first, then seed
-    const uint32_t pos = pair_off[size_t(set) * (nl + 1) + leaf] +
-                         atomicAdd(&fill[set * nl + leaf], 1u);
-    const size_t base = size_t(set) * nq * L;
-    pair_q[base + pos] = uint32_t(i / L);
-    pair_bias[base + pos] = topl_dist[i];
-  }
+  const uint32_t pos = pair_off[leaf] + atomicAdd(&fill[leaf], 1u);
+  pair_q[pos] = uint32_t(i / L);
+  pair_bias[pos] = topl_dist[i];
 }
 
-// Work item (query tile) -> leaf map for both sets.
-__global__ void pairs_tiles_kernel(const uint32_t* __restrict__ tile_prefix, int nl,
-                                   uint32_t* __restrict__ tile_leaf, uint32_t max_items) {
-  const int set = blockIdx.y;
-  const int leaf = blockIdx.x * blockDim.x + threadIdx.x;
-  if (leaf >= nl) return;
-  const uint32_t* tp = tile_prefix + size_t(set) * (nl + 1);
-  uint32_t* tl = tile_leaf + size_t(set) * max_items;
-  for (uint32_t t = tp[leaf]; t < tp[leaf + 1]; ++t) tl[t] = uint32_t(leaf);
+__global__ void pairs_work_kernel(const uint32_t* __restrict__ tile_prefix,
+                                  const uint32_t* __restrict__ order, int nl,
+                                  uint2* __restrict__ work) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nl) return;
+  const uint32_t leaf = order[p];
+  for (uint32_t w = tile_prefix[p]; w < tile_prefix[p + 1]; ++w)
+    work[w] = make_uint2(leaf, w - tile_prefix[p]);
 }
 
 // ---------------------------------------------------------------------------
@@ -300,14 +290,18 @@ __global__ void pairs_tiles_kernel(const uint32_t* __restrict__ tile_prefix, int
 // whose distance can pass, found by bisection: d is monotone in S) is
 // converted.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ v4i OneHot16(uint32_t t) {
-  const uint32_t one = 1u << ((t & 3u) << 3);
-  const uint32_t g = t >> 2;
+// 16-byte one-hot of nibble t (byte t = 1): 1 << 8(t mod 8) in the 64-bit
+// half selected by bit 3.  `sh` = 8 * t (bits 3..6), so the 64-bit shift
+// uses sh & 63 and bit 6 of sh picks the half.
+__device__ __forceinline__ v4i OneHot16(uint32_t sh) {
+  const uint64_t x = 1ull << (sh & 63u);
+  const uint32_t lo = uint32_t(x), hi = uint32_t(x >> 32);
+  const uint32_t m = 0u - ((sh >> 6) & 1u);  // all ones when t >= 8
   v4i r;
-  r[0] = g == 0 ? int(one) : 0;
-  r[1] = g == 1 ? int(one) : 0;
-  r[2] = g == 2 ? int(one) : 0;
-  r[3] = g == 3 ? int(one) : 0;
+  r[0] = int(lo & ~m);
+  r[1] = int(hi & ~m);
+  r[2] = int(lo & m);
+  r[3] = int(hi & m);
   return r;
 }
 
@@ -331,8 +325,10 @@ __device__ __forceinline__ v16i TileSums(const uint32_t* codes, const v4i* frag)
   v16i acc = {0};
 #pragma unroll
   for (int s = 0; s < K; ++s) {
-    const uint32_t nib = (codes[s >> 3] >> ((s & 7) * 4)) & 15u;
-    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(OneHot16(nib), frag[s], acc, 0, 0, 0);
+    const int sh = (s & 7) * 4;
+    const uint32_t w = codes[s >> 3];
+    const uint32_t e8 = sh >= 3 ? ((w >> (sh - 3)) & 0x78u) : ((w << 3) & 0x78u);
+    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(OneHot16(e8), frag[s], acc, 0, 0, 0);
   }
   return acc;
 }
@@ -367,10 +363,11 @@ __global__ void __launch_bounds__(256) lut16_scan_kernel(ScanArgs a) {
     if (lane == 0) w = atomicAdd(a.work_counter, 1u);
     w = __builtin_amdgcn_readfirstlane(__shfl(w, 0));
     if (w >= total) break;
-    const int leaf = int(a.tile_leaf[w]);
-    const uint32_t t = w - a.tile_prefix[leaf];
+    const uint2 item = a.work[w];
+    const int leaf = int(__builtin_amdgcn_readfirstlane(item.x));
+    const uint32_t t = __builtin_amdgcn_readfirstlane(item.y);
     const uint32_t pbeg = a.pair_off[leaf] + t * kQueriesPerTile;
-    const uint32_t pend = a.pair_off[leaf + 1];
+    const uint32_t pend = a.pair_off[leaf] + a.leaf_count[leaf];
     const int nvalid = int(min(uint32_t(kQueriesPerTile), pend - pbeg));
     const bool valid = c < nvalid;
     const uint32_t pidx = pbeg + uint32_t(valid ? c : 0);
@@ -381,8 +378,9 @@ __global__ void __launch_bounds__(256) lut16_scan_kernel(ScanArgs a) {
     const v4i* lrow = reinterpret_cast<const v4i*>(a.lut + size_t(qid) * (2 * K) * 16);
 #pragma unroll
     for (int s = 0; s < K; ++s) frag[s] = lrow[2 * s + h];
-    const uint64_t T = a.tau_key ? a.tau_key[qid] : kNoThreshold;
-    const int amax = (T == kNoThreshold)
+    const uint64_t T = a.tau_key[qid];
+    const int amax = !valid ? smin - 1
+                     : (T == kNoThreshold)
                          ? smax
                          : SumLimit(FromOrdered(uint32_t(T >> 32)), inv, bias, smin, smax);
     const uint32_t n = a.leaf_size[leaf];
@@ -394,25 +392,125 @@ __global__ void __launch_bounds__(256) lut16_scan_kernel(ScanArgs a) {
     for (uint32_t j = 0; j < ntile; ++j) {
       if (j + 1 < ntile) LoadCodes<K>(tb + size_t(j + 1) * 64 * W, next);
       const v16i acc = TileSums<K>(codes, frag);
+      // rows of this lane: (i & 3) + 8 * (i >> 2) + 4 * h of tile j
+      const uint32_t rows_left = n - j * kDpPerTile;  // > 0
+      uint32_t pass = 0;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const uint32_t row = (i & 3) + 8 * (i >> 2) + 4 * h;
-        const uint32_t dp = j * kDpPerTile + row;
-        if (valid && dp < n && acc[i] <= amax) {
-          const float d = DistOf(acc[i], inv, bias);
-          const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp)
-                                           : a.members[moff + dp];
-          const uint64_t key = (uint64_t(OrderedBits(d)) << 32) | tie;
-          if (key <= T) {
-            const uint32_t slot = atomicAdd(&a.cand_count[qid], 1u);
-            if (slot < a.cap) a.cand[size_t(qid) * a.cap + slot] = key;
+        pass |= uint32_t((row < rows_left) & (acc[i] <= amax)) << i;
+      }
+      if (pass) {
+        // Rare path: build keys, keep those <= T, one atomic per lane.
+        uint64_t keys[16];
+        uint32_t m = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          if (pass >> i & 1u) {
+            const uint32_t dp = j * kDpPerTile + (i & 3) + 8 * (i >> 2) + 4 * h;
+            const float d = DistOf(acc[i], inv, bias);
+            const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp)
+                                             : a.members[moff + dp];
+            const uint64_t key = (uint64_t(OrderedBits(d)) << 32) | tie;
+            if (key <= T) keys[m++] = key;
           }
+        }
+        if (m) {
+          const uint32_t slot = atomicAdd(&a.cand_count[qid], m);
+          uint64_t* dst = a.cand + size_t(qid) * a.cap;
+          for (uint32_t u = 0; u < m && slot + u < a.cap; ++u) dst[slot + u] = keys[u];
         }
       }
 #pragma unroll
       for (int i = 0; i < NW; ++i) codes[i] = next[i];
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Per-query threshold from the query's first `seed` leaves: every datapoint
+// there is scored with the int8 LUT held in LDS, and the k'-th smallest
+// distance (radix select over the order-preserving bits) bounds the final
+// k'-th from above.  The main pass rescans those leaves, so storing only the
+// first kSeedCap values is still correct (a subset's k'-th is a bound).
+// ---------------------------------------------------------------------------
+constexpr int kSeedCap = 12288;
+
+template <int K>
+__global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
+  constexpr int NW = ((((K + 1) / 2) + 3) / 4);
+  constexpr int W = 4 * NW;
+  __shared__ int8_t lut[2 * K * 16];
+  __shared__ uint32_t vals[kSeedCap];
+  __shared__ uint32_t hist[2048];
+  __shared__ uint32_t s_n, s_bin, s_rem;
+  const int qi = blockIdx.x;
+  for (int e = threadIdx.x; e < 2 * K * 16; e += blockDim.x)
+    lut[e] = a.lut[size_t(qi) * 2 * K * 16 + e];
+  const float inv = a.inv[qi];
+  __syncthreads();
+  uint32_t base = 0;
+  for (int r = 0; r < a.seed && base < uint32_t(kSeedCap); ++r) {
+    const int leaf = a.topl_leaf[size_t(qi) * a.L + r];
+    if (leaf < 0) break;
+    const float bias = a.residual ? a.topl_dist[size_t(qi) * a.L + r] : 0.0f;
+    const uint32_t n = min(a.leaf_size[leaf], uint32_t(kSeedCap) - base);
+    const uint8_t* tb = a.tiles + a.tile_off[leaf] * 64ull * W;
+    for (uint32_t dp = threadIdx.x; dp < n; dp += blockDim.x) {
+      const uint8_t* t0 = tb + ((dp >> 5) * 64 + (dp & 31)) * W;
+      uint32_t c0[NW], c1[NW];
+      LoadCodes<K>(t0, c0);
+      LoadCodes<K>(t0 + 32 * W, c1);
+      int acc = 0;
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        const uint32_t n0 = (c0[s >> 3] >> ((s & 7) * 4)) & 15u;
+        const uint32_t n1 = (c1[s >> 3] >> ((s & 7) * 4)) & 15u;
+        acc += int(lut[(2 * s) * 16 + n0]) + int(lut[(2 * s + 1) * 16 + n1]);
+      }
+      vals[base + dp] = OrderedBits(DistOf(acc, inv, bias));
+    }
+    base += n;
+  }
+  __syncthreads();
+  const uint32_t total = base;
+  const uint32_t kk = uint32_t(a.kk);
+  if (kk == 0 || total < kk) return;  // no bound: the threshold stays open
+  // Radix select of the kk-th smallest value: 11 + 11 + 10 bits.
+  uint32_t prefix = 0, rem = kk;
+  const int shifts[3] = {21, 10, 0};
+  const int widths[3] = {11, 11, 10};
+  for (int pass = 0; pass < 3; ++pass) {
+    const int sh = shifts[pass], wd = widths[pass];
+    const uint32_t nb = 1u << wd;
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    const int hs = sh + wd;  // bits above this digit must equal the prefix
+    for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) {
+      const uint32_t v = vals[i];
+      const bool match = (hs >= 32) || ((v >> hs) == (prefix >> hs));
+      if (match) atomicAdd(&hist[(v >> sh) & (nb - 1)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t cum = 0, b = 0;
+      for (; b < nb; ++b) {
+        if (cum + hist[b] >= rem) break;
+        cum += hist[b];
+      }
+      s_bin = b;
+      s_rem = rem - cum;
+    }
+    __syncthreads();
+    prefix |= s_bin << sh;
+    rem = s_rem;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const uint64_t t = (uint64_t(prefix) << 32) | 0xFFFFFFFFull;
+    if (t < a.tau_key[qi]) a.tau_key[qi] = t;
+  }
+  (void)s_n;
 }
 
 // One-query variant for the stage entry point: raw sums of one leaf.
@@ -443,27 +541,6 @@ __global__ void __launch_bounds__(64) leaf_scores_kernel(const uint8_t* __restri
       }
     }
   }
-}
-
-// ---------------------------------------------------------------------------
-// Seed selection: the k'-th best key among a query's seed-leaf candidates is
-// a valid threshold for the whole scan (every stored key is a genuine
-// candidate, so the k'-th of any subset bounds the final k'-th from above).
-// The main pass rescans the seed leaves, so nothing here must be complete.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) seed_select_kernel(
-    const uint64_t* __restrict__ seed_cand, const uint32_t* __restrict__ seed_count,
-    uint32_t seed_cap, int kk, uint64_t* __restrict__ tau_key) {
-  extern __shared__ uint64_t keys[];
-  const int qi = blockIdx.x;
-  const uint32_t n = min(seed_count[qi], seed_cap);
-  if (kk <= 0 || n < uint32_t(kk)) return;
-  const uint32_t np2 = NextPow2(n);
-  for (uint32_t i = threadIdx.x; i < np2; i += blockDim.x)
-    keys[i] = i < n ? seed_cand[size_t(qi) * seed_cap + i] : ~0ull;
-  __syncthreads();
-  BitonicSort(keys, np2);
-  if (threadIdx.x == 0 && keys[kk - 1] < tau_key[qi]) tau_key[qi] = keys[kk - 1];
 }
 
 // Overflow recovery: the k'-th smallest stored key is a valid (tighter)
@@ -665,25 +742,21 @@ hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq, i
 }
 
 hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf, const float* topl_dist,
-                       int nq, int L, int seed_leaves, uint32_t* cnt, uint32_t* fill,
-                       uint32_t* pair_off, uint32_t* tile_prefix, uint32_t* pair_q,
-                       float* pair_bias, uint32_t* tile_leaf, uint32_t max_items,
-                       unsigned long long* code_bytes, hipStream_t s) {
+                       int nq, int L, uint32_t* cnt, uint32_t* fill, uint32_t* pair_off,
+                       uint32_t* tile_prefix, uint32_t* pair_q, float* pair_bias, uint2* work,
+                       uint32_t* totals, unsigned long long* code_bytes, hipStream_t s) {
   const int n = nq * L;
   const int blocks = (n + 255) / 256;
-  if (n > 0) {
-    hipLaunchKernelGGL(pairs_count_kernel, dim3(blocks), dim3(256), 0, s, topl_leaf, nq, L,
-                       seed_leaves, ix.nl, cnt, ix.leaf_size, ix.nb,
-                       code_bytes);
-  }
-  hipLaunchKernelGGL(pairs_scan_kernel, dim3(2), dim3(1024), 0, s, cnt, ix.nl, pair_off,
-                     tile_prefix);
-  if (n > 0) {
-    hipLaunchKernelGGL(pairs_scatter_kernel, dim3(blocks), dim3(256), 0, s, topl_leaf,
-                       topl_dist, nq, L, seed_leaves, ix.nl, pair_off, fill, pair_q, pair_bias);
-  }
-  hipLaunchKernelGGL(pairs_tiles_kernel, dim3((ix.nl + 255) / 256, 2), dim3(256), 0, s,
-                     tile_prefix, ix.nl, tile_leaf, max_items);
+  if (n > 0)
+    hipLaunchKernelGGL(pairs_count_kernel, dim3(blocks), dim3(256), 0, s, topl_leaf, n, cnt,
+                       ix.leaf_size, ix.nb, code_bytes);
+  hipLaunchKernelGGL(pairs_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, ix.leaf_order, ix.nl,
+                     pair_off, tile_prefix, totals);
+  if (n > 0)
+    hipLaunchKernelGGL(pairs_scatter_kernel, dim3(blocks), dim3(256), 0, s, topl_leaf, topl_dist,
+                       n, L, pair_off, fill, pair_q, pair_bias);
+  hipLaunchKernelGGL(pairs_work_kernel, dim3((ix.nl + 255) / 256), dim3(256), 0, s, tile_prefix,
+                     ix.leaf_order, ix.nl, work);
   return hipGetLastError();
 }
 
@@ -742,16 +815,26 @@ hipError_t LaunchLeafScores(const DeviceIndex& ix, int leaf, const int8_t* lut, 
   return hipGetLastError();
 }
 
-hipError_t LaunchSeedSelect(const uint64_t* seed_cand, const uint32_t* seed_count,
-                            uint32_t seed_cap, int nq, int kk, uint64_t* tau_key,
-                            hipStream_t s) {
-  if (nq == 0) return hipSuccess;
-  uint32_t np2 = 1;
-  while (np2 < seed_cap) np2 <<= 1;
-  const size_t lds = size_t(np2) * 8;
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(seed_select_kernel, dim3(nq), dim3(256), lds, s, seed_cand, seed_count,
-                     seed_cap, kk, tau_key);
+#define SMX_SEED_CASE(KV)                                                        \
+  case KV:                                                                       \
+    hipLaunchKernelGGL(seed_tau_kernel<KV>, dim3(nq), dim3(256), 0, s, a);       \
+    break;
+
+hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s) {
+  if (nq == 0 || a.seed <= 0) return hipSuccess;
+  switch (ix.ksteps) {
+    SMX_SEED_CASE(4)
+    SMX_SEED_CASE(8)
+    SMX_SEED_CASE(12)
+    SMX_SEED_CASE(16)
+    SMX_SEED_CASE(20)
+    SMX_SEED_CASE(24)
+    SMX_SEED_CASE(25)
+    SMX_SEED_CASE(28)
+    SMX_SEED_CASE(32)
+    default:
+      return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -74,24 +74,20 @@ int EffectiveKSteps(int nb) {
 
 struct Workspace {
   int nq = 0, L = 0, kk = 0, dim = 0, width = 0;
-  uint32_t cap = 0, seed_cap = 0, max_items = 0;
+  uint32_t cap = 0, max_items = 0;
   float* queries = nullptr;
   int32_t* topl_leaf = nullptr;
   float* topl_dist = nullptr;
   int8_t* lut = nullptr;
-  uint8_t* lut_u8 = nullptr;
   float* mult = nullptr;
   float* inv = nullptr;
-  uint32_t* counters = nullptr;     // cnt[2][nl] | fill[2][nl] | work[2] | overflow[3]
-  uint32_t* pair_off = nullptr;     // [2][nl+1]
-  uint32_t* tile_prefix = nullptr;  // [2][nl+1]
-  uint32_t* pair_q = nullptr;       // [2][nq*L]
-  float* pair_bias = nullptr;       // [2][nq*L]
-  uint32_t* tile_leaf = nullptr;    // [2][max_items]
-  unsigned long long* code_bytes = nullptr;  // [2]
+  uint32_t* counters = nullptr;     // cnt[nl] | fill[nl] | work counter | stats[16]
+  uint32_t* pair_off = nullptr;     // [nl+1]
+  uint32_t* tile_prefix = nullptr;  // [nl+1]
+  uint32_t* pair_q = nullptr;       // [nq*L]
+  float* pair_bias = nullptr;       // [nq*L]
+  uint2* work = nullptr;            // [max_items]
   uint64_t* tau = nullptr;          // [nq]
-  uint64_t* seed_cand = nullptr;    // [nq][seed_cap]
-  uint32_t* seed_count = nullptr;   // [nq]
   uint64_t* cand = nullptr;         // [nq][cap]
   uint32_t* cand_count = nullptr;   // [nq]
   uint32_t* out_idx = nullptr;
@@ -99,13 +95,12 @@ struct Workspace {
   int32_t* out_count = nullptr;
 
   void Release() {
-    DFree(queries); DFree(topl_leaf); DFree(topl_dist); DFree(lut); DFree(lut_u8);
-    DFree(mult); DFree(inv); DFree(counters); DFree(pair_off); DFree(tile_prefix);
-    DFree(pair_q); DFree(pair_bias); DFree(tile_leaf); DFree(code_bytes); DFree(tau);
-    DFree(seed_cand); DFree(seed_count); DFree(cand); DFree(cand_count);
-    DFree(out_idx); DFree(out_dist); DFree(out_count);
+    DFree(queries); DFree(topl_leaf); DFree(topl_dist); DFree(lut); DFree(mult); DFree(inv);
+    DFree(counters); DFree(pair_off); DFree(tile_prefix); DFree(pair_q); DFree(pair_bias);
+    DFree(work); DFree(tau); DFree(cand); DFree(cand_count); DFree(out_idx); DFree(out_dist);
+    DFree(out_count);
     nq = L = kk = dim = width = 0;
-    cap = seed_cap = max_items = 0;
+    cap = max_items = 0;
   }
 };
 
@@ -118,7 +113,7 @@ struct smx_index {
   std::mutex mu;
   Workspace ws;
   uint32_t cap_per_query = 4096;   // candidate list capacity
-  int seed_leaves = 1;
+  int seed_leaves = 4;
   int grid = 0;                    // scan grid (blocks of 4 waves)
   bool profiling = false;
   smx_timings timings{};
@@ -208,7 +203,7 @@ int UploadIndex(const smx_index_desc* d, smx_index* h) {
       (rc = DAlloc(&ix.codebook, size_t(nb) * 16 * ix.dpb)) ||
       (rc = DAlloc(&ix.tiles, tiles.size())) || (rc = DAlloc(&ix.tile_off, nl + 1)) ||
       (rc = DAlloc(&ix.leaf_size, nl)) || (rc = DAlloc(&ix.member_off, nl + 1)) ||
-      (rc = DAlloc(&ix.members, M)))
+      (rc = DAlloc(&ix.members, M)) || (rc = DAlloc(&ix.leaf_order, nl)))
     return rc;
   if (d->dataset && (rc = DAlloc(&ix.dataset, size_t(d->num_datapoints) * dim))) return rc;
   SMX_HIP(hipMemcpy(ix.centers, d->centers, sizeof(float) * nl * dim, hipMemcpyHostToDevice));
@@ -221,6 +216,12 @@ int UploadIndex(const smx_index_desc* d, smx_index* h) {
   SMX_HIP(hipMemcpy(ix.leaf_size, size.data(), 4 * nl, hipMemcpyHostToDevice));
   SMX_HIP(hipMemcpy(ix.member_off, d->leaf_offsets, 8 * (nl + 1), hipMemcpyHostToDevice));
   if (M) SMX_HIP(hipMemcpy(ix.members, d->leaf_members, 4 * M, hipMemcpyHostToDevice));
+  // Work order: largest leaves first (their work items are the longest).
+  std::vector<uint32_t> order(nl);
+  for (int l = 0; l < nl; ++l) order[l] = uint32_t(l);
+  std::stable_sort(order.begin(), order.end(),
+                   [&](uint32_t a, uint32_t b) { return size[a] > size[b]; });
+  SMX_HIP(hipMemcpy(ix.leaf_order, order.data(), 4 * nl, hipMemcpyHostToDevice));
   if (d->dataset)
     SMX_HIP(hipMemcpy(ix.dataset, d->dataset, sizeof(float) * size_t(d->num_datapoints) * dim,
                       hipMemcpyHostToDevice));
@@ -230,7 +231,7 @@ int UploadIndex(const smx_index_desc* d, smx_index* h) {
 void FreeIndex(smx::DeviceIndex& ix) {
   DFree(ix.centers); DFree(ix.centers_t); DFree(ix.cnorm); DFree(ix.codebook);
   DFree(ix.tiles); DFree(ix.tile_off); DFree(ix.leaf_size); DFree(ix.member_off);
-  DFree(ix.members); DFree(ix.dataset);
+  DFree(ix.members); DFree(ix.leaf_order); DFree(ix.dataset);
 }
 
 int ValidateDesc(const smx_index_desc* d) {
@@ -267,10 +268,8 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
   Workspace& w = h->ws;
   const smx::DeviceIndex& ix = h->ix;
   const uint32_t cap = std::max<uint32_t>(h->cap_per_query, uint32_t(kk));
-  const uint32_t seed_cap = std::min<uint32_t>(
-      16384u, std::max<uint32_t>(uint32_t(kk), uint32_t(h->seed_leaves) * ix.max_leaf));
   if (nq <= w.nq && L <= w.L && kk <= w.kk && width <= w.width && cap == w.cap &&
-      seed_cap == w.seed_cap && ix.dim == w.dim)
+      ix.dim == w.dim)
     return SMX_OK;
   w.Release();
   const int nl = ix.nl;
@@ -279,22 +278,19 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
   int rc;
   if ((rc = DAlloc(&w.queries, size_t(nq) * ix.dim)) || (rc = DAlloc(&w.topl_leaf, pairs)) ||
       (rc = DAlloc(&w.topl_dist, pairs)) ||
-      (rc = DAlloc(&w.lut, size_t(nq) * 2 * ix.ksteps * 16)) ||
-      (rc = DAlloc(&w.lut_u8, size_t(nq) * ix.nb * 16)) || (rc = DAlloc(&w.mult, nq)) ||
-      (rc = DAlloc(&w.inv, nq)) || (rc = DAlloc(&w.counters, size_t(4) * nl + 8)) ||
-      (rc = DAlloc(&w.pair_off, size_t(2) * (nl + 1))) ||
-      (rc = DAlloc(&w.tile_prefix, size_t(2) * (nl + 1))) ||
-      (rc = DAlloc(&w.pair_q, 2 * pairs)) || (rc = DAlloc(&w.pair_bias, 2 * pairs)) ||
-      (rc = DAlloc(&w.tile_leaf, size_t(2) * max_items)) || (rc = DAlloc(&w.code_bytes, 2)) ||
-      (rc = DAlloc(&w.tau, nq)) || (rc = DAlloc(&w.seed_cand, size_t(nq) * seed_cap)) ||
-      (rc = DAlloc(&w.seed_count, nq)) || (rc = DAlloc(&w.cand, size_t(nq) * cap)) ||
-      (rc = DAlloc(&w.cand_count, nq)) || (rc = DAlloc(&w.out_idx, size_t(nq) * width)) ||
+      (rc = DAlloc(&w.lut, size_t(nq) * 2 * ix.ksteps * 16)) || (rc = DAlloc(&w.mult, nq)) ||
+      (rc = DAlloc(&w.inv, nq)) || (rc = DAlloc(&w.counters, size_t(2) * nl + 20)) ||
+      (rc = DAlloc(&w.pair_off, size_t(nl + 1))) || (rc = DAlloc(&w.tile_prefix, size_t(nl + 1))) ||
+      (rc = DAlloc(&w.pair_q, pairs)) || (rc = DAlloc(&w.pair_bias, pairs)) ||
+      (rc = DAlloc(&w.work, max_items)) || (rc = DAlloc(&w.tau, nq)) ||
+      (rc = DAlloc(&w.cand, size_t(nq) * cap)) || (rc = DAlloc(&w.cand_count, nq)) ||
+      (rc = DAlloc(&w.out_idx, size_t(nq) * width)) ||
       (rc = DAlloc(&w.out_dist, size_t(nq) * width)) || (rc = DAlloc(&w.out_count, nq))) {
     w.Release();
     return rc;
   }
   w.nq = nq; w.L = L; w.kk = kk; w.width = width; w.dim = ix.dim;
-  w.cap = cap; w.seed_cap = seed_cap; w.max_items = max_items;
+  w.cap = cap; w.max_items = max_items;
   return SMX_OK;
 }
 
@@ -330,63 +326,66 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   Workspace& w = h->ws;
   const int nl = ix.nl;
   uint32_t* cnt = w.counters;
-  uint32_t* fill = w.counters + 2 * nl;
-  uint32_t* work = w.counters + 4 * nl;
-  uint32_t* overflow = work + 2;
+  uint32_t* fill = w.counters + nl;
+  uint32_t* work = w.counters + 2 * nl;
+  // stats: [0] overflow flag [1] max overflowing count [2] max count
+  //        [3] pairs [4] work items [5] pad [6..7] code bytes (u64)
+  uint32_t* stats = ((reinterpret_cast<uintptr_t>(work + 1) & 7) == 0) ? work + 1 : work + 2;
+  unsigned long long* code_bytes = reinterpret_cast<unsigned long long*>(stats + 6);
   const int seed = std::min(h->seed_leaves, L);
 
   Mark(h, 0, s);
-  SMX_HIP(hipMemsetAsync(w.counters, 0, sizeof(uint32_t) * (4 * nl + 8), s));
-  SMX_HIP(hipMemsetAsync(w.code_bytes, 0, sizeof(unsigned long long) * 2, s));
-  SMX_HIP(hipMemsetAsync(w.seed_count, 0, sizeof(uint32_t) * nq, s));
+  SMX_HIP(hipMemsetAsync(w.counters, 0, sizeof(uint32_t) * (2 * nl + 20), s));
   SMX_HIP(hipMemsetAsync(w.cand_count, 0, sizeof(uint32_t) * nq, s));
   SMX_HIP(smx::LaunchFill64(w.tau, smx::kNoThreshold, nq, s));
   SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, s));
   Mark(h, 1, s);
   SMX_HIP(smx::LaunchLutBuild(ix, queries, nq, w.lut, w.mult, w.inv, nullptr, s));
   Mark(h, 2, s);
-  SMX_HIP(smx::LaunchPairs(ix, w.topl_leaf, w.topl_dist, nq, L, seed, cnt, fill, w.pair_off,
-                           w.tile_prefix, w.pair_q, w.pair_bias, w.tile_leaf, w.max_items,
-                           w.code_bytes, s));
+  SMX_HIP(smx::LaunchPairs(ix, w.topl_leaf, w.topl_dist, nq, L, cnt, fill, w.pair_off,
+                           w.tile_prefix, w.pair_q, w.pair_bias, w.work, stats + 3, code_bytes,
+                           s));
   Mark(h, 3, s);
-
-  const size_t pairs = size_t(nq) * L;
-  auto scan_args = [&](int set, const uint64_t* tau, uint64_t* cand, uint32_t* count,
-                       uint32_t capq) {
-    smx::ScanArgs a{};
-    a.tiles = ix.tiles;
-    a.tile_off = ix.tile_off;
-    a.leaf_size = ix.leaf_size;
-    a.member_off = ix.member_off;
-    a.members = ix.members;
-    a.lut = w.lut;
-    a.inv = w.inv;
-    a.pair_q = w.pair_q + size_t(set) * pairs;
-    a.pair_bias = w.pair_bias + size_t(set) * pairs;
-    a.pair_off = w.pair_off + size_t(set) * (nl + 1);
-    a.tile_prefix = w.tile_prefix + size_t(set) * (nl + 1);
-    a.tile_leaf = w.tile_leaf + size_t(set) * w.max_items;
-    a.tau_key = tau;
-    a.cand = cand;
-    a.cand_count = count;
-    a.work_counter = work + set;
-    a.cap = capq;
-    a.nl = nl;
-    a.nb = ix.nb;
-    a.shift = ix.shift;
-    a.residual = ix.residual;
-    return a;
-  };
-  // Seed pass: everything of the first `seed` leaves per query.
-  if (seed > 0) {
-    const smx::ScanArgs sa = scan_args(0, nullptr, w.seed_cand, w.seed_count, w.seed_cap);
-    SMX_HIP(smx::LaunchScan(ix, sa, h->grid, s));
-    Mark(h, 4, s);
-    SMX_HIP(smx::LaunchSeedSelect(w.seed_cand, w.seed_count, w.seed_cap, nq, kk, w.tau, s));
-  } else {
-    Mark(h, 4, s);
-  }
+  smx::SeedArgs sa{};
+  sa.topl_leaf = w.topl_leaf;
+  sa.topl_dist = w.topl_dist;
+  sa.lut = w.lut;
+  sa.inv = w.inv;
+  sa.tiles = ix.tiles;
+  sa.tile_off = ix.tile_off;
+  sa.leaf_size = ix.leaf_size;
+  sa.tau_key = w.tau;
+  sa.L = L;
+  sa.seed = seed;
+  sa.kk = kk;
+  sa.residual = ix.residual;
+  SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
+  Mark(h, 4, s);
   Mark(h, 5, s);
+
+  smx::ScanArgs a{};
+  a.tiles = ix.tiles;
+  a.tile_off = ix.tile_off;
+  a.leaf_size = ix.leaf_size;
+  a.member_off = ix.member_off;
+  a.members = ix.members;
+  a.lut = w.lut;
+  a.inv = w.inv;
+  a.pair_q = w.pair_q;
+  a.pair_bias = w.pair_bias;
+  a.pair_off = w.pair_off;
+  a.leaf_count = cnt;
+  a.tile_prefix = w.tile_prefix;
+  a.work = w.work;
+  a.tau_key = w.tau;
+  a.cand = w.cand;
+  a.cand_count = w.cand_count;
+  a.work_counter = work;
+  a.cap = w.cap;
+  a.nl = nl;
+  a.nb = ix.nb;
+  a.shift = ix.shift;
+  a.residual = ix.residual;
 
   smx::SelectArgs sel{};
   sel.cand = w.cand;
@@ -409,47 +408,44 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sel.out_dist = out_dist;
   sel.out_count = out_count;
   sel.out_width = width;
-  sel.overflow = overflow;
+  sel.overflow = stats;
 
   int retries = 0;
-  uint32_t ovf[3] = {0, 0, 0};
+  uint32_t st[8] = {0};
   for (;;) {
-    const smx::ScanArgs ma = scan_args(1, w.tau, w.cand, w.cand_count, w.cap);
-    SMX_HIP(smx::LaunchScan(ix, ma, h->grid, s));
+    SMX_HIP(smx::LaunchScan(ix, a, h->grid, s));
     Mark(h, 6, s);
     SMX_HIP(smx::LaunchFinalSelect(sel, nq, s));
     Mark(h, 7, s);
-    SMX_HIP(hipMemcpyAsync(ovf, overflow, sizeof(ovf), hipMemcpyDeviceToHost, s));
+    SMX_HIP(hipMemcpyAsync(st, stats, sizeof(st), hipMemcpyDeviceToHost, s));
     SMX_HIP(hipStreamSynchronize(s));
-    if (!ovf[0]) break;
+    if (!st[0]) break;
     if (++retries > 64) return Fail(SMX_INTERNAL, "candidate tightening did not converge");
     SMX_HIP(smx::LaunchTighten(w.cand, w.cand_count, w.cap, nq, kk, w.tau, s));
     SMX_HIP(hipMemsetAsync(w.cand_count, 0, sizeof(uint32_t) * nq, s));
-    SMX_HIP(hipMemsetAsync(overflow, 0, sizeof(uint32_t) * 3, s));
-    SMX_HIP(hipMemsetAsync(work + 1, 0, sizeof(uint32_t), s));
+    SMX_HIP(hipMemsetAsync(stats, 0, sizeof(uint32_t) * 3, s));
+    SMX_HIP(hipMemsetAsync(work, 0, sizeof(uint32_t), s));
   }
+  smx_timings& t = h->timings;
   if (h->profiling) {
-    smx_timings& t = h->timings;
+    // The stream is idle here, so reading the events costs no extra sync.
     t.partition_ms = Elapsed(h, 0, 1);
     t.lut_ms = Elapsed(h, 1, 2);
     t.invert_ms = Elapsed(h, 2, 3);
     t.seed_scan_ms = Elapsed(h, 3, 4);
-    t.seed_select_ms = Elapsed(h, 4, 5);
+    t.seed_select_ms = 0.0f;
     t.scan_ms = Elapsed(h, 5, 6);
     t.select_ms = Elapsed(h, 6, 7);
     t.total_ms = Elapsed(h, 0, 7);
-    unsigned long long cb[2] = {0, 0};
-    (void)hipMemcpy(cb, w.code_bytes, sizeof(cb), hipMemcpyDeviceToHost);
-    uint32_t cnts[2] = {0, 0};
-    (void)hipMemcpy(&cnts[0], w.pair_off + nl, 4, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(&cnts[1], w.pair_off + (nl + 1) + nl, 4, hipMemcpyDeviceToHost);
-    t.seed_code_bytes = double(cb[0]);
-    t.scan_code_bytes = double(cb[1]);
-    t.seed_pairs = int32_t(cnts[0]);
-    t.scan_pairs = int32_t(cnts[1]);
   }
-  h->timings.overflow_retries = retries;
-  h->timings.max_candidates = int32_t(ovf[2]);
+  unsigned long long cb;
+  std::memcpy(&cb, st + 6, sizeof(cb));
+  t.seed_code_bytes = 0.0;
+  t.scan_code_bytes = double(cb);
+  t.seed_pairs = int32_t(std::min(seed, L)) * nq;
+  t.scan_pairs = int32_t(st[3]);
+  t.overflow_retries = retries;
+  t.max_candidates = int32_t(st[2]);
   return SMX_OK;
 }
 
