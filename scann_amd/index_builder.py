@@ -13,9 +13,12 @@ builder API:
 * residuals against the assigned center for tree + dot product
   (tree_ah_hybrid_residual.cc:185-224, scann_builder.py:429-431);
 * one 16-center k-means codebook per block (asymmetric_hashing_impl.cc:41-198)
-  and nearest-center encoding.  Anisotropic (AVQ) noise shaping and SOAR
-  spilling are NOT reproduced; the searcher accepts indexes that use them
-  (spilled members, any codes) but this builder does not produce them.
+  and nearest-center encoding (anisotropic AVQ noise shaping is not
+  reproduced; the searcher takes any codes);
+* optional SOAR spilling: a second leaf per datapoint minimising
+  ||x - c||^2 + lambda * <r, x - c>^2 / ||r||^2 with r the primary residual
+  (SOAR's orthogonality-amplified loss, kmeans_tree_partitioner.cc:926-997),
+  encoded against that leaf's center.
 
 Uses torch on the GPU when one is visible (dense distance blocks), numpy
 otherwise; results differ only in training floating-point noise, which no
@@ -123,11 +126,44 @@ def encode(residuals: np.ndarray, codebook: np.ndarray, chunk: int = 1 << 15) ->
     return out
 
 
+def soar_assign(x: np.ndarray, centers: np.ndarray, primary: np.ndarray, lam: float,
+                chunk: int = 1 << 15) -> np.ndarray:
+    """Secondary leaf per row with the SOAR loss (never the primary leaf)."""
+    out = np.empty(x.shape[0], dtype=np.int64)
+    torch, dev = _torch_device()
+    if torch is not None:
+        c = torch.from_numpy(centers).to(dev)
+        cn = (c * c).sum(1)
+        for s in range(0, x.shape[0], chunk):
+            xb = torch.from_numpy(x[s:s + chunk]).to(dev)
+            p = torch.from_numpy(primary[s:s + chunk]).to(dev)
+            r = xb - c[p]
+            rn = (r * r).sum(1).clamp_min(1e-30)
+            d2 = (xb * xb).sum(1, keepdim=True) - 2.0 * (xb @ c.T) + cn[None, :]
+            proj = (r * xb).sum(1, keepdim=True) - r @ c.T
+            loss = d2 + lam * proj * proj / rn[:, None]
+            loss[torch.arange(xb.shape[0], device=dev), p] = float("inf")
+            out[s:s + chunk] = loss.argmin(1).cpu().numpy()
+        return out
+    cn = (centers * centers).sum(1)
+    for s in range(0, x.shape[0], chunk):
+        xb, p = x[s:s + chunk], primary[s:s + chunk]
+        r = xb - centers[p]
+        rn = np.maximum((r * r).sum(1), 1e-30)
+        d2 = (xb * xb).sum(1, keepdims=True) - 2.0 * (xb @ centers.T) + cn[None, :]
+        proj = (r * xb).sum(1, keepdims=True) - r @ centers.T
+        loss = d2 + lam * proj * proj / rn[:, None]
+        loss[np.arange(xb.shape[0]), p] = np.inf
+        out[s:s + chunk] = loss.argmin(1)
+    return out
+
+
 def build_tree_ah(db: np.ndarray, metric: int, num_leaves: int,
                   dims_per_block: int = 2, *, training_sample_size: int = 100000,
                   training_iterations: int = 12, ah_training_iterations: int = 10,
                   ah_training_sample_size: int = 100000, residual: Optional[bool] = None,
-                  keep_dataset: bool = True, seed: int = 0) -> TreeAHIndex:
+                  keep_dataset: bool = True, soar_lambda: Optional[float] = None,
+                  overretrieve_factor: float = 2.0, seed: int = 0) -> TreeAHIndex:
     db = np.ascontiguousarray(db, dtype=np.float32)
     n, dim = db.shape
     if residual is None:
@@ -135,13 +171,19 @@ def build_tree_ah(db: np.ndarray, metric: int, num_leaves: int,
     num_leaves = max(1, min(num_leaves, n))
     centers = kmeans(db, num_leaves, training_iterations, seed, training_sample_size)
     labels = _assign_l2(db, centers)
-    order = np.argsort(labels, kind="stable")   # members ascending by id per leaf
+    ids = np.arange(n, dtype=np.int64)
+    if soar_lambda is not None and num_leaves > 1:
+        second = soar_assign(db, centers, labels, float(soar_lambda))
+        ids = np.concatenate([ids, ids])
+        labels = np.concatenate([labels, second])
+    order = np.lexsort((ids, labels))          # by leaf, then ascending id
     counts = np.bincount(labels, minlength=num_leaves)
     offsets = np.zeros(num_leaves + 1, np.uint64)
     offsets[1:] = np.cumsum(counts)
-    members = order.astype(np.uint32)
+    members = ids[order].astype(np.uint32)
+    member_leaf = labels[order]
     num_blocks = int(math.ceil(dim / dims_per_block))
-    resid = db[members] - centers[labels[members]] if residual else db[members]
+    resid = db[members] - centers[member_leaf] if residual else db[members]
     rng = np.random.default_rng(seed + 1)
     samp = resid
     if resid.shape[0] > ah_training_sample_size:
@@ -152,4 +194,5 @@ def build_tree_ah(db: np.ndarray, metric: int, num_leaves: int,
                        dims_per_block=dims_per_block, residual=bool(residual),
                        centers=centers, codebook=codebook, leaf_offsets=offsets,
                        leaf_members=members, member_codes=codes, num_datapoints=n,
-                       dataset=db if keep_dataset else None)
+                       dataset=db if keep_dataset else None,
+                       spilling_overretrieve_factor=float(overretrieve_factor))

@@ -1,0 +1,123 @@
+"""``ScannNumpy`` over the MI355X C ABI.
+
+Mirrors the reference's pybind class (scann/scann_ops/cc/scann_npy.{h,cc},
+exposed as ``scann_pybind.ScannNumpy`` by scann_pybind.cc:24-54) for the
+tree-AH LUT16 path:
+
+* ``ScannNumpy(db, config, training_threads)`` trains an index with
+  scann_amd.index_builder and uploads it (scann_npy.cc:67-77);
+* ``ScannNumpy(artifacts_dir, assets_pbtxt)`` reloads a serialized searcher
+  (scann_npy.cc:57-65; this build's own asset format, see TreeAHIndex.save);
+* ``search`` / ``search_batched`` keep the argument order, the -1 = "config
+  default" convention (scann.cc:384-430), the float32 C-order cast, the
+  2-D check, the (0, NaN) padding and the x(-1) of dot-product distances
+  (scann.h:162-180, scann.cc:364-369).  Errors surface as RuntimeError with
+  the reference's "Error during search: " prefix (scann_npy.cc:41-55).
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import numpy as np
+
+from . import _native
+from .config import SearchConfig, search_config_from_text
+from .index import METRIC_NAMES, TreeAHIndex
+
+
+class ScannNumpy:
+    def __init__(self, db_or_dir, config: str, training_threads: int = 0, device: int = 0,
+                 seed: int = 0):
+        if isinstance(db_or_dir, str):
+            directory = db_or_dir
+            with open(os.path.join(directory, "scann_config.pb")) as f:
+                config = f.read()
+            self._cfg = search_config_from_text(config)
+            index = TreeAHIndex.load(directory)
+        else:
+            self._cfg = search_config_from_text(config)
+            db = np.ascontiguousarray(db_or_dir, dtype=np.float32)
+            if db.ndim != 2:
+                raise ValueError("dataset must be two-dimensional")
+            from .index_builder import build_tree_ah
+            cfg = self._cfg
+            index = build_tree_ah(
+                db, METRIC_NAMES[cfg.metric], cfg.num_leaves, cfg.dims_per_block,
+                training_sample_size=cfg.training_sample_size,
+                training_iterations=cfg.training_iterations,
+                ah_training_iterations=cfg.ah_training_iterations,
+                ah_training_sample_size=cfg.ah_training_sample_size,
+                residual=cfg.residual, keep_dataset=cfg.has_reordering,
+                soar_lambda=cfg.soar_lambda, overretrieve_factor=cfg.overretrieve_factor,
+                seed=seed)
+        self._config_text = config
+        self._index = index
+        self._native = _native.NativeIndex(index, device=device)
+        # ScannInterface::Initialize: dot-family distances are negated on output
+        self._result_multiplier = -1.0 if self._cfg.metric == "dot_product" else 1.0
+
+    # -- parameter resolution (ScannInterface::GetSearchParameters[Batched]) --
+    def _resolve(self, final_nn: int, pre_reorder_nn: int, leaves: int):
+        cfg = self._cfg
+        final_nn = cfg.num_neighbors if final_nn is None or final_nn <= 0 else int(final_nn)
+        if cfg.has_reordering:
+            pre = cfg.reorder_num_neighbors if pre_reorder_nn is None or pre_reorder_nn <= 0 \
+                else int(pre_reorder_nn)
+        else:
+            pre = final_nn
+        leaves = cfg.leaves_to_search if leaves is None or leaves <= 0 else int(leaves)
+        return final_nn, pre, leaves
+
+    def _run(self, queries: np.ndarray, final_nn, pre_reorder_nn, leaves):
+        final_nn, pre, leaves = self._resolve(final_nn, pre_reorder_nn, leaves)
+        try:
+            idx, dist, _ = self._native.search_batched(queries, leaves, pre, final_nn,
+                                                       self._cfg.has_reordering)
+        except _native.SmxError as e:
+            raise RuntimeError(f"Error during search: {e}") from None
+        return idx, dist * np.float32(self._result_multiplier)
+
+    def search(self, query, final_nn=-1, pre_reorder_nn=-1, leaves=-1):
+        q = np.ascontiguousarray(query, dtype=np.float32)
+        if q.ndim != 1:
+            raise ValueError("Query must be one-dimensional")
+        idx, dist = self._run(q[None, :], final_nn, pre_reorder_nn, leaves)
+        keep = ~np.isnan(dist[0])
+        return idx[0][keep], dist[0][keep]
+
+    def search_batched(self, queries, final_nn=-1, pre_reorder_nn=-1, leaves=-1,
+                       parallel=False, batch_size=0):
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        if q.ndim != 2:
+            raise ValueError("Queries must be in two-dimensional array")
+        # parallel mode (SearchBatchedParallel) exists to spread a batch over
+        # CPU threads; the GPU batch is already parallel, so both modes run
+        # the same device pipeline (results identical by construction).
+        del parallel, batch_size
+        return self._run(q, final_nn, pre_reorder_nn, leaves)
+
+    def serialize(self, path: str, relative_path: bool = False) -> None:
+        del relative_path
+        os.makedirs(path, exist_ok=True)
+        self._index.save(path)
+        with open(os.path.join(path, "scann_config.pb"), "w") as f:
+            f.write(self._config_text)
+        with open(os.path.join(path, "scann_assets.pbtxt"), "w") as f:
+            f.write('assets { asset_type: SMX_TREE_AH_INDEX asset_path: "smx_index.json" }\n')
+
+    def config(self) -> str:
+        return self._config_text
+
+    def size(self) -> int:
+        return self._index.num_datapoints
+
+    def set_num_threads(self, num_threads: int) -> None:
+        del num_threads  # host threads do not drive the GPU pipeline
+
+    def native(self) -> _native.NativeIndex:
+        return self._native
+
+    @property
+    def index(self) -> TreeAHIndex:
+        return self._index

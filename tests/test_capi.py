@@ -1,0 +1,81 @@
+"""The C-ABI library loads on a GPU-less host and exports every function
+include/scann_mi355x.h declares; argument validation that happens before any
+HIP call is exercised here (no device work)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from tests.conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "scann_mi355x.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(smx_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from scann_amd import build
+    build.build()
+    from scann_amd import _native
+    return _native.load()
+
+
+def test_header_declares_the_boundary():
+    fns = declared_functions()
+    for f in ("smx_index_create", "smx_search_batched", "smx_index_destroy", "smx_last_error"):
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol(lib):
+    missing = [f for f in declared_functions() if not hasattr(lib, f)]
+    assert not missing
+
+
+def test_binding_covers_every_declared_symbol():
+    from scann_amd import _native
+    assert sorted(_native.SIGNATURES) == declared_functions()
+
+
+def test_version_and_error_reporting_without_gpu(lib):
+    assert b"gfx950" in lib.smx_version()
+    from scann_amd import _native
+    h = ctypes.c_void_p()
+    rc = lib.smx_index_create(None, 0, ctypes.byref(h))
+    assert rc == -1 and b"null index description" in lib.smx_last_error()
+
+
+def test_descriptor_validation_without_gpu(lib, small_dot):
+    from scann_amd import _native
+    ix = small_dot[0]
+    d = ix.desc()
+    d.num_blocks = 65
+    h = ctypes.c_void_p()
+    assert lib.smx_index_create(ctypes.byref(d), 0, ctypes.byref(h)) == -1
+    assert b"at most 64" in lib.smx_last_error()
+    d = ix.desc()
+    d.dims_per_block = 1  # 16 blocks x 1 dim do not tile 32 dims
+    assert lib.smx_index_create(ctypes.byref(d), 0, ctypes.byref(h)) == -1
+    bad = ix.member_codes.copy()
+    bad[0, 0] = 16
+    d = ix.desc()
+    d.member_codes = bad.ctypes.data
+    assert lib.smx_index_create(ctypes.byref(d), 0, ctypes.byref(h)) == -1
+    assert b"< 16" in lib.smx_last_error()
+    p = _native.SearchParams(0, 10, 10, 1)
+    assert lib.smx_search_batched(None, None, 0, 32, ctypes.byref(p), None, None, None) == -1
+
+
+def test_struct_layout_matches_header():
+    """IndexDesc (ctypes) mirrors smx_index_desc: field order and offsets."""
+    from scann_amd.index import IndexDesc
+    names = [f[0] for f in IndexDesc._fields_]
+    assert names[:6] == ["metric", "dim", "num_leaves", "num_blocks", "dims_per_block", "residual"]
+    assert IndexDesc.centers.offset == 24 and IndexDesc.dataset.offset == 72
+    assert ctypes.sizeof(IndexDesc) == 88

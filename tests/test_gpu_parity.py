@@ -122,3 +122,69 @@ def test_overflow_tightening_is_exact(native, oracle, small_dot):
     oi, od, oc = oracle.search_pre_reorder(ix, q, 48, 100, oracle.MODE_IDEAL)
     np.testing.assert_array_equal(gi, oi)
     np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+
+
+def test_soar_spilled_index_matches_oracle(native, oracle):
+    """Datapoints in two leaves: k' = 2 x pre_nn before DeduplicateDatabaseSpilledResults."""
+    from scann_amd import index_builder, synthetic
+    db = synthetic.mixture(6000, 32, 48, 0.9, 41)
+    q = synthetic.mixture(48, 32, 48, 0.9, 141, means_seed=41)
+    ix = index_builder.build_tree_ah(db, 0, 40, 2, training_iterations=4,
+                                     ah_training_iterations=4, soar_lambda=1.5, seed=41)
+    assert not ix.disjoint
+    n = _nat(native, ix)
+    for leaves, pre in ((6, 20), (12, 100)):
+        gi, gd, gc = n.search_pre_reorder(q, leaves, pre)
+        oi, od, oc = oracle.search_pre_reorder(ix, q, leaves, pre, oracle.MODE_IDEAL)
+        np.testing.assert_array_equal(gc, oc)
+        np.testing.assert_array_equal(gi, oi)
+        np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+        gi, gd, gc = n.search_batched(q, leaves, pre, 10, True)
+        oi, od, oc = oracle.search(ix, q, leaves, pre, 10, True, oracle.MODE_IDEAL)
+        np.testing.assert_array_equal(gi, oi)
+        np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+
+
+def test_edge_cases(native, oracle):
+    """Empty leaves, a single query, k larger than the candidates available,
+    leaves_to_search larger than num_leaves, duplicate vectors (ties)."""
+    from scann_amd.index import TreeAHIndex
+    ix, db, q = make_index(n=900, d=16, leaves=12, seed=9, components=10)
+    # add an empty leaf and duplicated rows -> exact distance ties
+    offsets = np.concatenate([ix.leaf_offsets, ix.leaf_offsets[-1:]])
+    centers = np.concatenate([ix.centers, ix.centers[:1] + 5.0])
+    ix2 = TreeAHIndex(metric=0, dim=16, num_blocks=ix.num_blocks, dims_per_block=2, residual=True,
+                      centers=centers, codebook=ix.codebook, leaf_offsets=offsets,
+                      leaf_members=ix.leaf_members, member_codes=ix.member_codes,
+                      num_datapoints=ix.num_datapoints, dataset=ix.dataset)
+    n = _nat(native, ix2)
+    for nq, leaves, pre, final in ((1, 1, 5, 3), (7, 13, 50, 10), (5, 40, 2000, 25), (3, 2, 400, 400)):
+        qq = q[:nq]
+        gi, gd, gc = n.search_batched(qq, leaves, pre, final, True)
+        oi, od, oc = oracle.search(ix2, qq, leaves, pre, final, True, oracle.MODE_IDEAL)
+        np.testing.assert_array_equal(gc, oc)
+        np.testing.assert_array_equal(gi, oi)
+        np.testing.assert_array_equal(np.isnan(gd), np.isnan(od))
+        np.testing.assert_array_equal(np.nan_to_num(gd).view(np.uint32), np.nan_to_num(od).view(np.uint32))
+    # all-identical codes -> every distance ties inside a leaf
+    codes = np.zeros_like(ix.member_codes)
+    ix3 = TreeAHIndex(metric=0, dim=16, num_blocks=ix.num_blocks, dims_per_block=2, residual=True,
+                      centers=ix.centers, codebook=ix.codebook, leaf_offsets=ix.leaf_offsets,
+                      leaf_members=ix.leaf_members, member_codes=codes,
+                      num_datapoints=ix.num_datapoints, dataset=None)
+    n3 = _nat(native, ix3)
+    gi, gd, gc = n3.search_pre_reorder(q, 5, 60)
+    oi, od, oc = oracle.search_pre_reorder(ix3, q, 5, 60, oracle.MODE_IDEAL)
+    np.testing.assert_array_equal(gi, oi)
+    np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+
+
+def test_errors_surface_as_status(native, small_dot):
+    ix, db, q = small_dot
+    n = _nat(native, ix)
+    with pytest.raises(native.SmxError, match="dimsensionality"):
+        n.search_batched(q[:, :16], 4, 10, 10)
+    bad = q.copy()
+    bad[0, 0] = np.nan
+    with pytest.raises(native.SmxError, match="finite"):
+        n.search_batched(bad, 4, 10, 10)

@@ -1,0 +1,93 @@
+"""Oracle self-consistency at sizes it finishes in seconds.
+
+* the ideal pipeline against an independent exact-arithmetic restatement;
+* the AVX2 port (bench.py's cpu_baseline) equals the emulate mode bit for bit;
+* emulate-vs-ideal id mismatch stays below the reference's own tolerance
+  between its two search modes (1e-3, scann_ops_pybind_test.py:267-278);
+* recall against brute force is high (sanity of the whole restatement).
+"""
+import numpy as np
+import pytest
+
+from scann_amd import synthetic
+from tests.conftest import make_index
+from tests.exact import bits, fadd, ffma, fmul
+
+
+def _independent_ideal(ix, q, L, k):
+    """Exact-rational restatement of pipeline A's pre-reorder stage."""
+    from oracle import binding
+    out = []
+    for qi in range(q.shape[0]):
+        scores = []
+        for c in range(ix.num_leaves):
+            acc = np.float32(0)
+            for d in range(ix.dim):
+                acc = ffma(-q[qi, d], ix.centers[c, d], acc)
+            scores.append((float(acc), c))
+        scores.sort()
+        leaves = scores[:L]
+        _, u8, m = binding.create_lut(q[qi], ix.codebook, 0)
+        inv = np.float32(1.0 / np.float64(np.float32(m)))
+        shift = 32 - int(np.ceil(np.log2(ix.num_leaves)))
+        cands = []
+        for bias, leaf in leaves:
+            b, e = int(ix.leaf_offsets[leaf]), int(ix.leaf_offsets[leaf + 1])
+            for i in range(b, e):
+                s = int(u8[np.arange(ix.num_blocks), ix.member_codes[i]].astype(np.int64).sum()) \
+                    - 128 * ix.num_blocks
+                dd = fadd(fmul(np.float32(s), inv), np.float32(bias))
+                cands.append((float(dd), (leaf << shift) | (i - b), int(ix.leaf_members[i])))
+        cands.sort(key=lambda t: (t[0], t[1]))
+        out.append(sorted(cands[:k], key=lambda t: (t[0], t[2])))
+    return out
+
+
+def test_ideal_matches_exact_restatement(oracle):
+    ix, db, q = make_index(n=700, d=8, leaves=9, seed=21, components=12)
+    q = q[:4]
+    want = _independent_ideal(ix, q, 3, 15)
+    gi, gd, gc = oracle.search_pre_reorder(ix, q, 3, 15)
+    for r in range(q.shape[0]):
+        assert gi[r, :gc[r]].tolist() == [t[2] for t in want[r]]
+        assert [bits(x) for x in gd[r, :gc[r]]] == [bits(t[0]) for t in want[r]]
+
+
+@pytest.mark.parametrize("reorder", [True, False])
+def test_avx2_port_equals_emulate(oracle, small_dot, reorder):
+    ix, db, q = small_dot
+    port = oracle.Avx2Port(ix)
+    pi, pd, pc = port.search(q, 12, 100, 10, reorder, 4)
+    ei, ed, ec = oracle.search(ix, q, 12, 100, 10, reorder, oracle.MODE_EMULATE)
+    np.testing.assert_array_equal(pi, ei)
+    np.testing.assert_array_equal(pd.view(np.uint32), ed.view(np.uint32))
+    np.testing.assert_array_equal(pc, ec)
+
+
+def test_emulate_vs_ideal_mismatch_small(oracle):
+    ix, db, q = make_index(n=20000, d=32, leaves=64, seed=8, components=100)
+    ii, _, _ = oracle.search_pre_reorder(ix, q, 16, 100, oracle.MODE_IDEAL)
+    ei, _, _ = oracle.search_pre_reorder(ix, q, 16, 100, oracle.MODE_EMULATE)
+    mism = float(np.mean([len(set(a) ^ set(b)) / (2 * len(a)) for a, b in zip(ii, ei)]))
+    assert mism < 1e-3
+
+
+def test_recall_sanity(oracle, small_dot, small_l2):
+    for ix, db, q in (small_dot, small_l2):
+        gi, _, _ = oracle.search(ix, q, 24, 100, 10, True)
+        truth = synthetic.brute_force_topk(db, q, 10, ix.metric)
+        assert synthetic.recall_at_k(gi.astype(np.int64), truth, 10) > 0.9
+
+
+def test_soar_dedupe_and_spilled_members(oracle):
+    from scann_amd import index_builder
+    db = synthetic.mixture(3000, 16, 32, 0.9, 31)
+    q = synthetic.mixture(32, 16, 32, 0.9, 131, means_seed=31)
+    ix = index_builder.build_tree_ah(db, 0, 24, 2, training_iterations=4,
+                                     ah_training_iterations=4, soar_lambda=1.5)
+    assert not ix.disjoint and ix.num_members == 2 * ix.num_datapoints
+    gi, gd, gc = oracle.search_pre_reorder(ix, q, 6, 20)
+    for r in range(q.shape[0]):
+        row = gi[r, :gc[r]].tolist()
+        assert len(row) == len(set(row))          # no duplicate ids after dedupe
+        assert list(gd[r, :gc[r]]) == sorted(gd[r, :gc[r]])
