@@ -136,7 +136,7 @@ def search_pre_reorder(index, queries, leaves, pre_nn, mode=MODE_IDEAL, nthreads
     """k' best (global id, AH distance) per query, sorted by (dist, tie id)."""
     q = _c(queries, np.float32)
     nq = q.shape[0]
-    width = pre_nn if index.disjoint else int(pre_nn * index.spilling_overretrieve_factor)
+    width = pre_nn
     d = index.desc()
     idx = np.zeros((nq, width), np.uint32)
     dist = np.zeros((nq, width), np.float32)

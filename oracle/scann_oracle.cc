@@ -745,7 +745,7 @@ static int SearchImpl(const orc_index* ix, const float* queries, int nq,
   const bool reorder = do_reorder && ix->dataset != nullptr;
   // scann.cc:406-430: without reordering pre_nn = final_nn.
   const int pnn = reorder ? pre_nn : final_nn;
-  const int width = pre_only ? SpillK(v, pnn) : final_nn;
+  const int width = pre_only ? pnn : final_nn;
   ParallelFor(nq, nthreads, [&](int qi) {
     std::vector<float> scratch;
     const float* q = queries + size_t(qi) * ix->dim;

@@ -349,10 +349,21 @@ __device__ __forceinline__ void LoadCodes(const uint8_t* p, uint32_t* codes) {
   }
 }
 
+// Survivor staging: kStage keys per lane in LDS (64 KiB per 256-thread block).
+constexpr int kStage = 32;
+
+__device__ __forceinline__ void FlushStage(const uint64_t* stage, uint32_t n, uint64_t* dst,
+                                           uint32_t* count, uint32_t cap) {
+  const uint32_t slot = atomicAdd(count, n);
+  for (uint32_t u = 0; u < n && slot + u < cap; ++u) dst[slot + u] = stage[u];
+}
+
 template <int K>
 __global__ void __launch_bounds__(256) lut16_scan_kernel(ScanArgs a) {
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
   constexpr int W = 4 * NW;
+  __shared__ uint64_t stage_all[256 * kStage];
+  uint64_t* stage = stage_all + threadIdx.x * kStage;
   const int lane = threadIdx.x & 63;
   const int c = lane & 31;
   const int h = lane >> 5;
@@ -388,6 +399,7 @@ __global__ void __launch_bounds__(256) lut16_scan_kernel(ScanArgs a) {
     const uint8_t* tb = a.tiles + a.tile_off[leaf] * 64ull * W + size_t(lane) * W;
     const uint64_t moff = a.member_off[leaf];
     uint32_t codes[NW], next[NW];
+    uint32_t staged = 0;
     if (ntile) LoadCodes<K>(tb, codes);
     for (uint32_t j = 0; j < ntile; ++j) {
       if (j + 1 < ntile) LoadCodes<K>(tb + size_t(j + 1) * 64 * W, next);
@@ -401,9 +413,8 @@ __global__ void __launch_bounds__(256) lut16_scan_kernel(ScanArgs a) {
         pass |= uint32_t((row < rows_left) & (acc[i] <= amax)) << i;
       }
       if (pass) {
-        // Rare path: build keys, keep those <= T, one atomic per lane.
-        uint64_t keys[16];
-        uint32_t m = 0;
+        // Rare path: keys <= T go to this lane's LDS staging row; a full row
+        // is flushed with one atomic (the only value-returning atomic here).
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           if (pass >> i & 1u) {
@@ -412,18 +423,20 @@ __global__ void __launch_bounds__(256) lut16_scan_kernel(ScanArgs a) {
             const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp)
                                              : a.members[moff + dp];
             const uint64_t key = (uint64_t(OrderedBits(d)) << 32) | tie;
-            if (key <= T) keys[m++] = key;
+            if (key <= T) {
+              stage[staged++] = key;
+              if (staged == kStage) {
+                FlushStage(stage, staged, a.cand + size_t(qid) * a.cap, &a.cand_count[qid], a.cap);
+                staged = 0;
+              }
+            }
           }
-        }
-        if (m) {
-          const uint32_t slot = atomicAdd(&a.cand_count[qid], m);
-          uint64_t* dst = a.cand + size_t(qid) * a.cap;
-          for (uint32_t u = 0; u < m && slot + u < a.cap; ++u) dst[slot + u] = keys[u];
         }
       }
 #pragma unroll
       for (int i = 0; i < NW; ++i) codes[i] = next[i];
     }
+    if (staged) FlushStage(stage, staged, a.cand + size_t(qid) * a.cap, &a.cand_count[qid], a.cap);
   }
 }
 
@@ -434,7 +447,8 @@ __global__ void __launch_bounds__(256) lut16_scan_kernel(ScanArgs a) {
 // k'-th from above.  The main pass rescans those leaves, so storing only the
 // first kSeedCap values is still correct (a subset's k'-th is a bound).
 // ---------------------------------------------------------------------------
-constexpr int kSeedCap = 12288;
+constexpr int kSeedCap = 8192;
+constexpr uint32_t kSeedBins = 2048;
 
 template <int K>
 __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
@@ -442,8 +456,9 @@ __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
   constexpr int W = 4 * NW;
   __shared__ int8_t lut[2 * K * 16];
   __shared__ uint32_t vals[kSeedCap];
-  __shared__ uint32_t hist[2048];
-  __shared__ uint32_t s_n, s_bin, s_rem;
+  __shared__ uint32_t hist[kSeedBins];
+  __shared__ uint32_t binmax[kSeedBins];
+  __shared__ uint32_t scan_buf[256];
   const int qi = blockIdx.x;
   for (int e = threadIdx.x; e < 2 * K * 16; e += blockDim.x)
     lut[e] = a.lut[size_t(qi) * 2 * K * 16 + e];
@@ -476,41 +491,58 @@ __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
   const uint32_t total = base;
   const uint32_t kk = uint32_t(a.kk);
   if (kk == 0 || total < kk) return;  // no bound: the threshold stays open
-  // Radix select of the kk-th smallest value: 11 + 11 + 10 bits.
-  uint32_t prefix = 0, rem = kk;
-  const int shifts[3] = {21, 10, 0};
-  const int widths[3] = {11, 11, 10};
-  for (int pass = 0; pass < 3; ++pass) {
-    const int sh = shifts[pass], wd = widths[pass];
-    const uint32_t nb = 1u << wd;
-    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) hist[b] = 0;
+  // Any value >= the kk-th smallest is a valid threshold.  Bin the values
+  // linearly between their min and max (order-preserving bits), find the bin
+  // holding the kk-th smallest and take the largest value in it.
+  uint32_t lo = 0xFFFFFFFFu, hi = 0;
+  for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) {
+    lo = min(lo, vals[i]);
+    hi = max(hi, vals[i]);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = min(lo, __shfl_xor(lo, off));
+    hi = max(hi, __shfl_xor(hi, off));
+  }
+  __shared__ uint32_t s_lo[4], s_hi[4];
+  const int wid = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { s_lo[wid] = lo; s_hi[wid] = hi; }
+  for (uint32_t b = threadIdx.x; b < kSeedBins; b += blockDim.x) { hist[b] = 0; binmax[b] = 0; }
+  __syncthreads();
+  lo = min(min(s_lo[0], s_lo[1]), min(s_lo[2], s_lo[3]));
+  hi = max(max(s_hi[0], s_hi[1]), max(s_hi[2], s_hi[3]));
+  const uint64_t span = uint64_t(hi - lo) + 1;
+  for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) {
+    const uint32_t v = vals[i];
+    const uint32_t b = uint32_t((uint64_t(v - lo) * kSeedBins) / span);
+    atomicAdd(&hist[b], 1u);
+    atomicMax(&binmax[b], v);
+  }
+  __syncthreads();
+  // Block prefix over the bins: thread t owns kSeedBins / 256 consecutive bins.
+  constexpr uint32_t per = kSeedBins / 256;
+  uint32_t local = 0;
+  for (uint32_t u = 0; u < per; ++u) local += hist[threadIdx.x * per + u];
+  scan_buf[threadIdx.x] = local;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const uint32_t v = int(threadIdx.x) >= off ? scan_buf[threadIdx.x - off] : 0u;
     __syncthreads();
-    const int hs = sh + wd;  // bits above this digit must equal the prefix
-    for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) {
-      const uint32_t v = vals[i];
-      const bool match = (hs >= 32) || ((v >> hs) == (prefix >> hs));
-      if (match) atomicAdd(&hist[(v >> sh) & (nb - 1)], 1u);
-    }
+    scan_buf[threadIdx.x] += v;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t cum = 0, b = 0;
-      for (; b < nb; ++b) {
-        if (cum + hist[b] >= rem) break;
-        cum += hist[b];
+  }
+  const uint32_t before = threadIdx.x ? scan_buf[threadIdx.x - 1] : 0u;
+  if (before < kk && before + local >= kk) {
+    uint32_t cum = before;
+    for (uint32_t u = 0; u < per; ++u) {
+      const uint32_t b = threadIdx.x * per + u;
+      cum += hist[b];
+      if (cum >= kk) {
+        const uint64_t t = (uint64_t(binmax[b]) << 32) | 0xFFFFFFFFull;
+        if (t < a.tau_key[qi]) a.tau_key[qi] = t;
+        break;
       }
-      s_bin = b;
-      s_rem = rem - cum;
     }
-    __syncthreads();
-    prefix |= s_bin << sh;
-    rem = s_rem;
-    __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    const uint64_t t = (uint64_t(prefix) << 32) | 0xFFFFFFFFull;
-    if (t < a.tau_key[qi]) a.tau_key[qi] = t;
-  }
-  (void)s_n;
 }
 
 // One-query variant for the stage entry point: raw sums of one leaf.
