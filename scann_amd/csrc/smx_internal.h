@@ -111,7 +111,7 @@ struct SelectArgs {
 // ---- launchers (smx_kernels.hip) ------------------------------------------
 hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int nq,
                                int L, int32_t* out_leaf, float* out_dist,
-                               hipStream_t s);
+                               float* scores /*[nq][nl] scratch*/, hipStream_t s);
 hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq,
                           int8_t* lut, float* mult, float* inv, uint8_t* lut_u8,
                           hipStream_t s);

@@ -3,9 +3,10 @@
 // with an explicit round-to-nearest intrinsic; the library is also built with
 // -ffp-contract=off.
 //
-//   partition_topl_kernel   query tokenization: per-query FMA chains over all
-//                           leaf centers (many_to_many_impl.inc:522-560) and an
-//                           exact top-L by (distance, leaf) in LDS
+//   partition_scores_kernel query tokenization on MFMA f32 32x32x2: the exact
+//                           fma chain of the transposed many-to-many path
+//                           (many_to_many_impl.inc:522-560)
+//   topl_select_kernel      exact top-L by (distance, leaf) per query
 //                           (kmeans_tree_partitioner.cc:703-728)
 //   lut_build_kernel        raw float LUT + uint8 fixed point
 //                           (asymmetric_hashing_impl.cc:505-645)
@@ -21,6 +22,8 @@
 //                           (single_machine_base.cc:872-901)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
 
 #include "smx_internal.h"
 
@@ -70,53 +73,175 @@ __device__ void BitonicSort(uint64_t* keys, uint32_t n) {
   }
 }
 
+
+// Exact k smallest of n keys (u64, LDS) into out[0..m) sorted ascending,
+// m = min(k, n).  Keys are binned linearly on their high word between its
+// min and max; the keys in bins up to the one holding the k-th are compacted
+// and sorted (usually a few hundred), everything else is discarded.  Falls
+// back to sorting all n keys when one bin holds too many (massive ties).
+// scratch: kSelBins u32 + 256 u32.  All threads of the block must call.
+constexpr uint32_t kSelBins = 2048;
+
+__device__ uint32_t SelectSmallest(uint64_t* keys, uint32_t n, uint32_t k, uint64_t* out,
+                                   uint32_t out_cap, uint32_t* hist, uint32_t* scan_buf) {
+  __shared__ uint32_t s_lo[8], s_hi[8], s_bin, s_cnt;
+  const uint32_t m = min(n, k);
+  if (m == 0) return 0;
+  uint32_t lo = 0xFFFFFFFFu, hi = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t v = uint32_t(keys[i] >> 32);
+    lo = min(lo, v);
+    hi = max(hi, v);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = min(lo, __shfl_xor(lo, off));
+    hi = max(hi, __shfl_xor(hi, off));
+  }
+  const int wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) { s_lo[wid] = lo; s_hi[wid] = hi; }
+  for (uint32_t b = threadIdx.x; b < kSelBins; b += blockDim.x) hist[b] = 0;
+  if (threadIdx.x == 0) { s_bin = kSelBins - 1; s_cnt = 0; }
+  __syncthreads();
+  lo = s_lo[0];
+  hi = s_hi[0];
+  for (int w = 1; w < nw; ++w) { lo = min(lo, s_lo[w]); hi = max(hi, s_hi[w]); }
+  const uint64_t span = uint64_t(hi - lo) + 1;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t v = uint32_t(keys[i] >> 32);
+    atomicAdd(&hist[uint32_t((uint64_t(v - lo) * kSelBins) / span)], 1u);
+  }
+  __syncthreads();
+  const uint32_t per = kSelBins / blockDim.x;
+  uint32_t local = 0;
+  for (uint32_t u = 0; u < per; ++u) local += hist[threadIdx.x * per + u];
+  scan_buf[threadIdx.x] = local;
+  __syncthreads();
+  for (uint32_t off = 1; off < blockDim.x; off <<= 1) {
+    const uint32_t v = threadIdx.x >= off ? scan_buf[threadIdx.x - off] : 0u;
+    __syncthreads();
+    scan_buf[threadIdx.x] += v;
+    __syncthreads();
+  }
+  const uint32_t before = threadIdx.x ? scan_buf[threadIdx.x - 1] : 0u;
+  if (before < m && before + local >= m) {
+    uint32_t cum = before;
+    for (uint32_t u = 0; u < per; ++u) {
+      cum += hist[threadIdx.x * per + u];
+      if (cum >= m) { s_bin = threadIdx.x * per + u; break; }
+    }
+  }
+  __syncthreads();
+  const uint32_t bsel = s_bin;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint64_t key = keys[i];
+    const uint32_t b = uint32_t((uint64_t(uint32_t(key >> 32) - lo) * kSelBins) / span);
+    if (b <= bsel) {
+      const uint32_t p = atomicAdd(&s_cnt, 1u);
+      if (p < out_cap) out[p] = key;
+    }
+  }
+  __syncthreads();
+  const uint32_t c = s_cnt;
+  if (c <= out_cap) {
+    const uint32_t np2 = NextPow2(c);
+    for (uint32_t i = c + threadIdx.x; i < np2; i += blockDim.x) out[i] = ~0ull;
+    __syncthreads();
+    BitonicSort(out, np2);
+  } else {  // too many keys share the boundary bin: sort everything
+    const uint32_t np2 = NextPow2(n);
+    for (uint32_t i = n + threadIdx.x; i < np2; i += blockDim.x) keys[i] = ~0ull;
+    __syncthreads();
+    BitonicSort(keys, np2);
+    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) out[i] = keys[i];
+    __syncthreads();
+  }
+  return m;
+}
+
 // ---------------------------------------------------------------------------
-// Query tokenization.
-// Dot: acc <- fma(-q_d, c_d, acc) from 0, d ascending.
-// Squared L2: acc starts at ||c||^2 + ||q||^2, then acc <- fma(-q_d, 2c_d, acc);
-// ||q||^2 accumulated in double, sequentially (thread 0).
+// Query tokenization on the f32 MFMA.  v_mfma_f32_32x32x2_f32 computes
+// D = fma(a_k1, b_k1, fma(a_k0, b_k0, C)) with one rounding per step, so
+// feeding A = -q, B = c (or 2c) two dims per instruction, d ascending,
+// reproduces the reference's transposed many-to-many chain
+// acc <- fma(-q_d, c_d, acc) bit for bit (many_to_many_impl.inc:544-556).
+// One wave = 32 queries x 32 centers.  Odd dims pad with (-0) * (+0), which
+// leaves every accumulator (zeros included) unchanged.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) partition_topl_kernel(
-    const float* __restrict__ queries, int dim, const float* __restrict__ centers_t,
-    const float* __restrict__ cnorm, int nl, int metric, int L, uint32_t npow2,
-    int32_t* __restrict__ out_leaf, float* __restrict__ out_dist) {
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+__global__ void __launch_bounds__(64) partition_scores_kernel(
+    const float* __restrict__ queries, int nq, int dim, const float* __restrict__ centers,
+    const float* __restrict__ cnorm, int nl, int metric, float* __restrict__ scores) {
+  const int lane = threadIdx.x;
+  const int r = lane & 31, k = lane >> 5;
+  const int q0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+  const int qa = min(q0 + r, nq - 1);     // A row (query) of this lane
+  const int cb = min(c0 + r, nl - 1);     // B column (center) of this lane
+  const float* qrow = queries + size_t(qa) * dim;
+  const float* crow = centers + size_t(cb) * dim;
+  v16f acc;
+  __shared__ float qn[32];
+  if (metric == 1) {
+    if (lane < 32) {
+      double s = 0.0;
+      const float* qq = queries + size_t(min(q0 + lane, nq - 1)) * dim;
+      for (int d = 0; d < dim; ++d) s += double(qq[d]) * double(qq[d]);
+      qn[lane] = float(s);
+    }
+    __syncthreads();
+    // C layout: col = lane & 31 (center), row = (i&3) + 8*(i>>2) + 4*(lane>>5)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = (i & 3) + 8 * (i >> 2) + 4 * k;
+      acc[i] = __fadd_rn(cnorm[cb], qn[row]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+  }
+  const float cscale = metric == 1 ? 2.0f : 1.0f;
+  for (int d = 0; d < dim; d += 2) {
+    const int dd = d + k;
+    float av, bv;
+    if (dd < dim) {
+      av = -qrow[dd];
+      bv = __fmul_rn(crow[dd], cscale);
+    } else {
+      av = -0.0f;
+      bv = 0.0f;
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+  }
+  const int col = c0 + r;
+  if (col < nl) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = q0 + (i & 3) + 8 * (i >> 2) + 4 * k;
+      if (row < nq) scores[size_t(row) * nl + col] = acc[i];
+    }
+  }
+}
+
+// Exact top-L per query by (score, center index) from the score matrix.
+__global__ void __launch_bounds__(256) topl_select_kernel(const float* __restrict__ scores, int nl,
+                                                          int L, uint32_t kcap,
+                                                          int32_t* __restrict__ out_leaf,
+                                                          float* __restrict__ out_dist) {
   extern __shared__ uint64_t lds64[];
   uint64_t* keys = lds64;
-  float* q = reinterpret_cast<float*>(lds64 + npow2);
+  uint64_t* sel = keys + kcap;
+  const uint32_t selcap = max(2048u, 2 * NextPow2(uint32_t(L)));
+  uint32_t* hist = reinterpret_cast<uint32_t*>(sel + selcap);
+  uint32_t* scan_buf = hist + kSelBins;
   const int qi = blockIdx.x;
-  const float* qg = queries + size_t(qi) * dim;
-  for (int d = threadIdx.x; d < dim; d += blockDim.x) q[d] = qg[d];
-  __shared__ float qnorm;
+  for (int c = threadIdx.x; c < nl; c += blockDim.x)
+    keys[c] = (uint64_t(OrderedBits(scores[size_t(qi) * nl + c])) << 32) | uint32_t(c);
   __syncthreads();
-  if (metric == 1 && threadIdx.x == 0) {
-    double acc = 0.0;
-    for (int d = 0; d < dim; ++d) acc += double(q[d]) * double(q[d]);
-    qnorm = float(acc);
-  }
-  __syncthreads();
-  for (uint32_t c = threadIdx.x; c < npow2; c += blockDim.x) {
-    uint64_t key = ~0ull;
-    if (c < uint32_t(nl)) {
-      float acc;
-      if (metric == 0) {
-        acc = 0.0f;
-        for (int d = 0; d < dim; ++d) acc = __fmaf_rn(-q[d], centers_t[size_t(d) * nl + c], acc);
-      } else {
-        acc = __fadd_rn(cnorm[c], qnorm);
-        for (int d = 0; d < dim; ++d)
-          acc = __fmaf_rn(-q[d], __fmul_rn(centers_t[size_t(d) * nl + c], 2.0f), acc);
-      }
-      key = (uint64_t(OrderedBits(acc)) << 32) | c;
-    }
-    keys[c] = key;
-  }
-  __syncthreads();
-  BitonicSort(keys, npow2);
-  const int Lc = L < nl ? L : nl;
+  const uint32_t m = SelectSmallest(keys, uint32_t(nl), uint32_t(L), sel, selcap, hist, scan_buf);
   for (int i = threadIdx.x; i < L; i += blockDim.x) {
-    const bool has = i < Lc;
-    out_leaf[size_t(qi) * L + i] = has ? int32_t(keys[i] & 0xFFFFFFFFu) : -1;
-    out_dist[size_t(qi) * L + i] = has ? FromOrdered(uint32_t(keys[i] >> 32)) : __int_as_float(0x7fc00000);
+    const bool has = uint32_t(i) < m;
+    out_leaf[size_t(qi) * L + i] = has ? int32_t(sel[i] & 0xFFFFFFFFu) : -1;
+    out_dist[size_t(qi) * L + i] = has ? FromOrdered(uint32_t(sel[i] >> 32)) : __int_as_float(0x7fc00000);
   }
 }
 
@@ -191,36 +316,47 @@ __global__ void __launch_bounds__(256) lut_build_kernel(
 // dequeued first).
 // ---------------------------------------------------------------------------
 __global__ void pairs_count_kernel(const int32_t* __restrict__ topl_leaf, int n,
-                                   uint32_t* __restrict__ cnt,
-                                   const uint32_t* __restrict__ leaf_size, int nb,
-                                   unsigned long long* __restrict__ code_bytes) {
+                                   uint32_t* __restrict__ cnt) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int leaf = topl_leaf[i];
   if (leaf < 0) return;
   atomicAdd(&cnt[leaf], 1u);
-  atomicAdd(code_bytes, 16ull * nb * ((leaf_size[leaf] + 31u) / 32u));
 }
 
 __global__ void __launch_bounds__(1024) pairs_scan_kernel(const uint32_t* __restrict__ cnt,
                                                           const uint32_t* __restrict__ order,
-                                                          int nl, uint32_t* __restrict__ pair_off,
+                                                          const uint32_t* __restrict__ leaf_size,
+                                                          int nl, int nb,
+                                                          uint32_t* __restrict__ pair_off,
                                                           uint32_t* __restrict__ tile_prefix,
-                                                          uint32_t* __restrict__ totals) {
+                                                          uint32_t* __restrict__ totals,
+                                                          unsigned long long* __restrict__ code_bytes) {
   __shared__ uint32_t s_pairs[1024];
   __shared__ uint32_t s_tiles[1024];
+  __shared__ unsigned long long s_bytes[1024];
   const int per = (nl + blockDim.x - 1) / blockDim.x;
   const int beg = threadIdx.x * per;
   const int end = min(nl, beg + per);
   uint32_t sp = 0, st = 0;
+  unsigned long long sb = 0;
   for (int p = beg; p < end; ++p) {
-    const uint32_t c = cnt[order[p]];
+    const uint32_t leaf = order[p];
+    const uint32_t c = cnt[leaf];
     sp += c;
     st += (c + kQueriesPerTile - 1) / kQueriesPerTile;
+    // algorithmic code bytes: 16 * B * ceil(n / 32) per (query, leaf) pair
+    sb += 16ull * nb * ((leaf_size[leaf] + 31u) / 32u) * c;
   }
   s_pairs[threadIdx.x] = sp;
   s_tiles[threadIdx.x] = st;
+  s_bytes[threadIdx.x] = sb;
   __syncthreads();
+  for (int off = int(blockDim.x) / 2; off > 0; off >>= 1) {
+    if (int(threadIdx.x) < off) s_bytes[threadIdx.x] += s_bytes[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) code_bytes[0] = s_bytes[0];
   for (int off = 1; off < int(blockDim.x); off <<= 1) {
     uint32_t a = 0, b = 0;
     if (int(threadIdx.x) >= off) {
@@ -642,21 +778,26 @@ __global__ void __launch_bounds__(256) final_select_kernel(SelectArgs a) {
   }
   if (threadIdx.x == 0) atomicMax(&a.overflow[2], raw_n);
   const uint32_t n = min(raw_n, a.cap);
-  const uint32_t np2 = NextPow2(n);
-  uint64_t* keys = lds;
+  // LDS: keys[kcap] | sel[selcap] | aux[kkp2] | q[dim] | gid[kk] | dist[kk] | hist | scan
   const uint32_t kcap = NextPow2(a.cap);
-  uint64_t* aux = lds + kcap;
-  float* q = reinterpret_cast<float*>(aux + NextPow2(uint32_t(a.kk)));
+  const uint32_t kkp2 = NextPow2(uint32_t(a.kk));
+  const uint32_t selcap = max(2048u, 2 * kkp2);
+  uint64_t* keys = lds;
+  uint64_t* sel = lds + kcap;
+  uint64_t* aux = sel + selcap;
+  float* q = reinterpret_cast<float*>(aux + kkp2);
   uint32_t* gid = reinterpret_cast<uint32_t*>(q + a.dim);
   float* dist = reinterpret_cast<float*>(gid + a.kk);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(dist + a.kk);
+  uint32_t* scan_buf = hist + kSelBins;
   __shared__ uint32_t s_m;
-  for (uint32_t i = threadIdx.x; i < np2; i += blockDim.x)
-    keys[i] = i < n ? a.cand[size_t(qi) * a.cap + i] : ~0ull;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) keys[i] = a.cand[size_t(qi) * a.cap + i];
   if (a.reorder)
     for (int d = threadIdx.x; d < a.dim; d += blockDim.x) q[d] = a.queries[size_t(qi) * a.dim + d];
   __syncthreads();
-  BitonicSort(keys, np2);
-  uint32_t m = min(n, uint32_t(a.kk));
+  uint32_t m = SelectSmallest(keys, n, uint32_t(a.kk), sel, selcap, hist, scan_buf);
+  __syncthreads();
+  keys = sel;  // the m smallest, sorted
   // tie -> global id
   for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
     const uint64_t k = keys[i];
@@ -754,14 +895,19 @@ __global__ void fill64_kernel(uint64_t* p, uint64_t v, size_t n) {
 // Launchers.
 // ---------------------------------------------------------------------------
 hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int nq, int L,
-                               int32_t* out_leaf, float* out_dist, hipStream_t s) {
+                               int32_t* out_leaf, float* out_dist, float* scores, hipStream_t s) {
   if (nq == 0) return hipSuccess;
-  uint32_t np2 = 1;
-  while (np2 < uint32_t(ix.nl)) np2 <<= 1;
-  const size_t lds = size_t(np2) * 8 + size_t(ix.dim) * 4;
+  uint32_t kcap = 1;
+  while (kcap < uint32_t(ix.nl)) kcap <<= 1;
+  uint32_t lp2 = 1;
+  while (lp2 < uint32_t(L)) lp2 <<= 1;
+  const uint32_t selcap = std::max<uint32_t>(2048u, 2 * lp2);
+  const size_t lds = size_t(kcap) * 8 + size_t(selcap) * 8 + (kSelBins + 256) * 4;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(partition_topl_kernel, dim3(nq), dim3(256), lds, s, queries, ix.dim,
-                     ix.centers_t, ix.cnorm, ix.nl, ix.metric, L, np2, out_leaf, out_dist);
+  hipLaunchKernelGGL(partition_scores_kernel, dim3((nq + 31) / 32, (ix.nl + 31) / 32), dim3(64), 0,
+                     s, queries, nq, ix.dim, ix.centers, ix.cnorm, ix.nl, ix.metric, scores);
+  hipLaunchKernelGGL(topl_select_kernel, dim3(nq), dim3(256), lds, s, scores, ix.nl, L, kcap,
+                     out_leaf, out_dist);
   return hipGetLastError();
 }
 
@@ -780,10 +926,9 @@ hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf, const fl
   const int n = nq * L;
   const int blocks = (n + 255) / 256;
   if (n > 0)
-    hipLaunchKernelGGL(pairs_count_kernel, dim3(blocks), dim3(256), 0, s, topl_leaf, n, cnt,
-                       ix.leaf_size, ix.nb, code_bytes);
-  hipLaunchKernelGGL(pairs_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, ix.leaf_order, ix.nl,
-                     pair_off, tile_prefix, totals);
+    hipLaunchKernelGGL(pairs_count_kernel, dim3(blocks), dim3(256), 0, s, topl_leaf, n, cnt);
+  hipLaunchKernelGGL(pairs_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, ix.leaf_order,
+                     ix.leaf_size, ix.nl, ix.nb, pair_off, tile_prefix, totals, code_bytes);
   if (n > 0)
     hipLaunchKernelGGL(pairs_scatter_kernel, dim3(blocks), dim3(256), 0, s, topl_leaf, topl_dist,
                        n, L, pair_off, fill, pair_q, pair_bias);
@@ -888,7 +1033,9 @@ hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s) {
   while (kcap < a.cap) kcap <<= 1;
   uint32_t kkp2 = 1;
   while (kkp2 < uint32_t(a.kk)) kkp2 <<= 1;
-  const size_t lds = size_t(kcap) * 8 + size_t(kkp2) * 8 + size_t(a.dim) * 4 + size_t(a.kk) * 8;
+  const uint32_t selcap = std::max<uint32_t>(2048u, 2 * kkp2);
+  const size_t lds = size_t(kcap) * 8 + size_t(selcap) * 8 + size_t(kkp2) * 8 +
+                     size_t(a.dim) * 4 + size_t(a.kk) * 8 + (kSelBins + 256) * 4;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(final_select_kernel, dim3(nq), dim3(256), lds, s, a);
   return hipGetLastError();

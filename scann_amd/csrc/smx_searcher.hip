@@ -78,6 +78,7 @@ struct Workspace {
   float* queries = nullptr;
   int32_t* topl_leaf = nullptr;
   float* topl_dist = nullptr;
+  float* scores = nullptr;          // [nq][nl] partition scores
   int8_t* lut = nullptr;
   float* mult = nullptr;
   float* inv = nullptr;
@@ -95,7 +96,8 @@ struct Workspace {
   int32_t* out_count = nullptr;
 
   void Release() {
-    DFree(queries); DFree(topl_leaf); DFree(topl_dist); DFree(lut); DFree(mult); DFree(inv);
+    DFree(queries); DFree(topl_leaf); DFree(topl_dist); DFree(scores); DFree(lut); DFree(mult);
+    DFree(inv);
     DFree(counters); DFree(pair_off); DFree(tile_prefix); DFree(pair_q); DFree(pair_bias);
     DFree(work); DFree(tau); DFree(cand); DFree(cand_count); DFree(out_idx); DFree(out_dist);
     DFree(out_count);
@@ -277,7 +279,7 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
   const uint32_t max_items = uint32_t(pairs / smx::kQueriesPerTile + nl + 1);
   int rc;
   if ((rc = DAlloc(&w.queries, size_t(nq) * ix.dim)) || (rc = DAlloc(&w.topl_leaf, pairs)) ||
-      (rc = DAlloc(&w.topl_dist, pairs)) ||
+      (rc = DAlloc(&w.topl_dist, pairs)) || (rc = DAlloc(&w.scores, size_t(nq) * nl)) ||
       (rc = DAlloc(&w.lut, size_t(nq) * 2 * ix.ksteps * 16)) || (rc = DAlloc(&w.mult, nq)) ||
       (rc = DAlloc(&w.inv, nq)) || (rc = DAlloc(&w.counters, size_t(2) * nl + 20)) ||
       (rc = DAlloc(&w.pair_off, size_t(nl + 1))) || (rc = DAlloc(&w.tile_prefix, size_t(nl + 1))) ||
@@ -338,7 +340,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   SMX_HIP(hipMemsetAsync(w.counters, 0, sizeof(uint32_t) * (2 * nl + 20), s));
   SMX_HIP(hipMemsetAsync(w.cand_count, 0, sizeof(uint32_t) * nq, s));
   SMX_HIP(smx::LaunchFill64(w.tau, smx::kNoThreshold, nq, s));
-  SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, s));
+  SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s));
   Mark(h, 1, s);
   SMX_HIP(smx::LaunchLutBuild(ix, queries, nq, w.lut, w.mult, w.inv, nullptr, s));
   Mark(h, 2, s);
@@ -620,19 +622,20 @@ int smx_partition_topl(smx_index* h, const float* queries, int32_t nq, int32_t L
   float* dq = nullptr;
   int32_t* dl = nullptr;
   float* dd = nullptr;
+  float* dsc = nullptr;
   int rc;
   if ((rc = DAlloc(&dq, size_t(nq) * h->ix.dim)) || (rc = DAlloc(&dl, size_t(nq) * L)) ||
-      (rc = DAlloc(&dd, size_t(nq) * L))) {
-    DFree(dq); DFree(dl); DFree(dd);
+      (rc = DAlloc(&dd, size_t(nq) * L)) || (rc = DAlloc(&dsc, size_t(nq) * h->ix.nl))) {
+    DFree(dq); DFree(dl); DFree(dd); DFree(dsc);
     return rc;
   }
   hipError_t e = hipMemcpyAsync(dq, queries, sizeof(float) * size_t(nq) * h->ix.dim,
                                 hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = smx::LaunchPartitionTopL(h->ix, dq, nq, L, dl, dd, s);
+  if (e == hipSuccess) e = smx::LaunchPartitionTopL(h->ix, dq, nq, L, dl, dd, dsc, s);
   if (e == hipSuccess) e = hipMemcpyAsync(out_leaf, dl, 4 * size_t(nq) * L, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipMemcpyAsync(out_dist, dd, 4 * size_t(nq) * L, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
-  DFree(dq); DFree(dl); DFree(dd);
+  DFree(dq); DFree(dl); DFree(dd); DFree(dsc);
   if (e != hipSuccess) return Fail(SMX_DEVICE_ERROR, hipGetErrorString(e));
   return SMX_OK;
 }
