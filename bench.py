@@ -155,6 +155,15 @@ def main():
     achieved = bytes_per_launch / (avg_scan_ms * 1e-3) / 1e9
     peak = 8000.0
     t_last = nat.timings()
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "scan_traffic.json")
+    if os.path.exists(tpath):
+        import hashlib
+        with open(tpath) as f:
+            tr = json.load(f)
+        with open(os.path.join(ROOT, "scann_amd", "csrc", "smx_kernels.hip"), "rb") as f:
+            if hashlib.sha256(f.read()).hexdigest() == tr.get("smx_kernels_sha256"):
+                traffic = tr["hbm_read_bytes_per_launch"]
 
     if rank == 0:
         result = {
@@ -181,7 +190,7 @@ def main():
             "recall_at_10": round(recall, 4),
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
-                "frac": round(achieved / peak, 4), "traffic": None,
+                "frac": round(achieved / peak, 4), "traffic": traffic,
                 "kernel": "lut16_scan_kernel<25> (main pass)",
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "avg_launch_ms": round(avg_scan_ms, 5),

@@ -113,6 +113,9 @@ typedef struct smx_timings {
   int32_t seed_pairs;
   int32_t overflow_retries; /* candidate-buffer tightening passes            */
   int32_t max_candidates;   /* largest per-query survivor count              */
+  double scan_item_tiles;   /* 32x32 MFMA tiles of the main scan (x K MFMAs)  */
+  float mean_candidates;    /* survivors per query (last pass)               */
+  int32_t reserved_;
 } smx_timings;
 
 /* Index lifecycle (ScannNumpy ctor / destructor; scann_npy.cc:57-77). */

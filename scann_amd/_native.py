@@ -32,7 +32,9 @@ class Timings(ctypes.Structure):
                 ("select_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
                 ("scan_code_bytes", ctypes.c_double), ("seed_code_bytes", ctypes.c_double),
                 ("scan_pairs", ctypes.c_int32), ("seed_pairs", ctypes.c_int32),
-                ("overflow_retries", ctypes.c_int32), ("max_candidates", ctypes.c_int32)]
+                ("overflow_retries", ctypes.c_int32), ("max_candidates", ctypes.c_int32),
+                ("scan_item_tiles", ctypes.c_double), ("mean_candidates", ctypes.c_float),
+                ("reserved_", ctypes.c_int32)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -310,6 +310,14 @@ __global__ void __launch_bounds__(256) lut_build_kernel(
   }
 }
 
+// Work items split a leaf's 32-datapoint tiles into chunks of at most
+// kChunkTiles so that no single wave owns a whole large leaf.
+constexpr uint32_t kChunkTiles = 32;
+__device__ __forceinline__ uint32_t LeafChunks(uint32_t n) {
+  const uint32_t tiles = (n + 31u) / 32u;
+  return tiles == 0 ? 1u : (tiles + kChunkTiles - 1) / kChunkTiles;
+}
+
 // ---------------------------------------------------------------------------
 // Invert (query -> leaves) into (leaf -> queries) and cut every leaf's query
 // list into 32-query work items, listed largest leaf first (longest items
@@ -338,13 +346,14 @@ __global__ void __launch_bounds__(1024) pairs_scan_kernel(const uint32_t* __rest
   const int per = (nl + blockDim.x - 1) / blockDim.x;
   const int beg = threadIdx.x * per;
   const int end = min(nl, beg + per);
-  uint32_t sp = 0, st = 0;
+  uint32_t sp = 0, st = 0, sit = 0;
   unsigned long long sb = 0;
   for (int p = beg; p < end; ++p) {
     const uint32_t leaf = order[p];
     const uint32_t c = cnt[leaf];
     sp += c;
-    st += (c + kQueriesPerTile - 1) / kQueriesPerTile;
+    st += ((c + kQueriesPerTile - 1) / kQueriesPerTile) * LeafChunks(leaf_size[leaf]);
+    sit += ((c + kQueriesPerTile - 1) / kQueriesPerTile) * ((leaf_size[leaf] + 31u) / 32u);
     // algorithmic code bytes: 16 * B * ceil(n / 32) per (query, leaf) pair
     sb += 16ull * nb * ((leaf_size[leaf] + 31u) / 32u) * c;
   }
@@ -357,6 +366,16 @@ __global__ void __launch_bounds__(1024) pairs_scan_kernel(const uint32_t* __rest
     __syncthreads();
   }
   if (threadIdx.x == 0) code_bytes[0] = s_bytes[0];
+  __syncthreads();
+  s_tiles[threadIdx.x] = sit;   // reuse: item-tiles (MFMA tile count) reduction
+  __syncthreads();
+  for (int off = int(blockDim.x) / 2; off > 0; off >>= 1) {
+    if (int(threadIdx.x) < off) s_tiles[threadIdx.x] += s_tiles[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) totals[2] = s_tiles[0];
+  __syncthreads();
+  s_tiles[threadIdx.x] = st;
   for (int off = 1; off < int(blockDim.x); off <<= 1) {
     uint32_t a = 0, b = 0;
     if (int(threadIdx.x) >= off) {
@@ -376,7 +395,7 @@ __global__ void __launch_bounds__(1024) pairs_scan_kernel(const uint32_t* __rest
     pair_off[leaf] = rp;
     tile_prefix[p] = rt;
     rp += c;
-    rt += (c + kQueriesPerTile - 1) / kQueriesPerTile;
+    rt += ((c + kQueriesPerTile - 1) / kQueriesPerTile) * LeafChunks(leaf_size[leaf]);
   }
   if (threadIdx.x == blockDim.x - 1) {
     tile_prefix[nl] = s_tiles[blockDim.x - 1];
@@ -400,13 +419,19 @@ __global__ void pairs_scatter_kernel(const int32_t* __restrict__ topl_leaf,
 }
 
 __global__ void pairs_work_kernel(const uint32_t* __restrict__ tile_prefix,
-                                  const uint32_t* __restrict__ order, int nl,
+                                  const uint32_t* __restrict__ order,
+                                  const uint32_t* __restrict__ leaf_size, int nl,
                                   uint2* __restrict__ work) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= nl) return;
   const uint32_t leaf = order[p];
-  for (uint32_t w = tile_prefix[p]; w < tile_prefix[p + 1]; ++w)
-    work[w] = make_uint2(leaf, w - tile_prefix[p]);
+  const uint32_t chunks = LeafChunks(leaf_size[leaf]);
+  // item = (leaf, query tile << 16 | dp chunk); chunk-major so that a leaf's
+  // first chunks (all query tiles) are dequeued together
+  for (uint32_t w = tile_prefix[p]; w < tile_prefix[p + 1]; ++w) {
+    const uint32_t u = w - tile_prefix[p];
+    work[w] = make_uint2(leaf, ((u / chunks) << 16) | (u % chunks));
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -485,8 +510,9 @@ __device__ __forceinline__ void LoadCodes(const uint8_t* p, uint32_t* codes) {
   }
 }
 
-// Survivor staging: kStage keys per lane in LDS (64 KiB per 256-thread block).
-constexpr int kStage = 32;
+// Survivor staging: kStage keys per lane in LDS (32 KiB per 256-thread block,
+// so three blocks fit a CU next to the 3-waves/SIMD register budget).
+constexpr int kStage = 16;
 
 __device__ __forceinline__ void FlushStage(const uint64_t* stage, uint32_t n, uint64_t* dst,
                                            uint32_t* count, uint32_t cap) {
@@ -512,7 +538,8 @@ __global__ void __launch_bounds__(256) lut16_scan_kernel(ScanArgs a) {
     if (w >= total) break;
     const uint2 item = a.work[w];
     const int leaf = int(__builtin_amdgcn_readfirstlane(item.x));
-    const uint32_t t = __builtin_amdgcn_readfirstlane(item.y);
+    const uint32_t t = __builtin_amdgcn_readfirstlane(item.y) >> 16;
+    const uint32_t chunk = __builtin_amdgcn_readfirstlane(item.y) & 0xFFFFu;
     const uint32_t pbeg = a.pair_off[leaf] + t * kQueriesPerTile;
     const uint32_t pend = a.pair_off[leaf] + a.leaf_count[leaf];
     const int nvalid = int(min(uint32_t(kQueriesPerTile), pend - pbeg));
@@ -531,13 +558,15 @@ __global__ void __launch_bounds__(256) lut16_scan_kernel(ScanArgs a) {
                          ? smax
                          : SumLimit(FromOrdered(uint32_t(T >> 32)), inv, bias, smin, smax);
     const uint32_t n = a.leaf_size[leaf];
-    const uint32_t ntile = (n + kDpPerTile - 1) / kDpPerTile;
+    const uint32_t ntile_leaf = (n + kDpPerTile - 1) / kDpPerTile;
+    const uint32_t j0 = chunk * kChunkTiles;
+    const uint32_t ntile = min(ntile_leaf, j0 + kChunkTiles);
     const uint8_t* tb = a.tiles + a.tile_off[leaf] * 64ull * W + size_t(lane) * W;
     const uint64_t moff = a.member_off[leaf];
     uint32_t codes[NW], next[NW];
     uint32_t staged = 0;
-    if (ntile) LoadCodes<K>(tb, codes);
-    for (uint32_t j = 0; j < ntile; ++j) {
+    if (j0 < ntile) LoadCodes<K>(tb + size_t(j0) * 64 * W, codes);
+    for (uint32_t j = j0; j < ntile; ++j) {
       if (j + 1 < ntile) LoadCodes<K>(tb + size_t(j + 1) * 64 * W, next);
       const v16i acc = TileSums<K>(codes, frag);
       // rows of this lane: (i & 3) + 8 * (i >> 2) + 4 * h of tile j
@@ -776,7 +805,10 @@ __global__ void __launch_bounds__(256) final_select_kernel(SelectArgs a) {
     atomicOr(&a.overflow[0], 1u);
     atomicMax(&a.overflow[1], raw_n);
   }
-  if (threadIdx.x == 0) atomicMax(&a.overflow[2], raw_n);
+  if (threadIdx.x == 0) {
+    atomicMax(&a.overflow[2], raw_n);
+    atomicAdd(&a.overflow[8], raw_n);   // survivors summed over queries
+  }
   const uint32_t n = min(raw_n, a.cap);
   // LDS: keys[kcap] | sel[selcap] | aux[kkp2] | q[dim] | gid[kk] | dist[kk] | hist | scan
   const uint32_t kcap = NextPow2(a.cap);
@@ -933,7 +965,7 @@ hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf, const fl
     hipLaunchKernelGGL(pairs_scatter_kernel, dim3(blocks), dim3(256), 0, s, topl_leaf, topl_dist,
                        n, L, pair_off, fill, pair_q, pair_bias);
   hipLaunchKernelGGL(pairs_work_kernel, dim3((ix.nl + 255) / 256), dim3(256), 0, s, tile_prefix,
-                     ix.leaf_order, ix.nl, work);
+                     ix.leaf_order, ix.leaf_size, ix.nl, work);
   return hipGetLastError();
 }
 

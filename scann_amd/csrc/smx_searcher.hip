@@ -276,7 +276,8 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
   w.Release();
   const int nl = ix.nl;
   const size_t pairs = size_t(nq) * L;
-  const uint32_t max_items = uint32_t(pairs / smx::kQueriesPerTile + nl + 1);
+  const uint32_t chunks = (uint32_t((ix.max_leaf + 31) / 32) + 31) / 32 + 1;
+  const uint32_t max_items = uint32_t((pairs / smx::kQueriesPerTile + nl + 1) * chunks);
   int rc;
   if ((rc = DAlloc(&w.queries, size_t(nq) * ix.dim)) || (rc = DAlloc(&w.topl_leaf, pairs)) ||
       (rc = DAlloc(&w.topl_dist, pairs)) || (rc = DAlloc(&w.scores, size_t(nq) * nl)) ||
@@ -331,7 +332,8 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   uint32_t* fill = w.counters + nl;
   uint32_t* work = w.counters + 2 * nl;
   // stats: [0] overflow flag [1] max overflowing count [2] max count
-  //        [3] pairs [4] work items [5] pad [6..7] code bytes (u64)
+  //        [3] pairs [4] work items [5] item-tiles (MFMA tiles of the scan)
+  //        [6..7] code bytes (u64) [8] survivors summed over queries
   uint32_t* stats = ((reinterpret_cast<uintptr_t>(work + 1) & 7) == 0) ? work + 1 : work + 2;
   unsigned long long* code_bytes = reinterpret_cast<unsigned long long*>(stats + 6);
   const int seed = std::min(h->seed_leaves, L);
@@ -413,7 +415,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sel.overflow = stats;
 
   int retries = 0;
-  uint32_t st[8] = {0};
+  uint32_t st[10] = {0};
   for (;;) {
     SMX_HIP(smx::LaunchScan(ix, a, h->grid, s));
     Mark(h, 6, s);
@@ -426,6 +428,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     SMX_HIP(smx::LaunchTighten(w.cand, w.cand_count, w.cap, nq, kk, w.tau, s));
     SMX_HIP(hipMemsetAsync(w.cand_count, 0, sizeof(uint32_t) * nq, s));
     SMX_HIP(hipMemsetAsync(stats, 0, sizeof(uint32_t) * 3, s));
+    SMX_HIP(hipMemsetAsync(stats + 8, 0, sizeof(uint32_t), s));
     SMX_HIP(hipMemsetAsync(work, 0, sizeof(uint32_t), s));
   }
   smx_timings& t = h->timings;
@@ -448,6 +451,8 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   t.scan_pairs = int32_t(st[3]);
   t.overflow_retries = retries;
   t.max_candidates = int32_t(st[2]);
+  t.scan_item_tiles = double(st[5]);
+  t.mean_candidates = float(st[8]) / float(nq);
   return SMX_OK;
 }
 
