@@ -117,10 +117,10 @@ hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq,
                           hipStream_t s);
 hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf,
                        const float* topl_dist, int nq, int L, uint32_t* cnt /*[nl]*/,
-                       uint32_t* fill /*[nl]*/, uint32_t* pair_off /*[nl+1]*/,
-                       uint32_t* tile_prefix /*[nl+1]*/, uint32_t* pair_q /*[nq*L]*/,
-                       float* pair_bias /*[nq*L]*/, uint2* work /*[max items]*/,
-                       uint32_t* totals /*[2] pairs, items*/,
+                       uint32_t* block_cnt /*[ceil(nq*L/4096)][nl]*/,
+                       uint32_t* pair_off /*[nl]*/, uint32_t* tile_prefix /*[nl+1]*/,
+                       uint32_t* pair_q /*[nq*L]*/, float* pair_bias /*[nq*L]*/,
+                       uint2* work /*[max items]*/, uint32_t* totals /*[3]*/,
                        unsigned long long* code_bytes /*[1]*/, hipStream_t s);
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, hipStream_t s);
 hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s);

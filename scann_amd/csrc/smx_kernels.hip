@@ -323,13 +323,41 @@ __device__ __forceinline__ uint32_t LeafChunks(uint32_t n) {
 // list into 32-query work items, listed largest leaf first (longest items
 // dequeued first).
 // ---------------------------------------------------------------------------
-__global__ void pairs_count_kernel(const int32_t* __restrict__ topl_leaf, int n,
-                                   uint32_t* __restrict__ cnt) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int leaf = topl_leaf[i];
-  if (leaf < 0) return;
-  atomicAdd(&cnt[leaf], 1u);
+// Block-local counting: every block histograms kPairsPerBlock pairs in LDS and
+// publishes one count per (block, leaf) -- no contended global atomics.
+constexpr int kPairsPerBlock = 4096;
+
+__global__ void __launch_bounds__(256) pairs_count_kernel(const int32_t* __restrict__ topl_leaf,
+                                                          int n, int nl,
+                                                          uint32_t* __restrict__ block_cnt,
+                                                          uint32_t* __restrict__ cnt) {
+  extern __shared__ uint32_t hist[];
+  for (int l = threadIdx.x; l < nl; l += blockDim.x) hist[l] = 0;
+  __syncthreads();
+  const int beg = blockIdx.x * kPairsPerBlock, end = min(n, beg + kPairsPerBlock);
+  for (int i = beg + threadIdx.x; i < end; i += blockDim.x) {
+    const int leaf = topl_leaf[i];
+    if (leaf >= 0) atomicAdd(&hist[leaf], 1u);
+  }
+  __syncthreads();
+  uint32_t* bc = block_cnt + size_t(blockIdx.x) * nl;
+  for (int l = threadIdx.x; l < nl; l += blockDim.x) {
+    const uint32_t c = hist[l];
+    bc[l] = c;
+    if (c) atomicAdd(&cnt[l], c);
+  }
+}
+
+// Exclusive prefix over blocks for every leaf: block b's first slot in leaf l.
+__global__ void pairs_block_offsets_kernel(uint32_t* __restrict__ block_cnt, int nblocks, int nl) {
+  const int l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= nl) return;
+  uint32_t run = 0;
+  for (int b = 0; b < nblocks; ++b) {
+    const uint32_t c = block_cnt[size_t(b) * nl + l];
+    block_cnt[size_t(b) * nl + l] = run;
+    run += c;
+  }
 }
 
 __global__ void __launch_bounds__(1024) pairs_scan_kernel(const uint32_t* __restrict__ cnt,
@@ -404,18 +432,22 @@ __global__ void __launch_bounds__(1024) pairs_scan_kernel(const uint32_t* __rest
   }
 }
 
-__global__ void pairs_scatter_kernel(const int32_t* __restrict__ topl_leaf,
-                                     const float* __restrict__ topl_dist, int n, int L,
-                                     const uint32_t* __restrict__ pair_off,
-                                     uint32_t* __restrict__ fill, uint32_t* __restrict__ pair_q,
-                                     float* __restrict__ pair_bias) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int leaf = topl_leaf[i];
-  if (leaf < 0) return;
-  const uint32_t pos = pair_off[leaf] + atomicAdd(&fill[leaf], 1u);
-  pair_q[pos] = uint32_t(i / L);
-  pair_bias[pos] = topl_dist[i];
+__global__ void __launch_bounds__(256) pairs_scatter_kernel(
+    const int32_t* __restrict__ topl_leaf, const float* __restrict__ topl_dist, int n, int L, int nl,
+    const uint32_t* __restrict__ pair_off, const uint32_t* __restrict__ block_off,
+    uint32_t* __restrict__ pair_q, float* __restrict__ pair_bias) {
+  extern __shared__ uint32_t fill[];
+  for (int l = threadIdx.x; l < nl; l += blockDim.x) fill[l] = 0;
+  __syncthreads();
+  const uint32_t* bo = block_off + size_t(blockIdx.x) * nl;
+  const int beg = blockIdx.x * kPairsPerBlock, end = min(n, beg + kPairsPerBlock);
+  for (int i = beg + threadIdx.x; i < end; i += blockDim.x) {
+    const int leaf = topl_leaf[i];
+    if (leaf < 0) continue;
+    const uint32_t pos = pair_off[leaf] + bo[leaf] + atomicAdd(&fill[leaf], 1u);
+    pair_q[pos] = uint32_t(i / L);
+    pair_bias[pos] = topl_dist[i];
+  }
 }
 
 __global__ void pairs_work_kernel(const uint32_t* __restrict__ tile_prefix,
@@ -636,19 +668,29 @@ __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
     const float bias = a.residual ? a.topl_dist[size_t(qi) * a.L + r] : 0.0f;
     const uint32_t n = min(a.leaf_size[leaf], uint32_t(kSeedCap) - base);
     const uint8_t* tb = a.tiles + a.tile_off[leaf] * 64ull * W;
-    for (uint32_t dp = threadIdx.x; dp < n; dp += blockDim.x) {
-      const uint8_t* t0 = tb + ((dp >> 5) * 64 + (dp & 31)) * W;
-      uint32_t c0[NW], c1[NW];
-      LoadCodes<K>(t0, c0);
-      LoadCodes<K>(t0 + 32 * W, c1);
-      int acc = 0;
+    // 4 datapoints per thread per round, all code loads issued first
+    constexpr int U = 4;
+    for (uint32_t d0 = threadIdx.x; d0 < n; d0 += U * blockDim.x) {
+      uint32_t c0[U][NW], c1[U][NW];
 #pragma unroll
-      for (int s = 0; s < K; ++s) {
-        const uint32_t n0 = (c0[s >> 3] >> ((s & 7) * 4)) & 15u;
-        const uint32_t n1 = (c1[s >> 3] >> ((s & 7) * 4)) & 15u;
-        acc += int(lut[(2 * s) * 16 + n0]) + int(lut[(2 * s + 1) * 16 + n1]);
+      for (int u = 0; u < U; ++u) {
+        const uint32_t dp = min(d0 + u * blockDim.x, n - 1);
+        const uint8_t* t0 = tb + ((dp >> 5) * 64 + (dp & 31)) * W;
+        LoadCodes<K>(t0, c0[u]);
+        LoadCodes<K>(t0 + 32 * W, c1[u]);
       }
-      vals[base + dp] = OrderedBits(DistOf(acc, inv, bias));
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t dp = d0 + u * blockDim.x;
+        int acc = 0;
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+          const uint32_t n0 = (c0[u][s >> 3] >> ((s & 7) * 4)) & 15u;
+          const uint32_t n1 = (c1[u][s >> 3] >> ((s & 7) * 4)) & 15u;
+          acc += int(lut[(2 * s) * 16 + n0]) + int(lut[(2 * s + 1) * 16 + n1]);
+        }
+        if (dp < n) vals[base + dp] = OrderedBits(DistOf(acc, inv, bias));
+      }
     }
     base += n;
   }
@@ -952,18 +994,24 @@ hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq, i
 }
 
 hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf, const float* topl_dist,
-                       int nq, int L, uint32_t* cnt, uint32_t* fill, uint32_t* pair_off,
+                       int nq, int L, uint32_t* cnt, uint32_t* block_cnt, uint32_t* pair_off,
                        uint32_t* tile_prefix, uint32_t* pair_q, float* pair_bias, uint2* work,
                        uint32_t* totals, unsigned long long* code_bytes, hipStream_t s) {
   const int n = nq * L;
-  const int blocks = (n + 255) / 256;
+  const int nblocks = (n + kPairsPerBlock - 1) / kPairsPerBlock;
+  const size_t lds = size_t(ix.nl) * 4;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (n > 0)
-    hipLaunchKernelGGL(pairs_count_kernel, dim3(blocks), dim3(256), 0, s, topl_leaf, n, cnt);
+    hipLaunchKernelGGL(pairs_count_kernel, dim3(nblocks), dim3(256), lds, s, topl_leaf, n, ix.nl,
+                       block_cnt, cnt);
   hipLaunchKernelGGL(pairs_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, ix.leaf_order,
                      ix.leaf_size, ix.nl, ix.nb, pair_off, tile_prefix, totals, code_bytes);
-  if (n > 0)
-    hipLaunchKernelGGL(pairs_scatter_kernel, dim3(blocks), dim3(256), 0, s, topl_leaf, topl_dist,
-                       n, L, pair_off, fill, pair_q, pair_bias);
+  if (n > 0) {
+    hipLaunchKernelGGL(pairs_block_offsets_kernel, dim3((ix.nl + 255) / 256), dim3(256), 0, s,
+                       block_cnt, nblocks, ix.nl);
+    hipLaunchKernelGGL(pairs_scatter_kernel, dim3(nblocks), dim3(256), lds, s, topl_leaf,
+                       topl_dist, n, L, ix.nl, pair_off, block_cnt, pair_q, pair_bias);
+  }
   hipLaunchKernelGGL(pairs_work_kernel, dim3((ix.nl + 255) / 256), dim3(256), 0, s, tile_prefix,
                      ix.leaf_order, ix.leaf_size, ix.nl, work);
   return hipGetLastError();

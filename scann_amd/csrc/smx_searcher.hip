@@ -82,7 +82,8 @@ struct Workspace {
   int8_t* lut = nullptr;
   float* mult = nullptr;
   float* inv = nullptr;
-  uint32_t* counters = nullptr;     // cnt[nl] | fill[nl] | work counter | stats[16]
+  uint32_t* counters = nullptr;     // cnt[nl] | spare[nl] | work counter | stats[16]
+  uint32_t* block_cnt = nullptr;    // [ceil(nq*L/4096)][nl] per-block leaf counts
   uint32_t* pair_off = nullptr;     // [nl+1]
   uint32_t* tile_prefix = nullptr;  // [nl+1]
   uint32_t* pair_q = nullptr;       // [nq*L]
@@ -98,7 +99,7 @@ struct Workspace {
   void Release() {
     DFree(queries); DFree(topl_leaf); DFree(topl_dist); DFree(scores); DFree(lut); DFree(mult);
     DFree(inv);
-    DFree(counters); DFree(pair_off); DFree(tile_prefix); DFree(pair_q); DFree(pair_bias);
+    DFree(counters); DFree(block_cnt); DFree(pair_off); DFree(tile_prefix); DFree(pair_q); DFree(pair_bias);
     DFree(work); DFree(tau); DFree(cand); DFree(cand_count); DFree(out_idx); DFree(out_dist);
     DFree(out_count);
     nq = L = kk = dim = width = 0;
@@ -115,7 +116,7 @@ struct smx_index {
   std::mutex mu;
   Workspace ws;
   uint32_t cap_per_query = 4096;   // candidate list capacity
-  int seed_leaves = 4;
+  int seed_leaves = 2;
   int grid = 0;                    // scan grid (blocks of 4 waves)
   bool profiling = false;
   smx_timings timings{};
@@ -283,6 +284,7 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
       (rc = DAlloc(&w.topl_dist, pairs)) || (rc = DAlloc(&w.scores, size_t(nq) * nl)) ||
       (rc = DAlloc(&w.lut, size_t(nq) * 2 * ix.ksteps * 16)) || (rc = DAlloc(&w.mult, nq)) ||
       (rc = DAlloc(&w.inv, nq)) || (rc = DAlloc(&w.counters, size_t(2) * nl + 20)) ||
+      (rc = DAlloc(&w.block_cnt, ((pairs + 4095) / 4096) * size_t(nl))) ||
       (rc = DAlloc(&w.pair_off, size_t(nl + 1))) || (rc = DAlloc(&w.tile_prefix, size_t(nl + 1))) ||
       (rc = DAlloc(&w.pair_q, pairs)) || (rc = DAlloc(&w.pair_bias, pairs)) ||
       (rc = DAlloc(&w.work, max_items)) || (rc = DAlloc(&w.tau, nq)) ||
@@ -329,7 +331,6 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   Workspace& w = h->ws;
   const int nl = ix.nl;
   uint32_t* cnt = w.counters;
-  uint32_t* fill = w.counters + nl;
   uint32_t* work = w.counters + 2 * nl;
   // stats: [0] overflow flag [1] max overflowing count [2] max count
   //        [3] pairs [4] work items [5] item-tiles (MFMA tiles of the scan)
@@ -346,7 +347,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   Mark(h, 1, s);
   SMX_HIP(smx::LaunchLutBuild(ix, queries, nq, w.lut, w.mult, w.inv, nullptr, s));
   Mark(h, 2, s);
-  SMX_HIP(smx::LaunchPairs(ix, w.topl_leaf, w.topl_dist, nq, L, cnt, fill, w.pair_off,
+  SMX_HIP(smx::LaunchPairs(ix, w.topl_leaf, w.topl_dist, nq, L, cnt, w.block_cnt, w.pair_off,
                            w.tile_prefix, w.pair_q, w.pair_bias, w.work, stats + 3, code_bytes,
                            s));
   Mark(h, 3, s);

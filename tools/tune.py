@@ -22,7 +22,7 @@ def main():
     qd = torch.from_numpy(q).cuda()
     oi = torch.zeros((NQ, FINAL_NN), dtype=torch.int32, device="cuda")
     od = torch.zeros((NQ, FINAL_NN), dtype=torch.float32, device="cuda")
-    for cap, seed in [(4096, 2), (4096, 4), (4096, 8)]:
+    for cap, seed in [(4096, 2), (4096, 3), (4096, 4)]:
         nat.set_tuning(cap, seed)
         acc = {}
         steps = 10
