@@ -56,7 +56,7 @@ SIGNATURES = {
     "smx_lut16_leaf_scores": (ctypes.c_int, [_vp, _i32, _vp, _vp]),
     "smx_set_profiling": (ctypes.c_int, [_vp, _i32]),
     "smx_get_timings": (ctypes.c_int, [_vp, ctypes.POINTER(Timings)]),
-    "smx_set_tuning": (ctypes.c_int, [_vp, _i32, _i32]),
+    "smx_set_tuning": (ctypes.c_int, [_vp, _i32, _i32, _i32, _i32]),
     "smx_last_error": (ctypes.c_char_p, []),
     "smx_version": (ctypes.c_char_p, []),
 }
@@ -201,6 +201,7 @@ class NativeIndex:
         check(self.lib.smx_get_timings(self.h, ctypes.byref(t)), "smx_get_timings")
         return t.as_dict()
 
-    def set_tuning(self, candidates_per_query: int, seed_leaves: int):
-        check(self.lib.smx_set_tuning(self.h, int(candidates_per_query), int(seed_leaves)),
-              "smx_set_tuning")
+    def set_tuning(self, candidates_per_query: int = 4096, seed_leaves: int = 2,
+                   scan_variant: int = 0, chunk_tiles: int = 0):
+        check(self.lib.smx_set_tuning(self.h, int(candidates_per_query), int(seed_leaves),
+                                      int(scan_variant), int(chunk_tiles)), "smx_set_tuning")

@@ -63,6 +63,7 @@ struct ScanArgs {
   uint32_t* cand_count;       // [nq]
   uint32_t* work_counter;
   uint32_t cap;
+  uint32_t chunk_tiles;       // tiles per work item (LeafChunks)
   int nl;
   int nb;
   int shift;
@@ -121,8 +122,13 @@ hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf,
                        uint32_t* pair_off /*[nl]*/, uint32_t* tile_prefix /*[nl+1]*/,
                        uint32_t* pair_q /*[nq*L]*/, float* pair_bias /*[nq*L]*/,
                        uint2* work /*[max items]*/, uint32_t* totals /*[3]*/,
-                       unsigned long long* code_bytes /*[1]*/, hipStream_t s);
-hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, hipStream_t s);
+                       unsigned long long* code_bytes /*[1]*/, uint32_t chunk_tiles,
+                       uint32_t queries_per_item /*32 or 64*/, hipStream_t s);
+// variant 0: block-level items of 32 queries, LUT rows in LDS (default);
+// 1: wave-level items with the LUT rows in VGPRs; 2: block items of 64
+// queries (one one-hot A fragment feeds two MFMAs), 4 waves; 3: as 2 with 8.
+hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,
+                      hipStream_t s);
 hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s);
 hipError_t LaunchTighten(const uint64_t* cand, const uint32_t* cand_count, uint32_t cap,
                          int nq, int kk, uint64_t* tau_key, hipStream_t s);

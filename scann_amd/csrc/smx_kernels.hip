@@ -21,6 +21,8 @@
 //                           (one_to_many_symmetric.h:373-503) and SortAndDrop
 //                           (single_machine_base.cc:872-901)
 #include <hip/hip_runtime.h>
+
+#include <climits>
 #include <stdint.h>
 
 #include <algorithm>
@@ -311,11 +313,10 @@ __global__ void __launch_bounds__(256) lut_build_kernel(
 }
 
 // Work items split a leaf's 32-datapoint tiles into chunks of at most
-// kChunkTiles so that no single wave owns a whole large leaf.
-constexpr uint32_t kChunkTiles = 32;
-__device__ __forceinline__ uint32_t LeafChunks(uint32_t n) {
+// chunk_tiles so that no single wave (or block) owns a whole large leaf.
+__device__ __forceinline__ uint32_t LeafChunks(uint32_t n, uint32_t chunk_tiles) {
   const uint32_t tiles = (n + 31u) / 32u;
-  return tiles == 0 ? 1u : (tiles + kChunkTiles - 1) / kChunkTiles;
+  return tiles == 0 ? 1u : (tiles + chunk_tiles - 1) / chunk_tiles;
 }
 
 // ---------------------------------------------------------------------------
@@ -363,7 +364,8 @@ __global__ void pairs_block_offsets_kernel(uint32_t* __restrict__ block_cnt, int
 __global__ void __launch_bounds__(1024) pairs_scan_kernel(const uint32_t* __restrict__ cnt,
                                                           const uint32_t* __restrict__ order,
                                                           const uint32_t* __restrict__ leaf_size,
-                                                          int nl, int nb,
+                                                          int nl, int nb, uint32_t chunk_tiles,
+                                                          uint32_t qpi,
                                                           uint32_t* __restrict__ pair_off,
                                                           uint32_t* __restrict__ tile_prefix,
                                                           uint32_t* __restrict__ totals,
@@ -380,7 +382,7 @@ __global__ void __launch_bounds__(1024) pairs_scan_kernel(const uint32_t* __rest
     const uint32_t leaf = order[p];
     const uint32_t c = cnt[leaf];
     sp += c;
-    st += ((c + kQueriesPerTile - 1) / kQueriesPerTile) * LeafChunks(leaf_size[leaf]);
+    st += ((c + qpi - 1) / qpi) * LeafChunks(leaf_size[leaf], chunk_tiles);
     sit += ((c + kQueriesPerTile - 1) / kQueriesPerTile) * ((leaf_size[leaf] + 31u) / 32u);
     // algorithmic code bytes: 16 * B * ceil(n / 32) per (query, leaf) pair
     sb += 16ull * nb * ((leaf_size[leaf] + 31u) / 32u) * c;
@@ -423,7 +425,7 @@ __global__ void __launch_bounds__(1024) pairs_scan_kernel(const uint32_t* __rest
     pair_off[leaf] = rp;
     tile_prefix[p] = rt;
     rp += c;
-    rt += ((c + kQueriesPerTile - 1) / kQueriesPerTile) * LeafChunks(leaf_size[leaf]);
+    rt += ((c + qpi - 1) / qpi) * LeafChunks(leaf_size[leaf], chunk_tiles);
   }
   if (threadIdx.x == blockDim.x - 1) {
     tile_prefix[nl] = s_tiles[blockDim.x - 1];
@@ -453,11 +455,11 @@ __global__ void __launch_bounds__(256) pairs_scatter_kernel(
 __global__ void pairs_work_kernel(const uint32_t* __restrict__ tile_prefix,
                                   const uint32_t* __restrict__ order,
                                   const uint32_t* __restrict__ leaf_size, int nl,
-                                  uint2* __restrict__ work) {
+                                  uint32_t chunk_tiles, uint2* __restrict__ work) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= nl) return;
   const uint32_t leaf = order[p];
-  const uint32_t chunks = LeafChunks(leaf_size[leaf]);
+  const uint32_t chunks = LeafChunks(leaf_size[leaf], chunk_tiles);
   // item = (leaf, query tile << 16 | dp chunk); chunk-major so that a leaf's
   // first chunks (all query tiles) are dequeued together
   for (uint32_t w = tile_prefix[p]; w < tile_prefix[p + 1]; ++w) {
@@ -495,6 +497,21 @@ __device__ __forceinline__ v4i OneHot16(uint32_t sh) {
   r[1] = int(hi & ~m);
   r[2] = int(lo & m);
   r[3] = int(hi & m);
+  return r;
+}
+
+// One-hot of the 4-bit code at bit offset `sh` of `wv`: the select bit
+// (code >= 8) and its complement are each shifted by 8*(code & 7), giving the
+// low and high 8-byte halves directly (6 VALU ops instead of mask-and-select).
+__device__ __forceinline__ v4i OneHotNibble(uint32_t wv, int sh) {
+  const uint32_t s8 = (sh >= 3 ? (wv >> (sh - 3)) : (wv << (3 - sh))) & 0x38u;
+  const uint64_t hb = (wv >> (sh + 3)) & 1u;
+  const uint64_t lo = (hb ^ 1u) << s8, hi = hb << s8;
+  v4i r;
+  r[0] = int(uint32_t(lo));
+  r[1] = int(uint32_t(lo >> 32));
+  r[2] = int(uint32_t(hi));
+  r[3] = int(uint32_t(hi >> 32));
   return r;
 }
 
@@ -591,8 +608,8 @@ __global__ void __launch_bounds__(256) lut16_scan_kernel(ScanArgs a) {
                          : SumLimit(FromOrdered(uint32_t(T >> 32)), inv, bias, smin, smax);
     const uint32_t n = a.leaf_size[leaf];
     const uint32_t ntile_leaf = (n + kDpPerTile - 1) / kDpPerTile;
-    const uint32_t j0 = chunk * kChunkTiles;
-    const uint32_t ntile = min(ntile_leaf, j0 + kChunkTiles);
+    const uint32_t j0 = chunk * a.chunk_tiles;
+    const uint32_t ntile = min(ntile_leaf, j0 + a.chunk_tiles);
     const uint8_t* tb = a.tiles + a.tile_off[leaf] * 64ull * W + size_t(lane) * W;
     const uint64_t moff = a.member_off[leaf];
     uint32_t codes[NW], next[NW];
@@ -749,6 +766,313 @@ __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
         break;
       }
     }
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Block-level variant (default): a 256-thread block owns a work item
+// (leaf, 32 queries, chunk of tiles); the 32 queries' int8 LUT rows sit in
+// LDS step-major ([2K][32 queries][16 B]: one wave-wide ds_read_b128 per MFMA,
+// conflict-free), the 4 waves take the chunk's tiles round-robin, and
+// survivors are staged per query in LDS (one global atomic per query per
+// item).  Frees the ~100 VGPRs the wave variant spends on B fragments.
+// ---------------------------------------------------------------------------
+// Tile body of the block kernel: K MFMAs per query tile on the same one-hot
+// A fragment (QT = 2 feeds two MFMAs per one-hot build), then the threshold
+// epilogue per query tile.
+template <int K, int QT>
+struct BlockScan {
+  static constexpr int NW = ((((K + 1) / 2) + 3) / 4);
+  static constexpr int W = 4 * NW;
+  static constexpr int Q = 32 * QT;
+  static constexpr int SL = 4;   // survivor slots per lane and item
+};
+
+// The second bound is the occupancy (waves per SIMD) the LDS footprint
+// allows; it caps the register budget to match.
+// Waves per SIMD that the block's LDS footprint allows (capped at 4); used
+// as the occupancy target so the register budget matches.
+constexpr int BlockOccupancy(int k, int qt, int nwv) {
+  const int q = 32 * qt;
+  const int bytes = 2 * k * q * 16 + nwv * qt * 64 * (4 * 4 + 8) + q * 24 + 64;
+  const int blocks = (160 * 1024) / bytes;
+  const int w = blocks * nwv / 4;
+  return w > 4 ? 4 : (w < 1 ? 1 : w);
+}
+
+// K MFMAs of one 32-datapoint tile against NB query tiles whose LUT rows sit
+// in LDS ([2K][Q] x 16 B, this lane's row at lut[2s*Q + off]); B fragments
+// are read kRing steps ahead of their MFMA so LDS latency stays hidden.
+constexpr int kRing = 4;
+template <int K, int Q, int NB, int NACC, bool HOIST>
+__device__ __forceinline__ void TileMfma(const uint32_t* codes, const v4i* lut, int off,
+                                         v16i (&acc)[NACC]) {
+  // HOIST: the LUT reads are loop-invariant over the item's tiles and the
+  // compiler keeps them in VGPRs; otherwise an opaque offset forces per-tile
+  // LDS reads (fewer VGPRs, LDS latency on the MFMA chain)
+  if (!HOIST) asm volatile("" : "+v"(off));
+  v4i b[kRing][NB];
+#pragma unroll
+  for (int p = 0; p < kRing; ++p)
+#pragma unroll
+    for (int t = 0; t < NB; ++t)
+      if (p < K) b[p][t] = lut[2 * p * Q + off + 32 * t];
+#pragma unroll
+  for (int t = 0; t < NB; ++t) acc[t] = v16i{0};
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    const v4i oh = OneHotNibble(codes[s >> 3], (s & 7) * 4);
+#pragma unroll
+    for (int t = 0; t < NB; ++t)
+      acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(oh, b[s % kRing][t], acc[t], 0, 0, 0);
+    if (s + kRing < K) {
+#pragma unroll
+      for (int t = 0; t < NB; ++t) b[s % kRing][t] = lut[2 * (s + kRing) * Q + off + 32 * t];
+    }
+    // pin the interleave: one-hot VALU, the MFMA(s), then the ring refill
+    __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, NB, 0);
+    if (s + kRing < K) __builtin_amdgcn_sched_group_barrier(0x100, NB, 0);
+  }
+}
+
+// K MFMAs of one tile with the LUT fragments already in registers.
+template <int K>
+__device__ __forceinline__ v16i TileMfmaReg(const uint32_t* codes, const v4i* frag) {
+  v16i acc = {0};
+#pragma unroll
+  for (int s = 0; s < K; ++s)
+    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(OneHotNibble(codes[s >> 3], (s & 7) * 4), frag[s],
+                                                acc, 0, 0, 0);
+  return acc;
+}
+
+// ABL: 8 = LUT fragments held in VGPRs for the whole item (3 waves/SIMD);
+// timing ablations only (results invalid): 2 = no code loads, 4 = no
+// epilogue, 16 = nothing passes the threshold, 32 = no flush.
+template <int K, int QT, int NWV, int ABL = 0>
+__global__ void __launch_bounds__(64 * NWV, ((ABL & 8) ? 3 : BlockOccupancy(K, QT, NWV)))
+    lut16_scan_block_kernel(ScanArgs a) {
+  using B = BlockScan<K, QT>;
+  constexpr int NW = B::NW, W = B::W, Q = B::Q, SL = B::SL, NT = 64 * NWV;
+  __shared__ v4i lut_s[2 * K * Q];
+  // per-lane survivor slots: [wave][query tile][lane][SL] of (sum << 16 | dp)
+  __shared__ uint32_t lstage[NWV * QT * 64 * SL];
+  __shared__ uint32_t lcnt[NWV * QT * 64], loff[NWV * QT * 64];
+  __shared__ uint32_t q_id[Q];
+  __shared__ float q_bias[Q], q_inv[Q];
+  __shared__ int q_amax[Q];
+  __shared__ uint64_t q_T[Q];
+  __shared__ uint32_t s_w;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int c = lane & 31;
+  const int h = lane >> 5;
+  const uint32_t total = a.tile_prefix[a.nl];
+  const int smin = -128 * a.nb, smax = 128 * a.nb;
+  for (;;) {
+    if (tid == 0) s_w = atomicAdd(a.work_counter, 1u);
+    __syncthreads();
+    const uint32_t w = s_w;
+    if (w >= total) break;
+    const uint2 item = a.work[w];
+    const int leaf = int(item.x);
+    const uint32_t t = item.y >> 16;
+    const uint32_t chunk = item.y & 0xFFFFu;
+    const uint32_t pbeg = a.pair_off[leaf] + t * uint32_t(Q);
+    const int nvalid = int(min(uint32_t(Q), a.pair_off[leaf] + a.leaf_count[leaf] - pbeg));
+    // per-query-slot metadata, then the LUT rows ([2K][Q] step-major)
+    for (int i = tid; i < Q; i += NT) {
+      const bool v = i < nvalid;
+      const uint32_t pidx = pbeg + uint32_t(v ? i : 0);
+      const uint32_t qid = a.pair_q[pidx];
+      const float bias = a.residual ? a.pair_bias[pidx] : 0.0f;
+      const float inv = a.inv[qid];
+      const uint64_t T = a.tau_key[qid];
+      q_id[i] = qid;
+      q_bias[i] = bias;
+      q_inv[i] = inv;
+      q_T[i] = T;
+      q_amax[i] = !v ? smin - 1
+                : (T == kNoThreshold) ? smax
+                : SumLimit(FromOrdered(uint32_t(T >> 32)), inv, bias, smin, smax);
+    }
+    for (int e = tid; e < K * Q; e += NT) {
+      const int qs = e % Q, rp = e / Q;   // rows 2rp, 2rp+1 of query slot qs
+      const uint32_t pidx = pbeg + uint32_t(qs < nvalid ? qs : 0);
+      const v4i* src = reinterpret_cast<const v4i*>(a.lut) + size_t(a.pair_q[pidx]) * 2 * K + 2 * rp;
+      const v4i r0 = src[0], r1 = src[1];
+      lut_s[(2 * rp) * Q + qs] = r0;
+      lut_s[(2 * rp + 1) * Q + qs] = r1;
+    }
+    __syncthreads();
+    const bool two = QT == 2 && nvalid > 32;   // block-uniform
+    uint32_t qid[QT], ns[QT];
+    float bias[QT], inv[QT];
+    int amax[QT];
+    uint64_t T[QT];
+#pragma unroll
+    for (int u = 0; u < QT; ++u) {
+      qid[u] = q_id[u * 32 + c];
+      bias[u] = q_bias[u * 32 + c];
+      inv[u] = q_inv[u * 32 + c];
+      amax[u] = (ABL & 16) ? smin - 1 : q_amax[u * 32 + c];
+      T[u] = q_T[u * 32 + c];
+      ns[u] = 0;
+    }
+    const uint32_t n = a.leaf_size[leaf];
+    const uint32_t ntile_leaf = (n + kDpPerTile - 1) / kDpPerTile;
+    const uint32_t j0 = chunk * a.chunk_tiles;
+    const uint32_t jend = min(ntile_leaf, j0 + a.chunk_tiles);
+    const uint8_t* tb = a.tiles + a.tile_off[leaf] * 64ull * W + size_t(lane) * W;
+    const uint64_t moff = a.member_off[leaf];
+
+    constexpr bool kRegFrag = QT == 1 && (ABL & 8);
+    v4i frag[kRegFrag ? K : 1];
+    if (kRegFrag) {
+#pragma unroll
+      for (int s2 = 0; s2 < K; ++s2) frag[s2] = lut_s[(2 * s2 + h) * Q + c];
+    }
+    auto body = [&](const uint32_t (&codes)[NW], uint32_t j) {
+      v16i acc[QT];
+      if (kRegFrag)
+        acc[0] = TileMfmaReg<K>(codes, frag);
+      else if (QT == 2 && two)
+        TileMfma<K, Q, 2, QT, false>(codes, lut_s, h * Q + c, acc);
+      else
+        TileMfma<K, Q, 1, QT, false>(codes, lut_s, h * Q + c, acc);
+      if (ABL & 4) {
+        int m = acc[0][0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) m ^= acc[0][i];
+        if (m == 0x7fffffff) a.cand_count[0] = m;
+        return;
+      }
+      const uint32_t rows_left = n - j * kDpPerTile;
+      const bool full = rows_left >= uint32_t(kDpPerTile);   // wave-uniform
+#pragma unroll
+      for (int u = 0; u < QT; ++u) {
+        if (u == 1 && !two) break;
+        // one compare per lane on the tile minimum; survivors are rare, so
+        // the per-element tests below run under a mostly empty exec mask
+        int m = min(min(acc[u][0], acc[u][1]), acc[u][2]);
+#pragma unroll
+        for (int i = 3; i < 15; i += 2) m = min(min(m, acc[u][i]), acc[u][i + 1]);
+        m = min(m, acc[u][15]);
+        if (m > amax[u]) continue;
+        uint32_t* st = lstage + ((wave * QT + u) * 64 + lane) * SL;
+        // wave-uniform list of the elements some lane passes (ballots), then
+        // a scalar loop over just those: no per-element branch structure
+        if (!full) {  // last tile of the leaf: rows past its end never pass
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const uint32_t row = (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (row >= rows_left) acc[u][i] = INT_MAX;
+          }
+        }
+        uint32_t emask = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          emask |= (__builtin_amdgcn_ballot_w64(acc[u][i] <= amax[u]) != 0 ? 1u : 0u) << i;
+        while (emask) {
+          const int i = __builtin_ctz(emask);
+          emask &= emask - 1;
+          int v = acc[u][0];
+#pragma unroll
+          for (int k = 1; k < 16; ++k) v = (k == i) ? acc[u][k] : v;
+          const uint32_t row = (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (v <= amax[u]) {
+            // slot = (sum, local dp) packed in 32 bits; the distance, the key
+            // and the exact threshold test are applied at the flush
+            const uint32_t dp = j * kDpPerTile + row;
+            if (ns[u] < uint32_t(SL)) {
+              st[ns[u]] = (uint32_t(v) << 16) | dp;
+            } else {  // lane slots full (rare): straight to the global list
+              const float d = DistOf(v, inv[u], bias[u]);
+              const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp)
+                                               : a.members[moff + dp];
+              const uint64_t key = (uint64_t(OrderedBits(d)) << 32) | tie;
+              if (key <= T[u]) {
+                const uint32_t gs = atomicAdd(&a.cand_count[qid[u]], 1u);
+                if (gs < a.cap) a.cand[size_t(qid[u]) * a.cap + gs] = key;
+              }
+            }
+            ++ns[u];
+          }
+        }
+      }
+    };
+
+    // codes of the next tile are loaded while the current one is scored
+    uint32_t codes[NW], next[NW];
+    uint32_t j = j0 + wave;
+    if (j < jend) LoadCodes<K>(tb + size_t(j) * 64 * W, codes);
+    for (; j < jend; j += NWV) {
+      if (ABL & 2) {
+#pragma unroll
+        for (int i = 0; i < NW; ++i) next[i] = codes[i] * 0x9E3779B9u + j;
+      } else if (j + NWV < jend) LoadCodes<K>(tb + size_t(j + NWV) * 64 * W, next);
+      body(codes, j);
+#pragma unroll
+      for (int i = 0; i < NW; ++i) codes[i] = next[i];
+    }
+    // exact threshold test on this lane's slots (keys at the threshold
+    // distance are decided by the tie id); survivors are compacted in place
+#pragma unroll
+    for (int u = 0; u < QT; ++u) {
+      uint32_t* st = lstage + ((wave * QT + u) * 64 + lane) * SL;
+      const uint32_t m = min(ns[u], uint32_t(SL));
+      uint32_t kept = 0;
+      for (uint32_t k = 0; k < m; ++k) {
+        const uint32_t v = st[k];
+        const int sum = int(v) >> 16;
+        const uint32_t dp = v & 0xFFFFu;
+        const uint32_t ob = OrderedBits(DistOf(sum, inv[u], bias[u]));
+        const uint32_t tob = uint32_t(T[u] >> 32);
+        bool ok = ob < tob;
+        if (ob == tob) {
+          const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp)
+                                           : a.members[moff + dp];
+          ok = tie <= uint32_t(T[u]);
+        }
+        if (ok) st[kept++] = v;
+      }
+      lcnt[(wave * QT + u) * 64 + lane] = kept;
+    }
+    __syncthreads();
+    // flush: per query slot, one global atomic for the survivors its 2*NWV
+    // lanes kept; each lane's slots then land at their running offset
+    for (int i = tid; i < Q; i += NT) {
+      const int u = i >> 5, cc = i & 31;
+      uint32_t tot = 0;
+      for (int wv = 0; wv < NWV; ++wv)
+        for (int hh = 0; hh < 2; ++hh) {
+          const int src = (wv * QT + u) * 64 + hh * 32 + cc;
+          loff[src] = tot;
+          tot += lcnt[src];
+        }
+      const uint32_t base = tot ? atomicAdd(&a.cand_count[q_id[i]], tot) : 0u;
+      for (int wv = 0; wv < NWV; ++wv)
+        for (int hh = 0; hh < 2; ++hh) loff[(wv * QT + u) * 64 + hh * 32 + cc] += base;
+    }
+    __syncthreads();
+    for (int e = tid; e < NWV * QT * 64 * SL; e += NT) {
+      const int src = e / SL, k = e - src * SL;
+      if (uint32_t(k) < lcnt[src]) {
+        const int u = (src / 64) % QT, l = src & 63;
+        const int qs = u * 32 + (l & 31);
+        const uint32_t slot = loff[src] + k;
+        const uint32_t v = lstage[e];
+        const uint32_t dp = v & 0xFFFFu;
+        const float d = DistOf(int(v) >> 16, q_inv[qs], q_bias[qs]);
+        const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp) : a.members[moff + dp];
+        if (slot < a.cap)
+          a.cand[size_t(q_id[qs]) * a.cap + slot] = (uint64_t(OrderedBits(d)) << 32) | tie;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -996,7 +1320,8 @@ hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq, i
 hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf, const float* topl_dist,
                        int nq, int L, uint32_t* cnt, uint32_t* block_cnt, uint32_t* pair_off,
                        uint32_t* tile_prefix, uint32_t* pair_q, float* pair_bias, uint2* work,
-                       uint32_t* totals, unsigned long long* code_bytes, hipStream_t s) {
+                       uint32_t* totals, unsigned long long* code_bytes, uint32_t chunk_tiles,
+                       uint32_t queries_per_item, hipStream_t s) {
   const int n = nq * L;
   const int nblocks = (n + kPairsPerBlock - 1) / kPairsPerBlock;
   const size_t lds = size_t(ix.nl) * 4;
@@ -1005,7 +1330,8 @@ hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf, const fl
     hipLaunchKernelGGL(pairs_count_kernel, dim3(nblocks), dim3(256), lds, s, topl_leaf, n, ix.nl,
                        block_cnt, cnt);
   hipLaunchKernelGGL(pairs_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, ix.leaf_order,
-                     ix.leaf_size, ix.nl, ix.nb, pair_off, tile_prefix, totals, code_bytes);
+                     ix.leaf_size, ix.nl, ix.nb, chunk_tiles, queries_per_item, pair_off,
+                     tile_prefix, totals, code_bytes);
   if (n > 0) {
     hipLaunchKernelGGL(pairs_block_offsets_kernel, dim3((ix.nl + 255) / 256), dim3(256), 0, s,
                        block_cnt, nblocks, ix.nl);
@@ -1013,16 +1339,36 @@ hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf, const fl
                        topl_dist, n, L, ix.nl, pair_off, block_cnt, pair_q, pair_bias);
   }
   hipLaunchKernelGGL(pairs_work_kernel, dim3((ix.nl + 255) / 256), dim3(256), 0, s, tile_prefix,
-                     ix.leaf_order, ix.leaf_size, ix.nl, work);
+                     ix.leaf_order, ix.leaf_size, ix.nl, chunk_tiles, work);
   return hipGetLastError();
 }
 
-#define SMX_SCAN_CASE(KV)                                                        \
-  case KV:                                                                       \
-    hipLaunchKernelGGL(lut16_scan_kernel<KV>, dim3(grid), dim3(256), 0, s, a);   \
+#define SMX_SCAN_CASE(KV)                                                          \
+  case KV:                                                                         \
+    if (variant == 0)                                                              \
+      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 1, 4>), dim3(grid), dim3(256), 0, s, a); \
+    else if (variant == 2)                                                         \
+      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 2, 4>), dim3(grid), dim3(256), 0, s, a); \
+    else if (variant == 3)                                                         \
+      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 2, 8>), dim3(grid / 2), dim3(512), 0, s, a); \
+    else if (variant == 4)                                                         \
+      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 1, 4, 4>), dim3(grid), dim3(256), 0, s, a); \
+    else if (variant == 5)                                                         \
+      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 1, 4, 8>), dim3(grid), dim3(256), 0, s, a); \
+    else if (variant == 7)                                                         \
+      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 1, 4, 12>), dim3(grid), dim3(256), 0, s, a); \
+    else if (variant == 8)                                                         \
+      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 1, 4, 16>), dim3(grid), dim3(256), 0, s, a); \
+    else if (variant == 9)                                                         \
+      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 1, 4, 32>), dim3(grid), dim3(256), 0, s, a); \
+    else if (variant == 6)                                                         \
+      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 1, 4, 6>), dim3(grid), dim3(256), 0, s, a); \
+    else                                                                           \
+      hipLaunchKernelGGL(lut16_scan_kernel<KV>, dim3(grid), dim3(256), 0, s, a);   \
     break;
 
-hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, hipStream_t s) {
+hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,
+                      hipStream_t s) {
   switch (ix.ksteps) {
     SMX_SCAN_CASE(4)
     SMX_SCAN_CASE(8)

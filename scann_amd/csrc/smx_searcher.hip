@@ -117,7 +117,10 @@ struct smx_index {
   Workspace ws;
   uint32_t cap_per_query = 4096;   // candidate list capacity
   int seed_leaves = 2;
-  int grid = 0;                    // scan grid (blocks of 4 waves)
+  int scan_variant = 0;            // see smx::LaunchScan
+  uint32_t chunk_tiles[10] = {32, 32, 32, 32, 32, 32, 32, 32, 32, 32};
+  int grid = 0;                    // wave-variant scan grid (blocks of 4 waves)
+  int grid_block = 0;              // block-variant scan grid
   bool profiling = false;
   smx_timings timings{};
   hipEvent_t ev[16] = {};
@@ -277,7 +280,7 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
   w.Release();
   const int nl = ix.nl;
   const size_t pairs = size_t(nq) * L;
-  const uint32_t chunks = (uint32_t((ix.max_leaf + 31) / 32) + 31) / 32 + 1;
+  const uint32_t chunks = (uint32_t((ix.max_leaf + 31) / 32) + 15) / 16 + 1;  // chunk >= 16
   const uint32_t max_items = uint32_t((pairs / smx::kQueriesPerTile + nl + 1) * chunks);
   int rc;
   if ((rc = DAlloc(&w.queries, size_t(nq) * ix.dim)) || (rc = DAlloc(&w.topl_leaf, pairs)) ||
@@ -347,8 +350,12 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   Mark(h, 1, s);
   SMX_HIP(smx::LaunchLutBuild(ix, queries, nq, w.lut, w.mult, w.inv, nullptr, s));
   Mark(h, 2, s);
+  // the block scan stages 16-bit local datapoint numbers: larger leaves use
+  // the wave scan
+  const int variant = ix.max_leaf > 65535u ? 1 : h->scan_variant;
   SMX_HIP(smx::LaunchPairs(ix, w.topl_leaf, w.topl_dist, nq, L, cnt, w.block_cnt, w.pair_off,
                            w.tile_prefix, w.pair_q, w.pair_bias, w.work, stats + 3, code_bytes,
+                           h->chunk_tiles[variant], (variant == 2 || variant == 3) ? 64u : 32u,
                            s));
   Mark(h, 3, s);
   smx::SeedArgs sa{};
@@ -387,6 +394,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   a.cand_count = w.cand_count;
   a.work_counter = work;
   a.cap = w.cap;
+  a.chunk_tiles = h->chunk_tiles[variant];
   a.nl = nl;
   a.nb = ix.nb;
   a.shift = ix.shift;
@@ -418,7 +426,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   int retries = 0;
   uint32_t st[10] = {0};
   for (;;) {
-    SMX_HIP(smx::LaunchScan(ix, a, h->grid, s));
+    SMX_HIP(smx::LaunchScan(ix, a, variant == 1 ? h->grid : h->grid_block, variant, s));
     Mark(h, 6, s);
     SMX_HIP(smx::LaunchFinalSelect(sel, nq, s));
     Mark(h, 7, s);
@@ -516,6 +524,7 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
   hipDeviceProp_t prop;
   SMX_HIP(hipGetDeviceProperties(&prop, device));
   h->grid = prop.multiProcessorCount * 4;
+  h->grid_block = prop.multiProcessorCount * 4;
   *out = h;
   return SMX_OK;
 }
@@ -747,14 +756,20 @@ int smx_get_timings(const smx_index* h, smx_timings* out) {
   return SMX_OK;
 }
 
-int smx_set_tuning(smx_index* h, int32_t candidates_per_query, int32_t seed_leaves) {
+int smx_set_tuning(smx_index* h, int32_t candidates_per_query, int32_t seed_leaves,
+                   int32_t scan_variant, int32_t chunk_tiles) {
   if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
+  if (scan_variant < 0 || scan_variant > 9) return Fail(SMX_INVALID_ARGUMENT, "scan_variant is 0..9");
+  if (chunk_tiles != 0 && (chunk_tiles < 16 || chunk_tiles > 65535))
+    return Fail(SMX_INVALID_ARGUMENT, "chunk_tiles must be 0 (default) or in [16, 65535]");
   if (candidates_per_query < 32 || candidates_per_query > 16384)
     return Fail(SMX_INVALID_ARGUMENT, "candidates_per_query must be in [32, 16384]");
   if (seed_leaves < 0) return Fail(SMX_INVALID_ARGUMENT, "seed_leaves must be >= 0");
   std::lock_guard<std::mutex> lock(h->mu);
   h->cap_per_query = uint32_t(candidates_per_query);
   h->seed_leaves = seed_leaves;
+  h->scan_variant = scan_variant;
+  if (chunk_tiles) h->chunk_tiles[scan_variant] = uint32_t(chunk_tiles);
   return SMX_OK;
 }
 

@@ -22,8 +22,10 @@ def main():
     qd = torch.from_numpy(q).cuda()
     oi = torch.zeros((NQ, FINAL_NN), dtype=torch.int32, device="cuda")
     od = torch.zeros((NQ, FINAL_NN), dtype=torch.float32, device="cuda")
-    for cap, seed in [(4096, 2), (4096, 3), (4096, 4)]:
-        nat.set_tuning(cap, seed)
+    grid = [tuple(int(x) for x in g.split(",")) for g in sys.argv[1:]] or [
+        (4096, 2, 0, 32), (4096, 2, 2, 32), (4096, 2, 3, 32), (4096, 2, 2, 16), (4096, 2, 3, 64)]
+    for cap, seed, variant, chunk in grid:
+        nat.set_tuning(cap, seed, variant, chunk)
         acc = {}
         steps = 10
         for i in range(steps + 2):
@@ -34,7 +36,7 @@ def main():
                 for k, v in t.items():
                     acc[k] = acc.get(k, 0.0) + float(v) / steps
         mfma_tops = acc["scan_item_tiles"] * 25 * 65536 / (acc["scan_ms"] * 1e-3) / 1e12
-        print(f"cap={cap:5d} seed={seed:2d} total={acc['total_ms']:.3f} part={acc['partition_ms']:.3f} "
+        print(f"var={variant} chunk={chunk:3d} cap={cap:5d} seed={seed:2d} total={acc['total_ms']:.3f} part={acc['partition_ms']:.3f} "
               f"lut={acc['lut_ms']:.3f} inv={acc['invert_ms']:.3f} seed={acc['seed_scan_ms']:.3f} "
               f"scan={acc['scan_ms']:.3f} sel={acc['select_ms']:.3f} retries={acc['overflow_retries']:.1f} "
               f"cand_mean={acc['mean_candidates']:.0f} cand_max={acc['max_candidates']:.0f} "
