@@ -106,7 +106,9 @@ struct SelectArgs {
   float* out_dist;
   int32_t* out_count;
   int out_width;
-  uint32_t* overflow;         // [2]: flag, max count
+  uint32_t* overflow;         // stats: [0] flag [1] max overflow [2] max count [8] sum [9] fallbacks
+  uint32_t* fallback;         // [nq] queries the wave kernel hands to the block kernel (or NULL)
+  const uint32_t* qlist;      // block kernel over these queries only (or NULL: all)
 };
 
 // ---- launchers (smx_kernels.hip) ------------------------------------------
@@ -124,14 +126,17 @@ hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf,
                        uint2* work /*[max items]*/, uint32_t* totals /*[3]*/,
                        unsigned long long* code_bytes /*[1]*/, uint32_t chunk_tiles,
                        uint32_t queries_per_item /*32 or 64*/, hipStream_t s);
-// variant 0: block-level items of 32 queries, LUT rows in LDS (default);
-// 1: wave-level items with the LUT rows in VGPRs; 2: block items of 64
-// queries (one one-hot A fragment feeds two MFMAs), 4 waves; 3: as 2 with 8.
+// variant 0 (default): block items of 32 queries, LUT rows in LDS, hit
+// lists drained once per item; 1: wave-level items with the LUT rows in
+// VGPRs; 2: block items with per-lane survivor slots; 4: variant 0 without
+// its threshold epilogue (timing ablation, results invalid).
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,
                       hipStream_t s);
 hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s);
 hipError_t LaunchTighten(const uint64_t* cand, const uint32_t* cand_count, uint32_t cap,
                          int nq, int kk, uint64_t* tau_key, hipStream_t s);
+// One wave per query when a.fallback is set and the buffers fit; the block
+// kernel otherwise, or over a.qlist (the wave kernel's fallback queries).
 hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s);
 hipError_t LaunchExactDistances(const DeviceIndex& ix, const float* queries, int nq,
                                 const uint32_t* ids, int k, float* out, hipStream_t s);

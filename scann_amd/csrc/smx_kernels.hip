@@ -1076,6 +1076,193 @@ __global__ void __launch_bounds__(64 * NWV, ((ABL & 8) ? 3 : BlockOccupancy(K, Q
   }
 }
 
+// ---------------------------------------------------------------------------
+// Default scan (variant 0): block items as above, but the threshold epilogue
+// is split in two.  In the tile loop a lane whose tile minimum passes only
+// appends its 16 sums (packed int16) and a tag to its wave's LDS hit list
+// (~20 instructions for the whole wave, once per tile with a hit); the
+// per-element test, the key and the exact threshold compare run in drain(),
+// lane-parallel over hits, once per item (or when the list fills).
+// ---------------------------------------------------------------------------
+constexpr int kHitsPerWave = 64;   // >= 64: a tile may add a hit per lane right after a drain
+constexpr int kQStageHits = 16;
+
+template <int K, int ABL = 0>
+__global__ void __launch_bounds__(256, (K <= 25 ? 4 : 3)) lut16_scan_hits_kernel(ScanArgs a) {
+  constexpr int NW = ((((K + 1) / 2) + 3) / 4);
+  constexpr int W = 4 * NW;
+  constexpr int Q = 32, NWV = 4, NT = 256, HW = kHitsPerWave, S = kQStageHits;
+  __shared__ v4i lut_s[2 * K * Q];
+  __shared__ uint4 hsum[NWV][HW][2];     // 16 sums as int16 pairs
+  __shared__ uint32_t hmeta[NWV][HW];    // tile << 6 | lane
+  __shared__ uint64_t qstage[Q * S];
+  __shared__ uint32_t qcnt[Q], q_slot[Q], q_id[Q];
+  __shared__ float q_bias[Q], q_inv[Q];
+  __shared__ int q_amax[Q];
+  __shared__ uint64_t q_T[Q];
+  __shared__ uint32_t s_w;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int c = lane & 31;
+  const int h = lane >> 5;
+  const uint32_t total = a.tile_prefix[a.nl];
+  const int smin = -128 * a.nb, smax = 128 * a.nb;
+  for (;;) {
+    if (tid == 0) s_w = atomicAdd(a.work_counter, 1u);
+    if (tid < Q) qcnt[tid] = 0;
+    __syncthreads();
+    const uint32_t w = s_w;
+    if (w >= total) break;
+    const uint2 item = a.work[w];
+    const int leaf = int(item.x);
+    const uint32_t t = item.y >> 16;
+    const uint32_t chunk = item.y & 0xFFFFu;
+    const uint32_t pbeg = a.pair_off[leaf] + t * uint32_t(Q);
+    const int nvalid = int(min(uint32_t(Q), a.pair_off[leaf] + a.leaf_count[leaf] - pbeg));
+    if (tid < Q) {
+      const bool v = tid < nvalid;
+      const uint32_t pidx = pbeg + uint32_t(v ? tid : 0);
+      const uint32_t qid = a.pair_q[pidx];
+      const float bias = a.residual ? a.pair_bias[pidx] : 0.0f;
+      const float inv = a.inv[qid];
+      const uint64_t T = a.tau_key[qid];
+      q_id[tid] = qid;
+      q_bias[tid] = bias;
+      q_inv[tid] = inv;
+      q_T[tid] = T;
+      q_amax[tid] = !v ? smin - 1
+                  : (T == kNoThreshold) ? smax
+                  : SumLimit(FromOrdered(uint32_t(T >> 32)), inv, bias, smin, smax);
+    }
+    for (int e = tid; e < K * Q; e += NT) {
+      const int qs = e % Q, rp = e / Q;   // rows 2rp, 2rp+1 of query slot qs
+      const uint32_t pidx = pbeg + uint32_t(qs < nvalid ? qs : 0);
+      const v4i* src = reinterpret_cast<const v4i*>(a.lut) + size_t(a.pair_q[pidx]) * 2 * K + 2 * rp;
+      const v4i r0 = src[0], r1 = src[1];
+      lut_s[(2 * rp) * Q + qs] = r0;
+      lut_s[(2 * rp + 1) * Q + qs] = r1;
+    }
+    __syncthreads();
+    const int amax = q_amax[c];
+    const uint32_t n = a.leaf_size[leaf];
+    const uint32_t ntile_leaf = (n + kDpPerTile - 1) / kDpPerTile;
+    const uint32_t j0 = chunk * a.chunk_tiles;
+    const uint32_t jend = min(ntile_leaf, j0 + a.chunk_tiles);
+    const uint8_t* tb = a.tiles + a.tile_off[leaf] * 64ull * W + size_t(lane) * W;
+    const uint64_t moff = a.member_off[leaf];
+    uint32_t whits = 0;   // wave-uniform
+
+    // lane k of the wave takes hit k: per-element test, key, exact
+    // threshold compare, append to the query's LDS stage
+    auto drain = [&]() {
+      if (uint32_t(lane) < whits) {
+        const uint32_t meta = hmeta[wave][lane];
+        const uint32_t jj = meta >> 6;
+        const int cc = int(meta & 31u), hh = int((meta >> 5) & 1u);
+        const uint4 s0 = hsum[wave][lane][0], s1 = hsum[wave][lane][1];
+        const uint32_t sw[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const int am = q_amax[cc];
+        const float iv = q_inv[cc], bs = q_bias[cc];
+        const uint64_t TT = q_T[cc];
+        const uint32_t qq = q_id[cc];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int sum = int(int16_t(uint16_t(sw[i >> 1] >> (16 * (i & 1)))));
+          if (sum <= am) {
+            const uint32_t dp = jj * kDpPerTile + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            const float d = DistOf(sum, iv, bs);
+            const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp)
+                                             : a.members[moff + dp];
+            const uint64_t key = (uint64_t(OrderedBits(d)) << 32) | tie;
+            if (key <= TT) {
+              const uint32_t p = atomicAdd(&qcnt[cc], 1u);
+              if (p < uint32_t(S)) {
+                qstage[cc * S + p] = key;
+              } else {  // stage full: straight to the global list
+                const uint32_t gs = atomicAdd(&a.cand_count[qq], 1u);
+                if (gs < a.cap) a.cand[size_t(qq) * a.cap + gs] = key;
+              }
+            }
+          }
+        }
+      }
+    };
+
+    auto body = [&](const uint32_t (&codes)[NW], uint32_t j) {
+      v16i acc[1];
+      TileMfma<K, Q, 1, 1, false>(codes, lut_s, h * Q + c, acc);
+      if (ABL & 4) {
+        int x = acc[0][0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) x ^= acc[0][i];
+        if (x == 0x7fffffff) a.cand_count[0] = x;
+        return;
+      }
+      const uint32_t rows_left = n - j * kDpPerTile;
+      if (rows_left < uint32_t(kDpPerTile)) {  // last tile of the leaf
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t row = (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (row >= rows_left) acc[0][i] = 0x7FFF;
+        }
+      }
+      int m = min(min(acc[0][0], acc[0][1]), acc[0][2]);
+#pragma unroll
+      for (int i = 3; i < 15; i += 2) m = min(min(m, acc[0][i]), acc[0][i + 1]);
+      m = min(m, acc[0][15]);
+      const bool hit = m <= amax;
+      const uint64_t hb = __builtin_amdgcn_ballot_w64(hit);
+      if (hb) {
+        const uint32_t nh = uint32_t(__popcll(hb));
+        if (whits + nh > uint32_t(HW)) {
+          drain();
+          whits = 0;
+        }
+        if (hit) {
+          const uint32_t slot =
+              whits + __builtin_amdgcn_mbcnt_hi(uint32_t(hb >> 32),
+                                                __builtin_amdgcn_mbcnt_lo(uint32_t(hb), 0u));
+          uint32_t pk[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            pk[k] = (uint32_t(acc[0][2 * k]) & 0xFFFFu) | (uint32_t(acc[0][2 * k + 1]) << 16);
+          hsum[wave][slot][0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+          hsum[wave][slot][1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+          hmeta[wave][slot] = (j << 6) | uint32_t(lane);
+        }
+        whits += nh;
+      }
+    };
+
+    uint32_t codes[NW], next[NW];
+    uint32_t j = j0 + wave;
+    if (j < jend) LoadCodes<K>(tb + size_t(j) * 64 * W, codes);
+    for (; j < jend; j += NWV) {
+      if (j + NWV < jend) LoadCodes<K>(tb + size_t(j + NWV) * 64 * W, next);
+      body(codes, j);
+#pragma unroll
+      for (int i = 0; i < NW; ++i) codes[i] = next[i];
+    }
+    drain();
+    __syncthreads();
+    // one global atomic per query slot with survivors, then the copy
+    if (tid < Q) {
+      const uint32_t m = min(qcnt[tid], uint32_t(S));
+      q_slot[tid] = m ? atomicAdd(&a.cand_count[q_id[tid]], m) : 0u;
+    }
+    __syncthreads();
+    for (int e = tid; e < Q * S; e += NT) {
+      const int qs = e / S, u = e - qs * S;
+      if (uint32_t(u) < min(qcnt[qs], uint32_t(S))) {
+        const uint32_t slot = q_slot[qs] + u;
+        if (slot < a.cap) a.cand[size_t(q_id[qs]) * a.cap + slot] = qstage[e];
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // One-query variant for the stage entry point: raw sums of one leaf.
 template <int K>
 __global__ void __launch_bounds__(64) leaf_scores_kernel(const uint8_t* __restrict__ tiles,
@@ -1165,16 +1352,9 @@ __device__ float ExactDistance(const float* __restrict__ q, const float* __restr
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) final_select_kernel(SelectArgs a) {
   extern __shared__ uint64_t lds[];
-  const int qi = blockIdx.x;
+  const int qi = a.qlist ? int(a.qlist[blockIdx.x]) : int(blockIdx.x);
   const uint32_t raw_n = a.cand_count[qi];
-  if (raw_n > a.cap && threadIdx.x == 0) {
-    atomicOr(&a.overflow[0], 1u);
-    atomicMax(&a.overflow[1], raw_n);
-  }
-  if (threadIdx.x == 0) {
-    atomicMax(&a.overflow[2], raw_n);
-    atomicAdd(&a.overflow[8], raw_n);   // survivors summed over queries
-  }
+
   const uint32_t n = min(raw_n, a.cap);
   // LDS: keys[kcap] | sel[selcap] | aux[kkp2] | q[dim] | gid[kk] | dist[kk] | hist | scan
   const uint32_t kcap = NextPow2(a.cap);
@@ -1272,6 +1452,256 @@ __global__ void __launch_bounds__(256) final_select_kernel(SelectArgs a) {
   if (threadIdx.x == 0 && a.out_count) a.out_count[qi] = int32_t(keep);
 }
 
+// ---------------------------------------------------------------------------
+// Final selection, default path: one 256-thread block per query and at most
+// kSelMax keys ever held in LDS.  A linear histogram of the distance word
+// (refined up to 6 times, straight from the global candidate list) bounds the
+// k'-th key; the <= kSelMax keys under that bound are ordered by a counting
+// rank (keys are unique, so each thread's rank is its slot; one barrier
+// instead of a bitonic network).  Then tie -> global id, SOAR
+// de-duplication, the exact reorder with 8 lanes per candidate (the A.8
+// order of ExactDistance) and the final (distance, id) rank.  Queries whose
+// boundary distance value alone holds more than kSelMax keys are appended to
+// a.fallback and re-run by final_select_kernel.
+// ---------------------------------------------------------------------------
+constexpr int kSelMax = 256;
+constexpr int kFsBins = 256;
+
+// Inclusive block scan of one value per thread (256 threads).
+__device__ __forceinline__ uint32_t BlockInclusiveScan256(uint32_t v, uint32_t* wsum) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = uint32_t(__shfl_up(int(v), off));
+    if (lane >= off) v += t;
+  }
+  if (lane == 63) wsum[wid] = v;
+  __syncthreads();
+  for (int w = 0; w < wid; ++w) v += wsum[w];
+  return v;
+}
+
+__global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
+  __shared__ uint64_t sel[kSelMax], out[kSelMax];
+  __shared__ uint32_t hist[kFsBins], wsum[4], gid[kSelMax];
+  __shared__ float dist[kSelMax];
+  __shared__ uint32_t s_lo[4], s_hi[4], s_b, s_cle, s_cbef, s_c;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int qi = blockIdx.x;
+  const uint32_t raw_n = a.cand_count[qi];
+  if (tid == 0) s_c = 0;
+  const uint32_t n = min(raw_n, a.cap);
+  const uint32_t k = uint32_t(a.kk);
+  const uint64_t* ck = a.cand + size_t(qi) * a.cap;
+  if (n <= uint32_t(kSelMax)) {
+    if (uint32_t(tid) < n) sel[tid] = ck[tid];
+    __syncthreads();
+  } else {
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+    for (uint32_t i = tid; i < n; i += 256) {
+      const uint32_t v = uint32_t(ck[i] >> 32);
+      lo = min(lo, v);
+      hi = max(hi, v);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      lo = min(lo, uint32_t(__shfl_xor(int(lo), off)));
+      hi = max(hi, uint32_t(__shfl_xor(int(hi), off)));
+    }
+    if (lane == 0) { s_lo[wid] = lo; s_hi[wid] = hi; }
+    __syncthreads();
+    lo = min(min(s_lo[0], s_lo[1]), min(s_lo[2], s_lo[3]));
+    hi = max(max(s_hi[0], s_hi[1]), max(s_hi[2], s_hi[3]));
+    uint32_t below = 0, lim = 0;
+    bool ok = false;
+    for (int it = 0; it < 6; ++it) {
+      const uint64_t span = uint64_t(hi - lo) + 1;
+      hist[tid] = 0;
+      __syncthreads();
+      for (uint32_t i = tid; i < n; i += 256) {
+        const uint32_t v = uint32_t(ck[i] >> 32);
+        if (v >= lo && v <= hi) atomicAdd(&hist[uint32_t((uint64_t(v - lo) * kFsBins) / span)], 1u);
+      }
+      __syncthreads();
+      const uint32_t hv = hist[tid];
+      const uint32_t inc = BlockInclusiveScan256(hv, wsum);
+      if (below + inc - hv < k && below + inc >= k) {
+        s_b = uint32_t(tid);
+        s_cle = below + inc;
+        s_cbef = below + inc - hv;
+      }
+      __syncthreads();
+      const uint32_t b = s_b, cle = s_cle, cbef = s_cbef;
+      // values of bin b: [lo + ceil(b*span/256), lo + ceil((b+1)*span/256) - 1]
+      const uint32_t blo = lo + uint32_t((uint64_t(b) * span + kFsBins - 1) / kFsBins);
+      const uint32_t bhi = lo + uint32_t((uint64_t(b + 1) * span + kFsBins - 1) / kFsBins) - 1;
+      __syncthreads();   // s_b/wsum are rewritten by the next round
+      if (cle <= uint32_t(kSelMax)) {
+        lim = bhi;
+        ok = true;
+        break;
+      }
+      if (bhi == blo) break;   // one distance value holds too many keys
+      below = cbef;
+      lo = blo;
+      hi = bhi;
+    }
+    if (!ok) {   // block-uniform
+      if (tid == 0) a.fallback[atomicAdd(&a.overflow[9], 1u)] = uint32_t(qi);
+      return;
+    }
+    for (uint32_t i = tid; i < n; i += 256) {
+      const uint64_t key = ck[i];
+      if (uint32_t(key >> 32) <= lim) sel[atomicAdd(&s_c, 1u)] = key;
+    }
+    __syncthreads();
+  }
+  const uint32_t c = n <= uint32_t(kSelMax) ? n : s_c;
+  // counting rank: keys are unique, so rank = number of smaller keys
+  if (uint32_t(tid) < c) {
+    const uint64_t key = sel[tid];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < c; ++j) r += sel[j] < key ? 1u : 0u;
+    out[r] = key;
+  }
+  __syncthreads();
+  uint32_t m = min(c, k);
+  if (uint32_t(tid) < m) {
+    const uint64_t key = out[tid];
+    uint32_t tie = uint32_t(key & 0xFFFFFFFFu);
+    if (a.shift > 0) {
+      const uint32_t leaf = tie >> a.shift;
+      tie = a.members[a.member_off[leaf] + (tie & ((1u << a.shift) - 1u))];
+    }
+    gid[tid] = tie;
+    dist[tid] = FromOrdered(uint32_t(key >> 32));
+  }
+  __syncthreads();
+  if (!a.disjoint) {
+    // group duplicate ids: rank (gid << 32 | slot); run starts keep the
+    // averaged distance 0.5a + 0.5b (two copies at most), the rest drop out
+    if (uint32_t(tid) < m) {
+      const uint64_t key = (uint64_t(gid[tid]) << 32) | uint32_t(tid);
+      uint32_t r = 0;
+      for (uint32_t j = 0; j < m; ++j) r += ((uint64_t(gid[j]) << 32) | j) < key ? 1u : 0u;
+      sel[r] = key;
+    }
+    __syncthreads();
+    uint64_t o = ~0ull;
+    if (uint32_t(tid) < m) {
+      const uint32_t g = uint32_t(sel[tid] >> 32);
+      if (tid == 0 || uint32_t(sel[tid - 1] >> 32) != g) {
+        float d = dist[uint32_t(sel[tid] & 0xFFFFFFFFu)];
+        if (uint32_t(tid) + 1 < m && uint32_t(sel[tid + 1] >> 32) == g) {
+          const float d2 = dist[uint32_t(sel[tid + 1] & 0xFFFFFFFFu)];
+          d = __fadd_rn(__fmul_rn(0.5f, d), __fmul_rn(0.5f, d2));
+        }
+        o = (uint64_t(OrderedBits(d)) << 32) | g;
+      }
+    }
+    out[tid] = o;
+    if (tid == 0) s_c = 0;
+    __syncthreads();
+    if (o != ~0ull) {
+      uint32_t r = 0;
+      for (uint32_t j = 0; j < m; ++j) r += out[j] < o ? 1u : 0u;
+      atomicAdd(&s_c, 1u);
+      if (r < uint32_t(a.pre_nn)) {
+        gid[r] = uint32_t(o & 0xFFFFFFFFu);
+        dist[r] = FromOrdered(uint32_t(o >> 32));
+      }
+    }
+    __syncthreads();
+    m = min(s_c, uint32_t(a.pre_nn));
+  }
+  if (a.reorder && !a.pre_only) {
+    // 8 lanes per candidate: lane l of a group owns accumulator l of the A.8
+    // layout (dims l, l+8, ...); the folds follow ExactDistance exactly
+    const int l = tid & 7, gb = lane & ~7;
+    const float* q = a.queries + size_t(qi) * a.dim;
+    const int dim = a.dim, j8 = dim & ~7;
+    const bool l2 = a.metric != 0;
+    auto term = [l2](float acc, float x, float y) {
+      if (!l2) return __fmaf_rn(-x, y, acc);
+      const float t = __fsub_rn(x, y);
+      return __fmaf_rn(t, t, acc);
+    };
+    for (uint32_t base = 0; base < m; base += 32) {
+      const uint32_t i = base + uint32_t(tid >> 3);
+      const bool act = i < m;
+      const float* x = a.dataset + size_t(gid[act ? i : 0]) * dim;
+      float acc = 0.0f;
+      for (int j = 0; j < j8; j += 8) acc = term(acc, q[j + l], x[j + l]);
+      const float hi4 = __shfl(acc, gb + ((l + 4) & 7));
+      float sv = __fadd_rn(hi4, acc);   // lanes l < 4: s[l]
+      int j = j8;
+      if (j + 4 <= dim) {
+        if (l < 4) sv = term(sv, q[j + l], x[j + l]);
+        j += 4;
+      }
+      if (j + 2 <= dim) {
+        if (l == 2 || l == 3) sv = term(sv, q[j + l - 2], x[j + l - 2]);
+        j += 2;
+      }
+      const float s1 = __shfl(sv, gb + 1), s2 = __shfl(sv, gb + 2), s3 = __shfl(sv, gb + 3);
+      float r = __fadd_rn(__fadd_rn(sv, s2), __fadd_rn(s1, s3));
+      if (j < dim) r = term(r, q[j], x[j]);
+      __syncthreads();   // all reads of gid/dist for this pass are done
+      if (l == 0 && act) dist[i] = r;
+    }
+    __syncthreads();
+  }
+  // final (distance, global id) rank; keep the output width
+  const uint32_t keep = min(m, uint32_t(a.out_width));
+  if (uint32_t(tid) < m) {
+    const uint64_t key = (uint64_t(OrderedBits(dist[tid])) << 32) | gid[tid];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < m; ++j) r += ((uint64_t(OrderedBits(dist[j])) << 32) | gid[j]) < key;
+    if (r < keep) {
+      a.out_idx[size_t(qi) * a.out_width + r] = uint32_t(key & 0xFFFFFFFFu);
+      a.out_dist[size_t(qi) * a.out_width + r] = FromOrdered(uint32_t(key >> 32));
+    }
+  }
+  for (int i = int(keep) + tid; i < a.out_width; i += 256) {
+    a.out_idx[size_t(qi) * a.out_width + i] = 0u;
+    a.out_dist[size_t(qi) * a.out_width + i] = __int_as_float(0x7fc00000);
+  }
+  if (tid == 0 && a.out_count) a.out_count[qi] = int32_t(keep);
+}
+
+// Candidate-list statistics for the host loop (one block; no same-address
+// atomics from every query's block): [0] any list over capacity, [1] the
+// largest such count, [2] the largest count, [8] the sum of counts.
+__global__ void __launch_bounds__(1024) cand_stats_kernel(const uint32_t* __restrict__ cand_count,
+                                                          int nq, uint32_t cap,
+                                                          uint32_t* __restrict__ stats) {
+  __shared__ uint32_t s_over[16], s_max[16], s_sum[16];
+  uint32_t over = 0, mx = 0, sum = 0;
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+    const uint32_t v = cand_count[i];
+    if (v > cap) over = max(over, v);
+    mx = max(mx, v);
+    sum += v;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    over = max(over, uint32_t(__shfl_xor(int(over), off)));
+    mx = max(mx, uint32_t(__shfl_xor(int(mx), off)));
+    sum += uint32_t(__shfl_xor(int(sum), off));
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { s_over[wid] = over; s_max[wid] = mx; s_sum[wid] = sum; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < int(blockDim.x >> 6); ++w) {
+      over = max(over, s_over[w]);
+      mx = max(mx, s_max[w]);
+      sum += s_sum[w];
+    }
+    stats[0] = over ? 1u : 0u;
+    stats[1] = over;
+    stats[2] = mx;
+    stats[8] = sum;
+  }
+}
+
 __global__ void exact_distances_kernel(const float* __restrict__ queries, const float* __restrict__ dataset,
                                        int dim, int metric, const uint32_t* __restrict__ ids,
                                        int k, float* __restrict__ out) {
@@ -1346,23 +1776,11 @@ hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf, const fl
 #define SMX_SCAN_CASE(KV)                                                          \
   case KV:                                                                         \
     if (variant == 0)                                                              \
-      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 1, 4>), dim3(grid), dim3(256), 0, s, a); \
+      hipLaunchKernelGGL((lut16_scan_hits_kernel<KV, 0>), dim3(grid), dim3(256), 0, s, a); \
     else if (variant == 2)                                                         \
-      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 2, 4>), dim3(grid), dim3(256), 0, s, a); \
-    else if (variant == 3)                                                         \
-      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 2, 8>), dim3(grid / 2), dim3(512), 0, s, a); \
+      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 1, 4, 0>), dim3(grid), dim3(256), 0, s, a); \
     else if (variant == 4)                                                         \
-      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 1, 4, 4>), dim3(grid), dim3(256), 0, s, a); \
-    else if (variant == 5)                                                         \
-      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 1, 4, 8>), dim3(grid), dim3(256), 0, s, a); \
-    else if (variant == 7)                                                         \
-      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 1, 4, 12>), dim3(grid), dim3(256), 0, s, a); \
-    else if (variant == 8)                                                         \
-      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 1, 4, 16>), dim3(grid), dim3(256), 0, s, a); \
-    else if (variant == 9)                                                         \
-      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 1, 4, 32>), dim3(grid), dim3(256), 0, s, a); \
-    else if (variant == 6)                                                         \
-      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 1, 4, 6>), dim3(grid), dim3(256), 0, s, a); \
+      hipLaunchKernelGGL((lut16_scan_hits_kernel<KV, 4>), dim3(grid), dim3(256), 0, s, a); \
     else                                                                           \
       hipLaunchKernelGGL(lut16_scan_kernel<KV>, dim3(grid), dim3(256), 0, s, a);   \
     break;
@@ -1455,10 +1873,17 @@ hipError_t LaunchTighten(const uint64_t* cand, const uint32_t* cand_count, uint3
 
 hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s) {
   if (nq == 0) return hipSuccess;
-  uint32_t kcap = 1;
-  while (kcap < a.cap) kcap <<= 1;
+  if (!a.qlist)
+    hipLaunchKernelGGL(cand_stats_kernel, dim3(1), dim3(1024), 0, s, a.cand_count, nq, a.cap,
+                       a.overflow);
   uint32_t kkp2 = 1;
   while (kkp2 < uint32_t(a.kk)) kkp2 <<= 1;
+  if (!a.qlist && a.fallback && a.kk <= kSelMax) {
+    hipLaunchKernelGGL(final_select_rank_kernel, dim3(nq), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
+  uint32_t kcap = 1;
+  while (kcap < a.cap) kcap <<= 1;
   const uint32_t selcap = std::max<uint32_t>(2048u, 2 * kkp2);
   const size_t lds = size_t(kcap) * 8 + size_t(selcap) * 8 + size_t(kkp2) * 8 +
                      size_t(a.dim) * 4 + size_t(a.kk) * 8 + (kSelBins + 256) * 4;

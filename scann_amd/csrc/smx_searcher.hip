@@ -92,6 +92,7 @@ struct Workspace {
   uint64_t* tau = nullptr;          // [nq]
   uint64_t* cand = nullptr;         // [nq][cap]
   uint32_t* cand_count = nullptr;   // [nq]
+  uint32_t* fallback = nullptr;     // [nq] queries the wave final select hands back
   uint32_t* out_idx = nullptr;
   float* out_dist = nullptr;
   int32_t* out_count = nullptr;
@@ -100,7 +101,8 @@ struct Workspace {
     DFree(queries); DFree(topl_leaf); DFree(topl_dist); DFree(scores); DFree(lut); DFree(mult);
     DFree(inv);
     DFree(counters); DFree(block_cnt); DFree(pair_off); DFree(tile_prefix); DFree(pair_q); DFree(pair_bias);
-    DFree(work); DFree(tau); DFree(cand); DFree(cand_count); DFree(out_idx); DFree(out_dist);
+    DFree(work); DFree(tau); DFree(cand); DFree(cand_count); DFree(fallback); DFree(out_idx);
+    DFree(out_dist);
     DFree(out_count);
     nq = L = kk = dim = width = 0;
     cap = max_items = 0;
@@ -118,7 +120,7 @@ struct smx_index {
   uint32_t cap_per_query = 4096;   // candidate list capacity
   int seed_leaves = 2;
   int scan_variant = 0;            // see smx::LaunchScan
-  uint32_t chunk_tiles[10] = {32, 32, 32, 32, 32, 32, 32, 32, 32, 32};
+  uint32_t chunk_tiles[5] = {32, 32, 32, 32, 32};
   int grid = 0;                    // wave-variant scan grid (blocks of 4 waves)
   int grid_block = 0;              // block-variant scan grid
   bool profiling = false;
@@ -292,6 +294,7 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
       (rc = DAlloc(&w.pair_q, pairs)) || (rc = DAlloc(&w.pair_bias, pairs)) ||
       (rc = DAlloc(&w.work, max_items)) || (rc = DAlloc(&w.tau, nq)) ||
       (rc = DAlloc(&w.cand, size_t(nq) * cap)) || (rc = DAlloc(&w.cand_count, nq)) ||
+      (rc = DAlloc(&w.fallback, nq)) ||
       (rc = DAlloc(&w.out_idx, size_t(nq) * width)) ||
       (rc = DAlloc(&w.out_dist, size_t(nq) * width)) || (rc = DAlloc(&w.out_count, nq))) {
     w.Release();
@@ -350,12 +353,12 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   Mark(h, 1, s);
   SMX_HIP(smx::LaunchLutBuild(ix, queries, nq, w.lut, w.mult, w.inv, nullptr, s));
   Mark(h, 2, s);
-  // the block scan stages 16-bit local datapoint numbers: larger leaves use
-  // the wave scan
-  const int variant = ix.max_leaf > 65535u ? 1 : h->scan_variant;
+  // the per-lane-slot block scan stages 16-bit local datapoint numbers:
+  // larger leaves use the default scan
+  const int variant = (ix.max_leaf > 65535u && h->scan_variant == 2) ? 0 : h->scan_variant;
   SMX_HIP(smx::LaunchPairs(ix, w.topl_leaf, w.topl_dist, nq, L, cnt, w.block_cnt, w.pair_off,
                            w.tile_prefix, w.pair_q, w.pair_bias, w.work, stats + 3, code_bytes,
-                           h->chunk_tiles[variant], (variant == 2 || variant == 3) ? 64u : 32u,
+                           h->chunk_tiles[variant], 32u,
                            s));
   Mark(h, 3, s);
   smx::SeedArgs sa{};
@@ -422,6 +425,8 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sel.out_count = out_count;
   sel.out_width = width;
   sel.overflow = stats;
+  sel.fallback = w.fallback;
+  sel.qlist = nullptr;
 
   int retries = 0;
   uint32_t st[10] = {0};
@@ -432,12 +437,20 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     Mark(h, 7, s);
     SMX_HIP(hipMemcpyAsync(st, stats, sizeof(st), hipMemcpyDeviceToHost, s));
     SMX_HIP(hipStreamSynchronize(s));
-    if (!st[0]) break;
+    if (!st[0]) {
+      if (st[9]) {  // queries the wave final select could not narrow
+        smx::SelectArgs fb = sel;
+        fb.qlist = w.fallback;
+        SMX_HIP(smx::LaunchFinalSelect(fb, int(st[9]), s));
+        SMX_HIP(hipStreamSynchronize(s));
+      }
+      break;
+    }
     if (++retries > 64) return Fail(SMX_INTERNAL, "candidate tightening did not converge");
     SMX_HIP(smx::LaunchTighten(w.cand, w.cand_count, w.cap, nq, kk, w.tau, s));
     SMX_HIP(hipMemsetAsync(w.cand_count, 0, sizeof(uint32_t) * nq, s));
     SMX_HIP(hipMemsetAsync(stats, 0, sizeof(uint32_t) * 3, s));
-    SMX_HIP(hipMemsetAsync(stats + 8, 0, sizeof(uint32_t), s));
+    SMX_HIP(hipMemsetAsync(stats + 8, 0, 2 * sizeof(uint32_t), s));
     SMX_HIP(hipMemsetAsync(work, 0, sizeof(uint32_t), s));
   }
   smx_timings& t = h->timings;
@@ -759,7 +772,8 @@ int smx_get_timings(const smx_index* h, smx_timings* out) {
 int smx_set_tuning(smx_index* h, int32_t candidates_per_query, int32_t seed_leaves,
                    int32_t scan_variant, int32_t chunk_tiles) {
   if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
-  if (scan_variant < 0 || scan_variant > 9) return Fail(SMX_INVALID_ARGUMENT, "scan_variant is 0..9");
+  if (scan_variant < 0 || scan_variant > 4 || scan_variant == 3)
+    return Fail(SMX_INVALID_ARGUMENT, "scan_variant is 0, 1, 2 or 4");
   if (chunk_tiles != 0 && (chunk_tiles < 16 || chunk_tiles > 65535))
     return Fail(SMX_INVALID_ARGUMENT, "chunk_tiles must be 0 (default) or in [16, 65535]");
   if (candidates_per_query < 32 || candidates_per_query > 16384)
