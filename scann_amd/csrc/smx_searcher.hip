@@ -118,7 +118,7 @@ struct smx_index {
   std::mutex mu;
   Workspace ws;
   uint32_t cap_per_query = 4096;   // candidate list capacity
-  int seed_leaves = 2;
+  int seed_leaves = 4;
   int scan_variant = 0;            // see smx::LaunchScan
   uint32_t chunk_tiles[5] = {32, 32, 32, 32, 32};
   int grid = 0;                    // wave-variant scan grid (blocks of 4 waves)

@@ -5,12 +5,12 @@
 set -e
 CFG=${1:-4096,2,0,32}
 OUT=${2:-gpurun_out/pmc_scan}
-GROUPS=${3:-"SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE;SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU;SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS;SQ_INSTS_VMEM SQ_INST_CYCLES_VMEM SQ_WAVES SQ_BUSY_CYCLES"}
+PMCG=${3:-"SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE;SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU;SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS;SQ_INSTS_VMEM SQ_INST_CYCLES_VMEM SQ_WAVES SQ_BUSY_CYCLES"}
 ROOT=$(pwd)
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 i=0
-IFS=';' read -ra GRP <<< "$GROUPS"
+IFS=';' read -ra GRP <<< "$PMCG"
 for grp in "${GRP[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$ROOT/$OUT/p$i" -o run \

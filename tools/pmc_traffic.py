@@ -14,7 +14,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "lut16_scan_kernel"
+KERNEL = "lut16_scan_hits_kernel"
 
 
 def kernel_sha():
@@ -41,4 +41,4 @@ def main(path, out=os.path.join(ROOT, "profiles", "scan_traffic.json")):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(*sys.argv[1:3])
