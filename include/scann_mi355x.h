@@ -76,7 +76,29 @@ typedef struct smx_index_desc {
   const float* dataset;     /* [num_datapoints][dim] or NULL                  */
   float spilling_overretrieve_factor; /* tree_ah_hybrid_residual.h:320 (2.0) */
   int32_t reserved;
+  /* Range-split shard of a whole index: the shard holds
+   * rows [leaf_row_base[l], leaf_row_base[l] + size) of every full leaf l, so
+   * that tie keys stay the whole index's (leaf << shift | row).  Zero for a
+   * whole index (then nothing below is read). */
+  int32_t is_shard;
+  int32_t global_topn_shift;      /* the whole index's shift (smx_index_info)  */
+  int32_t global_spilled;         /* 1 if the whole index has SOAR duplicates  */
+  int32_t reserved2;
+  const uint32_t* leaf_row_base;  /* [num_leaves]                              */
+  const float* member_rows;       /* [members][dim] rows of this shard for the
+                                     exact reorder (global top-N indexes), or
+                                     NULL: `dataset` by global id              */
 } smx_index_desc;
+
+/* One entry of a shard's local top-k' list: key = ordered approximate
+ * distance << 32 | whole-index tie (UINT64_MAX pads an unused entry), the
+ * global datapoint id and the exact distance (the approximate one when the
+ * search does not reorder). */
+typedef struct smx_shard_entry {
+  uint64_t key;
+  uint32_t id;
+  float exact;
+} smx_shard_entry;
 
 typedef struct smx_index smx_index;
 
@@ -139,6 +161,30 @@ int smx_search_batched_device(smx_index* index, const float* d_queries, int32_t 
                               int32_t dim, const smx_search_params* params,
                               uint32_t* d_out_idx, float* d_out_dist,
                               int32_t* d_out_count, void* stream);
+
+/* ---- range-split shards -------------------------------
+ * Each rank searches its shard, producing its exact local top-k' by (approx
+ * distance, whole-index tie) with exact distances of its own rows; the
+ * ranks' lists are all-gathered (one collective, [world][nq][k'] entries) and
+ * merged.  The exact top-k' under a total order is shard-invariant, so the
+ * merged result equals the unsharded search. */
+
+/* k' (entries per query) of a shard search with these params. */
+int smx_shard_width(const smx_index* index, const smx_search_params* params, int32_t* out_k);
+
+/* This shard's local lists, device buffers on `stream`: d_entries [nq][k']. */
+int smx_search_shard_device(smx_index* index, const float* d_queries, int32_t nq, int32_t dim,
+                            const smx_search_params* params, smx_shard_entry* d_entries,
+                            void* stream);
+
+/* Merge of `world` shards' lists d_entries [world][nq][k'] (any shard's
+ * handle; it supplies the spill/dedupe setting): SOAR de-duplication by id,
+ * then the (distance, id) order of SortAndDropResults; outputs as
+ * smx_search_batched_device. */
+int smx_merge_shards_device(smx_index* index, int32_t world, int32_t nq,
+                            const smx_search_params* params, const smx_shard_entry* d_entries,
+                            uint32_t* d_out_idx, float* d_out_dist, int32_t* d_out_count,
+                            void* stream);
 
 /* ---- stage entry points (used by the parity tests; host buffers) ------- */
 

@@ -57,6 +57,9 @@ SIGNATURES = {
     "smx_set_profiling": (ctypes.c_int, [_vp, _i32]),
     "smx_get_timings": (ctypes.c_int, [_vp, ctypes.POINTER(Timings)]),
     "smx_set_tuning": (ctypes.c_int, [_vp, _i32, _i32, _i32, _i32]),
+    "smx_shard_width": (ctypes.c_int, [_vp, ctypes.POINTER(SearchParams), ctypes.POINTER(_i32)]),
+    "smx_search_shard_device": (ctypes.c_int, [_vp, _vp, _i32, _i32, ctypes.POINTER(SearchParams), _vp, _vp]),
+    "smx_merge_shards_device": (ctypes.c_int, [_vp, _i32, _i32, ctypes.POINTER(SearchParams), _vp, _vp, _vp, _vp, _vp]),
     "smx_last_error": (ctypes.c_char_p, []),
     "smx_version": (ctypes.c_char_p, []),
 }
@@ -148,6 +151,28 @@ class NativeIndex:
         check(self.lib.smx_search_batched_device(self.h, q_ptr, nq, self.dim, ctypes.byref(p),
                                                  out_idx_ptr, out_dist_ptr, out_count_ptr, stream),
               "Error during search")
+
+    # -- range-split shards; device pointers ----------------
+    SHARD_ENTRY_BYTES = 16   # smx_shard_entry {u64 key; u32 id; f32 exact}
+
+    def shard_width(self, leaves, pre_nn, final_nn, reorder=True) -> int:
+        p = SearchParams(int(leaves), int(pre_nn), int(final_nn), int(bool(reorder)))
+        k = _i32()
+        check(self.lib.smx_shard_width(self.h, ctypes.byref(p), ctypes.byref(k)), "smx_shard_width")
+        return k.value
+
+    def search_shard_device(self, q_ptr, nq, leaves, pre_nn, final_nn, reorder, entries_ptr,
+                            stream=None):
+        p = SearchParams(int(leaves), int(pre_nn), int(final_nn), int(bool(reorder)))
+        check(self.lib.smx_search_shard_device(self.h, q_ptr, nq, self.dim, ctypes.byref(p),
+                                               entries_ptr, stream), "Error during search")
+
+    def merge_shards_device(self, world, nq, leaves, pre_nn, final_nn, reorder, entries_ptr,
+                            out_idx_ptr, out_dist_ptr, out_count_ptr=None, stream=None):
+        p = SearchParams(int(leaves), int(pre_nn), int(final_nn), int(bool(reorder)))
+        check(self.lib.smx_merge_shards_device(self.h, int(world), int(nq), ctypes.byref(p),
+                                               entries_ptr, out_idx_ptr, out_dist_ptr,
+                                               out_count_ptr, stream), "smx_merge_shards")
 
     def search_pre_reorder(self, queries, leaves, pre_nn):
         q = _c(queries, np.float32)

@@ -42,6 +42,15 @@ struct DeviceIndex {
   uint32_t* members = nullptr;  // [num_members]
   uint32_t* leaf_order = nullptr; // [nl] leaves by descending size
   float* dataset = nullptr;     // [num_datapoints][dim] or null
+  uint32_t* row_base = nullptr; // [nl] shard's first row in each whole leaf, or null
+  float* member_rows = nullptr; // [num_members][dim] shard rows for the reorder, or null
+};
+
+// smx_shard_entry (include/scann_mi355x.h)
+struct ShardEntry {
+  uint64_t key;
+  uint32_t id;
+  float exact;
 };
 
 struct ScanArgs {
@@ -109,6 +118,23 @@ struct SelectArgs {
   uint32_t* overflow;         // stats: [0] flag [1] max overflow [2] max count [8] sum [9] fallbacks
   uint32_t* fallback;         // [nq] queries the wave kernel hands to the block kernel (or NULL)
   const uint32_t* qlist;      // block kernel over these queries only (or NULL: all)
+  ShardEntry* shard_out;      // shard mode: [nq][kk] local top-k' entries (or NULL)
+  const uint32_t* row_base;   // shard: whole-leaf row of each leaf's first shard row
+  const float* member_rows;   // shard: [members][dim] rows for the exact distances
+};
+
+struct MergeArgs {
+  const ShardEntry* entries;  // [world][nq][kk], each list sorted by key
+  int world;
+  int nq;
+  int kk;
+  int pre_nn;
+  int disjoint;
+  int reorder;
+  uint32_t* out_idx;
+  float* out_dist;
+  int32_t* out_count;
+  int out_width;
 };
 
 // ---- launchers (smx_kernels.hip) ------------------------------------------
@@ -138,6 +164,7 @@ hipError_t LaunchTighten(const uint64_t* cand, const uint32_t* cand_count, uint3
 // One wave per query when a.fallback is set and the buffers fit; the block
 // kernel otherwise, or over a.qlist (the wave kernel's fallback queries).
 hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s);
+hipError_t LaunchMergeShards(const MergeArgs& a, hipStream_t s);
 hipError_t LaunchExactDistances(const DeviceIndex& ix, const float* queries, int nq,
                                 const uint32_t* ids, int k, float* out, hipStream_t s);
 hipError_t LaunchLeafScores(const DeviceIndex& ix, int leaf, const int8_t* lut,

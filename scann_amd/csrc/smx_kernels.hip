@@ -1389,6 +1389,32 @@ __global__ void __launch_bounds__(256) final_select_kernel(SelectArgs a) {
     dist[i] = FromOrdered(uint32_t(k >> 32));
   }
   __syncthreads();
+  if (a.shard_out) {   // shard mode (rare fallback path): local top-k' entries
+    ShardEntry* so = a.shard_out + size_t(qi) * a.kk;
+    for (uint32_t i = threadIdx.x; i < uint32_t(a.kk); i += blockDim.x) {
+      ShardEntry e;
+      e.key = ~0ull;
+      e.id = 0u;
+      e.exact = 0.0f;
+      if (i < m) {
+        uint64_t key = keys[i];
+        const float* x = a.dataset ? a.dataset + size_t(gid[i]) * a.dim : nullptr;
+        if (a.shift > 0) {
+          const uint32_t tie = uint32_t(key & 0xFFFFFFFFu);
+          const uint32_t leaf = tie >> a.shift;
+          const uint32_t local = tie & ((1u << a.shift) - 1u);
+          if (a.member_rows) x = a.member_rows + (a.member_off[leaf] + local) * uint64_t(a.dim);
+          if (a.row_base)
+            key = (key & 0xFFFFFFFF00000000ull) | ((leaf << a.shift) | (local + a.row_base[leaf]));
+        }
+        e.key = key;
+        e.id = gid[i];
+        e.exact = a.reorder ? ExactDistance(q, x, a.dim, a.metric) : dist[i];
+      }
+      so[i] = e;
+    }
+    return;
+  }
   if (!a.disjoint) {
     // Group duplicates by id: sort (gid << 32 | rank).
     const uint32_t mp2 = NextPow2(m);
@@ -1480,9 +1506,51 @@ __device__ __forceinline__ uint32_t BlockInclusiveScan256(uint32_t v, uint32_t* 
   return v;
 }
 
+// Exact distances of m candidates (rows + rowid[i] * dim) into dist[], 8
+// lanes per candidate: lane l of a group owns accumulator l of the A.8 layout
+// (dims l, l+8, ...) and the folds follow ExactDistance exactly.  256
+// threads; ends with a barrier.
+__device__ void ExactDistances8(const SelectArgs& a, const float* rows, const uint32_t* rowid,
+                                uint32_t m, float* dist, int qi) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int l = tid & 7, gb = lane & ~7;
+  const float* q = a.queries + size_t(qi) * a.dim;
+  const int dim = a.dim, j8 = dim & ~7;
+  const bool l2 = a.metric != 0;
+  auto term = [l2](float acc, float x, float y) {
+    if (!l2) return __fmaf_rn(-x, y, acc);
+    const float t = __fsub_rn(x, y);
+    return __fmaf_rn(t, t, acc);
+  };
+  for (uint32_t base = 0; base < m; base += 32) {
+    const uint32_t i = base + uint32_t(tid >> 3);
+    const bool act = i < m;
+    const float* x = rows + size_t(rowid[act ? i : 0]) * dim;
+    float acc = 0.0f;
+    for (int j = 0; j < j8; j += 8) acc = term(acc, q[j + l], x[j + l]);
+    const float hi4 = __shfl(acc, gb + ((l + 4) & 7));
+    float sv = __fadd_rn(hi4, acc);   // lanes l < 4: s[l]
+    int j = j8;
+    if (j + 4 <= dim) {
+      if (l < 4) sv = term(sv, q[j + l], x[j + l]);
+      j += 4;
+    }
+    if (j + 2 <= dim) {
+      if (l == 2 || l == 3) sv = term(sv, q[j + l - 2], x[j + l - 2]);
+      j += 2;
+    }
+    const float s1 = __shfl(sv, gb + 1), s2 = __shfl(sv, gb + 2), s3 = __shfl(sv, gb + 3);
+    float r = __fadd_rn(__fadd_rn(sv, s2), __fadd_rn(s1, s3));
+    if (j < dim) r = term(r, q[j], x[j]);
+    __syncthreads();   // every read of rowid/dist for this pass is done
+    if (l == 0 && act) dist[i] = r;
+  }
+  __syncthreads();
+}
+
 __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
   __shared__ uint64_t sel[kSelMax], out[kSelMax];
-  __shared__ uint32_t hist[kFsBins], wsum[4], gid[kSelMax];
+  __shared__ uint32_t hist[kFsBins], wsum[4], gid[kSelMax], rowid[kSelMax];
   __shared__ float dist[kSelMax];
   __shared__ uint32_t s_lo[4], s_hi[4], s_b, s_cle, s_cbef, s_c;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1564,17 +1632,42 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
   }
   __syncthreads();
   uint32_t m = min(c, k);
+  // exact-reorder rows: dataset[global id], or in a shard with its own rows,
+  // member_rows[member slot]
+  const float* rows = a.member_rows ? a.member_rows : a.dataset;
   if (uint32_t(tid) < m) {
     const uint64_t key = out[tid];
     uint32_t tie = uint32_t(key & 0xFFFFFFFFu);
+    uint32_t rid = tie;
     if (a.shift > 0) {
       const uint32_t leaf = tie >> a.shift;
-      tie = a.members[a.member_off[leaf] + (tie & ((1u << a.shift) - 1u))];
+      const uint32_t local = tie & ((1u << a.shift) - 1u);
+      const uint64_t slot = a.member_off[leaf] + local;
+      tie = a.members[slot];
+      rid = a.member_rows ? uint32_t(slot) : tie;
+      if (a.shard_out && a.row_base)   // whole-index tie for the merge
+        out[tid] = (key & 0xFFFFFFFF00000000ull) |
+                   ((leaf << a.shift) | (local + a.row_base[leaf]));
     }
     gid[tid] = tie;
+    rowid[tid] = rid;
     dist[tid] = FromOrdered(uint32_t(key >> 32));
   }
   __syncthreads();
+  if (a.shard_out) {
+    // local top-k' with exact distances of this shard's rows; de-duplication
+    // and the final order happen in the merge
+    if (a.reorder) ExactDistances8(a, rows, rowid, m, dist, qi);
+    ShardEntry* so = a.shard_out + size_t(qi) * a.kk;
+    for (int i = tid; i < a.kk; i += 256) {
+      ShardEntry e;
+      e.key = uint32_t(i) < m ? out[i] : ~0ull;
+      e.id = uint32_t(i) < m ? gid[i] : 0u;
+      e.exact = uint32_t(i) < m ? dist[i] : 0.0f;
+      so[i] = e;
+    }
+    return;
+  }
   if (!a.disjoint) {
     // group duplicate ids: rank (gid << 32 | slot); run starts keep the
     // averaged distance 0.5a + 0.5b (two copies at most), the rest drop out
@@ -1595,6 +1688,7 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
           d = __fadd_rn(__fmul_rn(0.5f, d), __fmul_rn(0.5f, d2));
         }
         o = (uint64_t(OrderedBits(d)) << 32) | g;
+        hist[tid] = rowid[uint32_t(sel[tid] & 0xFFFFFFFFu)];   // the run's row
       }
     }
     out[tid] = o;
@@ -1607,48 +1701,13 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
       if (r < uint32_t(a.pre_nn)) {
         gid[r] = uint32_t(o & 0xFFFFFFFFu);
         dist[r] = FromOrdered(uint32_t(o >> 32));
+        rowid[r] = hist[tid];
       }
     }
     __syncthreads();
     m = min(s_c, uint32_t(a.pre_nn));
   }
-  if (a.reorder && !a.pre_only) {
-    // 8 lanes per candidate: lane l of a group owns accumulator l of the A.8
-    // layout (dims l, l+8, ...); the folds follow ExactDistance exactly
-    const int l = tid & 7, gb = lane & ~7;
-    const float* q = a.queries + size_t(qi) * a.dim;
-    const int dim = a.dim, j8 = dim & ~7;
-    const bool l2 = a.metric != 0;
-    auto term = [l2](float acc, float x, float y) {
-      if (!l2) return __fmaf_rn(-x, y, acc);
-      const float t = __fsub_rn(x, y);
-      return __fmaf_rn(t, t, acc);
-    };
-    for (uint32_t base = 0; base < m; base += 32) {
-      const uint32_t i = base + uint32_t(tid >> 3);
-      const bool act = i < m;
-      const float* x = a.dataset + size_t(gid[act ? i : 0]) * dim;
-      float acc = 0.0f;
-      for (int j = 0; j < j8; j += 8) acc = term(acc, q[j + l], x[j + l]);
-      const float hi4 = __shfl(acc, gb + ((l + 4) & 7));
-      float sv = __fadd_rn(hi4, acc);   // lanes l < 4: s[l]
-      int j = j8;
-      if (j + 4 <= dim) {
-        if (l < 4) sv = term(sv, q[j + l], x[j + l]);
-        j += 4;
-      }
-      if (j + 2 <= dim) {
-        if (l == 2 || l == 3) sv = term(sv, q[j + l - 2], x[j + l - 2]);
-        j += 2;
-      }
-      const float s1 = __shfl(sv, gb + 1), s2 = __shfl(sv, gb + 2), s3 = __shfl(sv, gb + 3);
-      float r = __fadd_rn(__fadd_rn(sv, s2), __fadd_rn(s1, s3));
-      if (j < dim) r = term(r, q[j], x[j]);
-      __syncthreads();   // all reads of gid/dist for this pass are done
-      if (l == 0 && act) dist[i] = r;
-    }
-    __syncthreads();
-  }
+  if (a.reorder && !a.pre_only) ExactDistances8(a, rows, rowid, m, dist, qi);
   // final (distance, global id) rank; keep the output width
   const uint32_t keep = min(m, uint32_t(a.out_width));
   if (uint32_t(tid) < m) {
@@ -1657,6 +1716,130 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
     for (uint32_t j = 0; j < m; ++j) r += ((uint64_t(OrderedBits(dist[j])) << 32) | gid[j]) < key;
     if (r < keep) {
       a.out_idx[size_t(qi) * a.out_width + r] = uint32_t(key & 0xFFFFFFFFu);
+      a.out_dist[size_t(qi) * a.out_width + r] = FromOrdered(uint32_t(key >> 32));
+    }
+  }
+  for (int i = int(keep) + tid; i < a.out_width; i += 256) {
+    a.out_idx[size_t(qi) * a.out_width + i] = 0u;
+    a.out_dist[size_t(qi) * a.out_width + i] = __int_as_float(0x7fc00000);
+  }
+  if (tid == 0 && a.out_count) a.out_count[qi] = int32_t(keep);
+}
+
+// ---------------------------------------------------------------------------
+// Merge of range-split shards.  Per query: the world lists
+// (each sorted by key, UINT64_MAX-padded) are loaded into LDS; an entry's
+// global rank is its position in its list plus, in every other list, the
+// number of smaller keys (binary search; keys are unique across shards since
+// ties are whole-index rows).  The kk smallest then go through the SOAR
+// de-duplication of final_select (averaged approximate distance of a
+// datapoint's two copies) and the final (distance, id) order, with the exact
+// distances the owning shards computed.
+// ---------------------------------------------------------------------------
+constexpr int kMergeMaxEntries = 2048;
+
+__global__ void __launch_bounds__(256) merge_shards_kernel(MergeArgs a) {
+  __shared__ uint64_t lk[kMergeMaxEntries];
+  __shared__ uint64_t sel[kSelMax], outk[kSelMax];
+  __shared__ uint32_t sid[kSelMax], gid[kSelMax];
+  __shared__ float sex[kSelMax], dist[kSelMax], ex[kSelMax];
+  __shared__ uint32_t cnt[64], s_c;
+  const int tid = threadIdx.x;
+  const int qi = blockIdx.x;
+  const int W = a.world, kk = a.kk;
+  auto entry = [&](int w, int j) -> const ShardEntry& {
+    return a.entries[(size_t(w) * a.nq + qi) * kk + j];
+  };
+  for (int e = tid; e < W * kk; e += 256) lk[e] = entry(e / kk, e % kk).key;
+  if (tid == 0) s_c = 0;
+  __syncthreads();
+  if (tid < W) {   // valid entries: the padding sorts last
+    int lo = 0, hi = kk;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (lk[tid * kk + mid] != ~0ull) lo = mid + 1; else hi = mid;
+    }
+    cnt[tid] = uint32_t(lo);
+  }
+  __syncthreads();
+  for (int e = tid; e < W * kk; e += 256) {
+    const int w = e / kk, j = e % kk;
+    if (uint32_t(j) >= cnt[w]) continue;
+    const uint64_t key = lk[e];
+    uint32_t r = uint32_t(j);
+    for (int v = 0; v < W && r < uint32_t(kk); ++v) {
+      if (v == w) continue;
+      int lo = 0, hi = int(cnt[v]);
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (lk[v * kk + mid] < key) lo = mid + 1; else hi = mid;
+      }
+      r += uint32_t(lo);
+    }
+    if (r < uint32_t(kk)) {
+      const ShardEntry& se = entry(w, j);
+      sel[r] = key;
+      sid[r] = se.id;
+      sex[r] = se.exact;
+    }
+  }
+  uint32_t total = 0;
+  for (int w = 0; w < W; ++w) total += cnt[w];
+  uint32_t m = min(total, uint32_t(kk));
+  __syncthreads();
+  if (uint32_t(tid) < m) {
+    gid[tid] = sid[tid];
+    dist[tid] = FromOrdered(uint32_t(sel[tid] >> 32));
+    ex[tid] = sex[tid];
+  }
+  __syncthreads();
+  if (!a.disjoint) {
+    if (uint32_t(tid) < m) {
+      const uint64_t key = (uint64_t(gid[tid]) << 32) | uint32_t(tid);
+      uint32_t r = 0;
+      for (uint32_t j = 0; j < m; ++j) r += ((uint64_t(gid[j]) << 32) | j) < key ? 1u : 0u;
+      sel[r] = key;
+    }
+    __syncthreads();
+    uint64_t o = ~0ull;
+    float oex = 0.0f;
+    if (uint32_t(tid) < m) {
+      const uint32_t g = uint32_t(sel[tid] >> 32);
+      if (tid == 0 || uint32_t(sel[tid - 1] >> 32) != g) {
+        const uint32_t s0 = uint32_t(sel[tid] & 0xFFFFFFFFu);
+        float d = dist[s0];
+        if (uint32_t(tid) + 1 < m && uint32_t(sel[tid + 1] >> 32) == g) {
+          const float d2 = dist[uint32_t(sel[tid + 1] & 0xFFFFFFFFu)];
+          d = __fadd_rn(__fmul_rn(0.5f, d), __fmul_rn(0.5f, d2));
+        }
+        o = (uint64_t(OrderedBits(d)) << 32) | g;
+        oex = ex[s0];
+      }
+    }
+    outk[tid] = o;
+    __syncthreads();
+    if (o != ~0ull) {
+      uint32_t r = 0;
+      for (uint32_t j = 0; j < m; ++j) r += outk[j] < o ? 1u : 0u;
+      atomicAdd(&s_c, 1u);
+      if (r < uint32_t(a.pre_nn)) {
+        gid[r] = uint32_t(o & 0xFFFFFFFFu);
+        dist[r] = FromOrdered(uint32_t(o >> 32));
+        ex[r] = oex;
+      }
+    }
+    __syncthreads();
+    m = min(s_c, uint32_t(a.pre_nn));
+  }
+  const uint32_t keep = min(m, uint32_t(a.out_width));
+  if (uint32_t(tid) < m) {
+    const float d = a.reorder ? ex[tid] : dist[tid];
+    const uint64_t key = (uint64_t(OrderedBits(d)) << 32) | gid[tid];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < m; ++j)
+      r += ((uint64_t(OrderedBits(a.reorder ? ex[j] : dist[j])) << 32) | gid[j]) < key;
+    if (r < keep) {
+      a.out_idx[size_t(qi) * a.out_width + r] = gid[tid];
       a.out_dist[size_t(qi) * a.out_width + r] = FromOrdered(uint32_t(key >> 32));
     }
   }
@@ -1871,6 +2054,14 @@ hipError_t LaunchTighten(const uint64_t* cand, const uint32_t* cand_count, uint3
   return hipGetLastError();
 }
 
+hipError_t LaunchMergeShards(const MergeArgs& a, hipStream_t s) {
+  if (a.nq == 0) return hipSuccess;
+  if (a.world < 1 || a.world > 64 || a.kk > kSelMax || a.world * a.kk > kMergeMaxEntries)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(merge_shards_kernel, dim3(a.nq), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s) {
   if (nq == 0) return hipSuccess;
   if (!a.qlist)
@@ -1878,7 +2069,7 @@ hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s) {
                        a.overflow);
   uint32_t kkp2 = 1;
   while (kkp2 < uint32_t(a.kk)) kkp2 <<= 1;
-  if (!a.qlist && a.fallback && a.kk <= kSelMax) {
+  if (!a.qlist && a.fallback && a.kk <= kSelMax) {   // (shard mode too)
     hipLaunchKernelGGL(final_select_rank_kernel, dim3(nq), dim3(256), 0, s, a);
     return hipGetLastError();
   }

@@ -171,6 +171,21 @@ int UploadIndex(const smx_index_desc* d, smx_index* h) {
     const int inner = 32 - Log2Ceil(uint32_t(nl));
     if (uint64_t(ix.max_leaf) <= (1ull << inner)) ix.shift = inner;
   }
+  if (d->is_shard) {
+    // a shard keeps the whole index's tie semantics and spill setting
+    if (d->global_topn_shift < 0 || d->global_topn_shift > 31)
+      return Fail(SMX_INVALID_ARGUMENT, "global_topn_shift out of range");
+    if (d->global_topn_shift > 0 && (!ix.residual || nl <= 1))
+      return Fail(SMX_INVALID_ARGUMENT, "global top-N shift needs a residual multi-leaf index");
+    ix.shift = d->global_topn_shift;
+    ix.disjoint = !d->global_spilled;
+    if (!d->leaf_row_base) return Fail(SMX_INVALID_ARGUMENT, "a shard needs leaf_row_base");
+    for (int l = 0; l < nl; ++l)
+      if (ix.shift > 0 && uint64_t(d->leaf_row_base[l]) + size[l] > (1ull << ix.shift))
+        return Fail(SMX_INVALID_ARGUMENT, "shard rows exceed the whole index's leaf range");
+    if (d->member_rows && ix.shift == 0)
+      return Fail(SMX_INVALID_ARGUMENT, "member_rows needs a global top-N (residual) index");
+  }
 
   // Code tiles: lane l = h*32 + r of tile j of a leaf holds, as nibbles
   // s = 0..K-1 (low nibble first), the codes of datapoint 32j + r for blocks
@@ -214,6 +229,15 @@ int UploadIndex(const smx_index_desc* d, smx_index* h) {
       (rc = DAlloc(&ix.members, M)) || (rc = DAlloc(&ix.leaf_order, nl)))
     return rc;
   if (d->dataset && (rc = DAlloc(&ix.dataset, size_t(d->num_datapoints) * dim))) return rc;
+  if (d->is_shard) {
+    if ((rc = DAlloc(&ix.row_base, nl))) return rc;
+    SMX_HIP(hipMemcpy(ix.row_base, d->leaf_row_base, 4 * nl, hipMemcpyHostToDevice));
+    if (d->member_rows && M) {
+      if ((rc = DAlloc(&ix.member_rows, size_t(M) * dim))) return rc;
+      SMX_HIP(hipMemcpy(ix.member_rows, d->member_rows, sizeof(float) * size_t(M) * dim,
+                        hipMemcpyHostToDevice));
+    }
+  }
   SMX_HIP(hipMemcpy(ix.centers, d->centers, sizeof(float) * nl * dim, hipMemcpyHostToDevice));
   SMX_HIP(hipMemcpy(ix.centers_t, ct.data(), sizeof(float) * nl * dim, hipMemcpyHostToDevice));
   SMX_HIP(hipMemcpy(ix.cnorm, cn.data(), sizeof(float) * nl, hipMemcpyHostToDevice));
@@ -239,7 +263,8 @@ int UploadIndex(const smx_index_desc* d, smx_index* h) {
 void FreeIndex(smx::DeviceIndex& ix) {
   DFree(ix.centers); DFree(ix.centers_t); DFree(ix.cnorm); DFree(ix.codebook);
   DFree(ix.tiles); DFree(ix.tile_off); DFree(ix.leaf_size); DFree(ix.member_off);
-  DFree(ix.members); DFree(ix.leaf_order); DFree(ix.dataset);
+  DFree(ix.members); DFree(ix.leaf_order); DFree(ix.dataset); DFree(ix.row_base);
+  DFree(ix.member_rows);
 }
 
 int ValidateDesc(const smx_index_desc* d) {
@@ -325,13 +350,13 @@ float Elapsed(smx_index* h, int a, int b) {
 // reorder and output the pre-reorder set (width pre_nn).
 int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int final_nn,
               bool reorder, bool pre_only, uint32_t* out_idx, float* out_dist,
-              int32_t* out_count, hipStream_t s) {
+              int32_t* out_count, hipStream_t s, smx::ShardEntry* shard_out = nullptr) {
   smx::DeviceIndex& ix = h->ix;
   if (nq == 0) return SMX_OK;
   L = std::min(L, ix.nl);
   const int pnn = reorder ? pre_nn : final_nn;
   const int kk = std::max(1, SpillK(ix, pnn));
-  const int width = pre_only ? pnn : final_nn;
+  const int width = shard_out ? 1 : pre_only ? pnn : final_nn;
   int rc = EnsureWorkspace(h, nq, L, kk, width);
   if (rc) return rc;
   Workspace& w = h->ws;
@@ -427,6 +452,9 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sel.overflow = stats;
   sel.fallback = w.fallback;
   sel.qlist = nullptr;
+  sel.shard_out = shard_out;
+  sel.row_base = ix.row_base;
+  sel.member_rows = ix.member_rows;
 
   int retries = 0;
   uint32_t st[10] = {0};
@@ -488,7 +516,7 @@ int CheckSearchArgs(smx_index* h, int nq, int dim, const smx_search_params* p) {
   if (p->final_nn <= 0) return Fail(SMX_INVALID_ARGUMENT, "final_num_neighbors must be > 0");
   if (p->reorder && p->pre_reorder_nn <= 0)
     return Fail(SMX_INVALID_ARGUMENT, "pre_reorder_num_neighbors must be > 0");
-  if (p->reorder && !h->ix.dataset)
+  if (p->reorder && !h->ix.dataset && !h->ix.member_rows)
     return Fail(SMX_FAILED_PRECONDITION, "exact reordering requested but index has no dataset");
   const int pnn = p->reorder ? p->pre_reorder_nn : p->final_nn;
   if (SpillK(h->ix, pnn) > 8192)
@@ -605,6 +633,65 @@ int smx_search_batched(smx_index* h, const float* queries, int32_t nq, int32_t d
   if (out_count)
     SMX_HIP(hipMemcpyAsync(out_count, w.out_count, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, s));
   SMX_HIP(hipStreamSynchronize(s));
+  return SMX_OK;
+}
+
+int smx_shard_width(const smx_index* h, const smx_search_params* p, int32_t* out_k) {
+  if (!h || !p || !out_k) return Fail(SMX_INVALID_ARGUMENT, "null argument");
+  const int pnn = p->reorder ? p->pre_reorder_nn : p->final_nn;
+  if (pnn <= 0) return Fail(SMX_INVALID_ARGUMENT, "neighbor counts must be > 0");
+  *out_k = std::max(1, SpillK(h->ix, pnn));
+  return SMX_OK;
+}
+
+int smx_search_shard_device(smx_index* h, const float* d_queries, int32_t nq, int32_t dim,
+                            const smx_search_params* p, smx_shard_entry* d_entries,
+                            void* stream) {
+  int rc = CheckSearchArgs(h, nq, dim, p);
+  if (rc) return rc;
+  const int pnn = p->reorder ? p->pre_reorder_nn : p->final_nn;
+  if (std::max(1, SpillK(h->ix, pnn)) > 256)
+    return Fail(SMX_INVALID_ARGUMENT, "shard lists above 256 entries per query are not supported");
+  if (nq > 0 && !d_entries) return Fail(SMX_INVALID_ARGUMENT, "null entries buffer");
+  static_assert(sizeof(smx_shard_entry) == sizeof(smx::ShardEntry), "entry layout");
+  std::lock_guard<std::mutex> lock(h->mu);
+  SMX_HIP(hipSetDevice(h->device));
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+  return RunSearch(h, d_queries, nq, p->leaves_to_search, p->pre_reorder_nn, p->final_nn,
+                   p->reorder != 0, false, nullptr, nullptr, nullptr, s,
+                   reinterpret_cast<smx::ShardEntry*>(d_entries));
+}
+
+int smx_merge_shards_device(smx_index* h, int32_t world, int32_t nq,
+                            const smx_search_params* p, const smx_shard_entry* d_entries,
+                            uint32_t* d_out_idx, float* d_out_dist, int32_t* d_out_count,
+                            void* stream) {
+  if (!h || !p) return Fail(SMX_INVALID_ARGUMENT, "null argument");
+  if (world < 1 || world > 64) return Fail(SMX_INVALID_ARGUMENT, "world must be in [1, 64]");
+  if (nq < 0) return Fail(SMX_INVALID_ARGUMENT, "negative batch size");
+  if (p->final_nn <= 0) return Fail(SMX_INVALID_ARGUMENT, "final_num_neighbors must be > 0");
+  const int pnn = p->reorder ? p->pre_reorder_nn : p->final_nn;
+  if (pnn <= 0) return Fail(SMX_INVALID_ARGUMENT, "neighbor counts must be > 0");
+  const int kk = std::max(1, SpillK(h->ix, pnn));
+  if (kk > 256 || world * kk > 2048)
+    return Fail(SMX_INVALID_ARGUMENT, "world x shard list width above 2048 is not supported");
+  if (nq == 0) return SMX_OK;
+  std::lock_guard<std::mutex> lock(h->mu);
+  SMX_HIP(hipSetDevice(h->device));
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+  smx::MergeArgs m{};
+  m.entries = reinterpret_cast<const smx::ShardEntry*>(d_entries);
+  m.world = world;
+  m.nq = nq;
+  m.kk = kk;
+  m.pre_nn = pnn;
+  m.disjoint = h->ix.disjoint ? 1 : 0;
+  m.reorder = p->reorder ? 1 : 0;
+  m.out_idx = d_out_idx;
+  m.out_dist = d_out_dist;
+  m.out_count = d_out_count;
+  m.out_width = p->final_nn;
+  SMX_HIP(smx::LaunchMergeShards(m, s));
   return SMX_OK;
 }
 

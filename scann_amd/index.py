@@ -43,6 +43,13 @@ class IndexDesc(ctypes.Structure):
         ("dataset", ctypes.c_void_p),
         ("spilling_overretrieve_factor", ctypes.c_float),
         ("pad_", ctypes.c_int32),
+        # range-split shard (include/scann_mi355x.h); zero for a whole index
+        ("is_shard", ctypes.c_int32),
+        ("global_topn_shift", ctypes.c_int32),
+        ("global_spilled", ctypes.c_int32),
+        ("reserved2", ctypes.c_int32),
+        ("leaf_row_base", ctypes.c_void_p),
+        ("member_rows", ctypes.c_void_p),
     ]
 
 
@@ -65,6 +72,11 @@ class TreeAHIndex:
     num_datapoints: int
     dataset: Optional[np.ndarray] = None   # float32 [N, D] (exact reorder)
     spilling_overretrieve_factor: float = 2.0
+    # range-split shard of a whole index; see shard()
+    leaf_row_base: Optional[np.ndarray] = None   # uint32 [L]
+    global_topn_shift: int = -1
+    global_spilled: bool = False
+    member_rows: Optional[np.ndarray] = None     # float32 [M, D]
 
     def __post_init__(self):
         self.centers = np.ascontiguousarray(self.centers, dtype=np.float32)
@@ -74,6 +86,10 @@ class TreeAHIndex:
         self.member_codes = np.ascontiguousarray(self.member_codes, dtype=np.uint8)
         if self.dataset is not None:
             self.dataset = np.ascontiguousarray(self.dataset, dtype=np.float32)
+        if self.leaf_row_base is not None:
+            self.leaf_row_base = np.ascontiguousarray(self.leaf_row_base, dtype=np.uint32)
+        if self.member_rows is not None:
+            self.member_rows = np.ascontiguousarray(self.member_rows, dtype=np.float32)
         self.validate()
 
     @property
@@ -85,8 +101,58 @@ class TreeAHIndex:
         return int(self.leaf_members.shape[0])
 
     @property
+    def is_shard(self) -> bool:
+        return self.leaf_row_base is not None
+
+    @property
     def disjoint(self) -> bool:
+        if self.is_shard:
+            return not self.global_spilled
         return self.num_members == self.num_datapoints
+
+    def global_topn_shift_value(self) -> int:
+        """GlobalTopNShift (tree_ah_hybrid_residual.h:234-247) of this whole index."""
+        if self.is_shard:
+            return int(self.global_topn_shift)
+        L = self.num_leaves
+        if not self.residual or L <= 1:
+            return 0
+        inner = 32 - int(np.ceil(np.log2(L)))
+        return inner if int(self.leaf_sizes().max(initial=0)) <= (1 << inner) else 0
+
+    def shard(self, rank: int, world: int, own_rows: bool = True) -> "TreeAHIndex":
+        """Rank `rank` of a `world`-way range split: rows [n*r/W, n*(r+1)/W) of
+        every leaf (balanced whatever the query popularity).
+        Ties stay the whole index's (leaf << shift | row) through
+        leaf_row_base.  With own_rows (global top-N indexes) the shard carries
+        only its members' float rows for the reorder instead of the dataset."""
+        if self.is_shard:
+            raise ValueError("already a shard")
+        if not 0 <= rank < world:
+            raise ValueError("rank out of range")
+        sizes = self.leaf_sizes()
+        lo = (sizes * rank) // world
+        hi = (sizes * (rank + 1)) // world
+        offs = self.leaf_offsets.astype(np.int64)
+        take = np.concatenate([np.arange(offs[l] + lo[l], offs[l] + hi[l]) for l in range(self.num_leaves)]
+                              ) if self.num_leaves else np.zeros(0, np.int64)
+        take = take.astype(np.int64)
+        new_offs = np.concatenate([[0], np.cumsum(hi - lo)]).astype(np.uint64)
+        shift = self.global_topn_shift_value()
+        members = self.leaf_members[take]
+        rows = None
+        dataset = self.dataset
+        if own_rows and shift > 0 and self.dataset is not None:
+            rows = self.dataset[members]
+            dataset = None
+        return TreeAHIndex(
+            metric=self.metric, dim=self.dim, num_blocks=self.num_blocks,
+            dims_per_block=self.dims_per_block, residual=self.residual, centers=self.centers,
+            codebook=self.codebook, leaf_offsets=new_offs, leaf_members=members,
+            member_codes=self.member_codes[take], num_datapoints=self.num_datapoints,
+            dataset=dataset, spilling_overretrieve_factor=self.spilling_overretrieve_factor,
+            leaf_row_base=lo.astype(np.uint32), global_topn_shift=shift,
+            global_spilled=not self.disjoint, member_rows=rows)
 
     def leaf_sizes(self) -> np.ndarray:
         return np.diff(self.leaf_offsets).astype(np.int64)
@@ -116,6 +182,10 @@ class TreeAHIndex:
             raise ValueError("member id out of range")
         if self.dataset is not None and self.dataset.shape != (self.num_datapoints, self.dim):
             raise ValueError("dataset shape mismatch")
+        if self.leaf_row_base is not None and self.leaf_row_base.shape != (L,):
+            raise ValueError("leaf_row_base must have num_leaves entries")
+        if self.member_rows is not None and self.member_rows.shape != (M, self.dim):
+            raise ValueError("member_rows must be [members, dim]")
 
     def desc(self) -> IndexDesc:
         """Borrowed-pointer descriptor; keep ``self`` alive while it is used."""
@@ -127,7 +197,12 @@ class TreeAHIndex:
             leaf_offsets=_ptr(self.leaf_offsets), leaf_members=_ptr(self.leaf_members),
             member_codes=_ptr(self.member_codes), num_datapoints=self.num_datapoints,
             dataset=_ptr(self.dataset),
-            spilling_overretrieve_factor=float(self.spilling_overretrieve_factor), pad_=0)
+            spilling_overretrieve_factor=float(self.spilling_overretrieve_factor), pad_=0,
+            is_shard=int(self.is_shard),
+            global_topn_shift=int(self.global_topn_shift) if self.is_shard else 0,
+            global_spilled=int(bool(self.global_spilled)) if self.is_shard else 0,
+            reserved2=0, leaf_row_base=_ptr(self.leaf_row_base),
+            member_rows=_ptr(self.member_rows))
 
     # -- serialization (own format; reference proto assets are SURVEY §8f-2) --
     def save(self, directory: str) -> None:

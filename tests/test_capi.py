@@ -72,10 +72,33 @@ def test_descriptor_validation_without_gpu(lib, small_dot):
     assert lib.smx_search_batched(None, None, 0, 32, ctypes.byref(p), None, None, None) == -1
 
 
-def test_struct_layout_matches_header():
-    """IndexDesc (ctypes) mirrors smx_index_desc: field order and offsets."""
+def test_struct_layout_matches_header(tmp_path):
+    """IndexDesc / SearchParams / Timings (ctypes) mirror the header: every
+    field offset and the struct sizes, as the C compiler lays them out."""
+    import os
+    import subprocess
     from scann_amd.index import IndexDesc
-    names = [f[0] for f in IndexDesc._fields_]
-    assert names[:6] == ["metric", "dim", "num_leaves", "num_blocks", "dims_per_block", "residual"]
-    assert IndexDesc.centers.offset == 24 and IndexDesc.dataset.offset == 72
-    assert ctypes.sizeof(IndexDesc) == 88
+    from scann_amd._native import SearchParams, Timings
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    structs = {"smx_index_desc": IndexDesc, "smx_search_params": SearchParams,
+               "smx_timings": Timings}
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "scann_mi355x.h"',
+             "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'  printf("{cname} %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            cf = "reserved" if (cname == "smx_index_desc" and fname == "pad_") else fname
+            lines.append(f'  printf("{cname}.{fname} %zu\\n", offsetof({cname}, {cf}));')
+    lines.append('  printf("smx_shard_entry %zu\\n", sizeof(smx_shard_entry));')
+    lines.append("  return 0;\n}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(root, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                         text=True).stdout.splitlines())
+    for cname, py in structs.items():
+        assert int(got[cname]) == ctypes.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert int(got[f"{cname}.{fname}"]) == getattr(py, fname).offset, (cname, fname)
+    assert int(got["smx_shard_entry"]) == 16
