@@ -225,9 +225,9 @@ int smx_lut16_leaf_scores(smx_index* index, int32_t leaf, const uint8_t* lut,
 int smx_set_profiling(smx_index* index, int32_t enabled);
 int smx_get_timings(const smx_index* index, smx_timings* out);
 /* Tuning knobs: candidate buffer capacity per query, seed leaves used for the
- * per-query threshold, scan kernel variant (0 = block items with LUT rows in
- * LDS, 1 = wave items with LUT rows in VGPRs) and tiles per work item
- * (0 keeps the variant's default). */
+ * per-query threshold, scan kernel variant (0 = the scan, 4 = the scan
+ * without its threshold epilogue: a timing ablation whose results are
+ * invalid) and tiles per work item (0 keeps the default, 32). */
 int smx_set_tuning(smx_index* index, int32_t candidates_per_query, int32_t seed_leaves,
                    int32_t scan_variant, int32_t chunk_tiles);
 

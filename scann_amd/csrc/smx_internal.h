@@ -144,18 +144,16 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
 hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq,
                           int8_t* lut, float* mult, float* inv, uint8_t* lut_u8,
                           hipStream_t s);
-hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf,
-                       const float* topl_dist, int nq, int L, uint32_t* cnt /*[nl]*/,
+hipError_t LaunchPairs(const DeviceIndex& ix, const uint32_t* order /*[nl] work order*/,
+                       const int32_t* topl_leaf, const float* topl_dist, int nq, int L, uint32_t* cnt /*[nl]*/,
                        uint32_t* block_cnt /*[ceil(nq*L/4096)][nl]*/,
                        uint32_t* pair_off /*[nl]*/, uint32_t* tile_prefix /*[nl+1]*/,
                        uint32_t* pair_q /*[nq*L]*/, float* pair_bias /*[nq*L]*/,
                        uint2* work /*[max items]*/, uint32_t* totals /*[3]*/,
                        unsigned long long* code_bytes /*[1]*/, uint32_t chunk_tiles,
-                       uint32_t queries_per_item /*32 or 64*/, hipStream_t s);
-// variant 0 (default): block items of 32 queries, LUT rows in LDS, hit
-// lists drained once per item; 1: wave-level items with the LUT rows in
-// VGPRs; 2: block items with per-lane survivor slots; 4: variant 0 without
-// its threshold epilogue (timing ablation, results invalid).
+                       uint32_t queries_per_item /*32*/, hipStream_t s);
+// variant 0: the LUT16 scan (lut16_scan_kernel); 4: the same without its
+// threshold epilogue (timing ablation, results invalid).
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,
                       hipStream_t s);
 hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s);

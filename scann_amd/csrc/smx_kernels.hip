@@ -460,8 +460,7 @@ __global__ void pairs_work_kernel(const uint32_t* __restrict__ tile_prefix,
   if (p >= nl) return;
   const uint32_t leaf = order[p];
   const uint32_t chunks = LeafChunks(leaf_size[leaf], chunk_tiles);
-  // item = (leaf, query tile << 16 | dp chunk); chunk-major so that a leaf's
-  // first chunks (all query tiles) are dequeued together
+  // item = (leaf, query tile << 16 | dp chunk)
   for (uint32_t w = tile_prefix[p]; w < tile_prefix[p + 1]; ++w) {
     const uint32_t u = w - tile_prefix[p];
     work[w] = make_uint2(leaf, ((u / chunks) << 16) | (u % chunks));
@@ -471,19 +470,19 @@ __global__ void pairs_work_kernel(const uint32_t* __restrict__ tile_prefix,
 // ---------------------------------------------------------------------------
 // LUT16 scan on MFMA.
 //
-// One wave owns a work item = (leaf, 32 queries of that leaf).  For every
-// 32-datapoint tile of the leaf it computes the 32x32 matrix of LUT16 sums
+// A 256-thread block owns a work item = (leaf, 32 queries of that leaf, a
+// chunk of the leaf's 32-datapoint tiles).  For every tile it computes the
+// 32x32 matrix of LUT16 sums
 //     S[dp][q] = sum_b int8LUT_q[b][code(dp, b)]
 // as K = ceil(B/2) MFMA i32_32x32x32_i8 steps: A = one-hot codes (row = dp,
 // 16 bytes per lane-half = one block's 16 centers), B = the queries' int8
-// LUT rows (held in VGPRs for the whole leaf).  The i32 sums are exact
+// LUT rows (staged in LDS once per item).  The i32 sums are exact
 // (|S| <= 127*B).  Lane (c, h) of the accumulator holds 16 datapoints of
-// query c, so the epilogue converts, thresholds and emits per lane:
+// query c; a datapoint can only pass when S <= amax_c (the largest sum whose
+// distance can pass the query's threshold: d is monotone in S), and only
+// those are converted:
 //     d = fl(fl(float(S) * inv_q) + bias_{q,leaf})
-// and appends (ordered(d) << 32 | tie) to the query's candidate list when
-// (d, tie) <= the query's threshold key.  Only S <= amax (the largest sum
-// whose distance can pass, found by bisection: d is monotone in S) is
-// converted.
+// and emitted as (ordered(d) << 32 | tie) when that key <= the threshold key.
 // ---------------------------------------------------------------------------
 // 16-byte one-hot of nibble t (byte t = 1): 1 << 8(t mod 8) in the 64-bit
 // half selected by bit 3.  `sh` = 8 * t (bits 3..6), so the 64-bit shift
@@ -497,21 +496,6 @@ __device__ __forceinline__ v4i OneHot16(uint32_t sh) {
   r[1] = int(hi & ~m);
   r[2] = int(lo & m);
   r[3] = int(hi & m);
-  return r;
-}
-
-// One-hot of the 4-bit code at bit offset `sh` of `wv`: the select bit
-// (code >= 8) and its complement are each shifted by 8*(code & 7), giving the
-// low and high 8-byte halves directly (6 VALU ops instead of mask-and-select).
-__device__ __forceinline__ v4i OneHotNibble(uint32_t wv, int sh) {
-  const uint32_t s8 = (sh >= 3 ? (wv >> (sh - 3)) : (wv << (3 - sh))) & 0x38u;
-  const uint64_t hb = (wv >> (sh + 3)) & 1u;
-  const uint64_t lo = (hb ^ 1u) << s8, hi = hb << s8;
-  v4i r;
-  r[0] = int(uint32_t(lo));
-  r[1] = int(uint32_t(lo >> 32));
-  r[2] = int(uint32_t(hi));
-  r[3] = int(uint32_t(hi >> 32));
   return r;
 }
 
@@ -556,101 +540,6 @@ __device__ __forceinline__ void LoadCodes(const uint8_t* p, uint32_t* codes) {
   } else {
 #pragma unroll
     for (int i = 0; i < NW; ++i) codes[i] = w[i];
-  }
-}
-
-// Survivor staging: kStage keys per lane in LDS (32 KiB per 256-thread block,
-// so three blocks fit a CU next to the 3-waves/SIMD register budget).
-constexpr int kStage = 16;
-
-__device__ __forceinline__ void FlushStage(const uint64_t* stage, uint32_t n, uint64_t* dst,
-                                           uint32_t* count, uint32_t cap) {
-  const uint32_t slot = atomicAdd(count, n);
-  for (uint32_t u = 0; u < n && slot + u < cap; ++u) dst[slot + u] = stage[u];
-}
-
-template <int K>
-__global__ void __launch_bounds__(256) lut16_scan_kernel(ScanArgs a) {
-  constexpr int NW = ((((K + 1) / 2) + 3) / 4);
-  constexpr int W = 4 * NW;
-  __shared__ uint64_t stage_all[256 * kStage];
-  uint64_t* stage = stage_all + threadIdx.x * kStage;
-  const int lane = threadIdx.x & 63;
-  const int c = lane & 31;
-  const int h = lane >> 5;
-  const uint32_t total = a.tile_prefix[a.nl];
-  const int smin = -128 * a.nb, smax = 128 * a.nb;
-  for (;;) {
-    uint32_t w = 0;
-    if (lane == 0) w = atomicAdd(a.work_counter, 1u);
-    w = __builtin_amdgcn_readfirstlane(__shfl(w, 0));
-    if (w >= total) break;
-    const uint2 item = a.work[w];
-    const int leaf = int(__builtin_amdgcn_readfirstlane(item.x));
-    const uint32_t t = __builtin_amdgcn_readfirstlane(item.y) >> 16;
-    const uint32_t chunk = __builtin_amdgcn_readfirstlane(item.y) & 0xFFFFu;
-    const uint32_t pbeg = a.pair_off[leaf] + t * kQueriesPerTile;
-    const uint32_t pend = a.pair_off[leaf] + a.leaf_count[leaf];
-    const int nvalid = int(min(uint32_t(kQueriesPerTile), pend - pbeg));
-    const bool valid = c < nvalid;
-    const uint32_t pidx = pbeg + uint32_t(valid ? c : 0);
-    const uint32_t qid = a.pair_q[pidx];
-    const float bias = a.residual ? a.pair_bias[pidx] : 0.0f;
-    const float inv = a.inv[qid];
-    v4i frag[K];
-    const v4i* lrow = reinterpret_cast<const v4i*>(a.lut + size_t(qid) * (2 * K) * 16);
-#pragma unroll
-    for (int s = 0; s < K; ++s) frag[s] = lrow[2 * s + h];
-    const uint64_t T = a.tau_key[qid];
-    const int amax = !valid ? smin - 1
-                     : (T == kNoThreshold)
-                         ? smax
-                         : SumLimit(FromOrdered(uint32_t(T >> 32)), inv, bias, smin, smax);
-    const uint32_t n = a.leaf_size[leaf];
-    const uint32_t ntile_leaf = (n + kDpPerTile - 1) / kDpPerTile;
-    const uint32_t j0 = chunk * a.chunk_tiles;
-    const uint32_t ntile = min(ntile_leaf, j0 + a.chunk_tiles);
-    const uint8_t* tb = a.tiles + a.tile_off[leaf] * 64ull * W + size_t(lane) * W;
-    const uint64_t moff = a.member_off[leaf];
-    uint32_t codes[NW], next[NW];
-    uint32_t staged = 0;
-    if (j0 < ntile) LoadCodes<K>(tb + size_t(j0) * 64 * W, codes);
-    for (uint32_t j = j0; j < ntile; ++j) {
-      if (j + 1 < ntile) LoadCodes<K>(tb + size_t(j + 1) * 64 * W, next);
-      const v16i acc = TileSums<K>(codes, frag);
-      // rows of this lane: (i & 3) + 8 * (i >> 2) + 4 * h of tile j
-      const uint32_t rows_left = n - j * kDpPerTile;  // > 0
-      uint32_t pass = 0;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint32_t row = (i & 3) + 8 * (i >> 2) + 4 * h;
-        pass |= uint32_t((row < rows_left) & (acc[i] <= amax)) << i;
-      }
-      if (pass) {
-        // Rare path: keys <= T go to this lane's LDS staging row; a full row
-        // is flushed with one atomic (the only value-returning atomic here).
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          if (pass >> i & 1u) {
-            const uint32_t dp = j * kDpPerTile + (i & 3) + 8 * (i >> 2) + 4 * h;
-            const float d = DistOf(acc[i], inv, bias);
-            const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp)
-                                             : a.members[moff + dp];
-            const uint64_t key = (uint64_t(OrderedBits(d)) << 32) | tie;
-            if (key <= T) {
-              stage[staged++] = key;
-              if (staged == kStage) {
-                FlushStage(stage, staged, a.cand + size_t(qid) * a.cap, &a.cand_count[qid], a.cap);
-                staged = 0;
-              }
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < NW; ++i) codes[i] = next[i];
-    }
-    if (staged) FlushStage(stage, staged, a.cand + size_t(qid) * a.cap, &a.cand_count[qid], a.cap);
   }
 }
 
@@ -770,329 +659,61 @@ __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
 }
 
 
-// ---------------------------------------------------------------------------
-// Block-level variant (default): a 256-thread block owns a work item
-// (leaf, 32 queries, chunk of tiles); the 32 queries' int8 LUT rows sit in
-// LDS step-major ([2K][32 queries][16 B]: one wave-wide ds_read_b128 per MFMA,
-// conflict-free), the 4 waves take the chunk's tiles round-robin, and
-// survivors are staged per query in LDS (one global atomic per query per
-// item).  Frees the ~100 VGPRs the wave variant spends on B fragments.
-// ---------------------------------------------------------------------------
-// Tile body of the block kernel: K MFMAs per query tile on the same one-hot
-// A fragment (QT = 2 feeds two MFMAs per one-hot build), then the threshold
-// epilogue per query tile.
-template <int K, int QT>
-struct BlockScan {
-  static constexpr int NW = ((((K + 1) / 2) + 3) / 4);
-  static constexpr int W = 4 * NW;
-  static constexpr int Q = 32 * QT;
-  static constexpr int SL = 4;   // survivor slots per lane and item
-};
-
-// The second bound is the occupancy (waves per SIMD) the LDS footprint
-// allows; it caps the register budget to match.
-// Waves per SIMD that the block's LDS footprint allows (capped at 4); used
-// as the occupancy target so the register budget matches.
-constexpr int BlockOccupancy(int k, int qt, int nwv) {
-  const int q = 32 * qt;
-  const int bytes = 2 * k * q * 16 + nwv * qt * 64 * (4 * 4 + 8) + q * 24 + 64;
-  const int blocks = (160 * 1024) / bytes;
-  const int w = blocks * nwv / 4;
-  return w > 4 ? 4 : (w < 1 ? 1 : w);
-}
-
-// K MFMAs of one 32-datapoint tile against NB query tiles whose LUT rows sit
-// in LDS ([2K][Q] x 16 B, this lane's row at lut[2s*Q + off]); B fragments
-// are read kRing steps ahead of their MFMA so LDS latency stays hidden.
+// K MFMAs of one tile.  The one-hot A fragments come from a 16-entry LDS
+// table (oh_tab[t] = 16 bytes with byte t = 1): per MFMA one nibble
+// extraction and two ds_read_b128, both conflict-free (the table spans the 64
+// banks exactly; a step's B rows are 1 KiB contiguous per wave).  Both are
+// read R steps ahead of their MFMA, and a full scheduling barrier closes each
+// step so the compiler cannot collapse the ring.
 constexpr int kRing = 4;
-template <int K, int Q, int NB, int NACC, bool HOIST>
-__device__ __forceinline__ void TileMfma(const uint32_t* codes, const v4i* lut, int off,
-                                         v16i (&acc)[NACC]) {
-  // HOIST: the LUT reads are loop-invariant over the item's tiles and the
-  // compiler keeps them in VGPRs; otherwise an opaque offset forces per-tile
-  // LDS reads (fewer VGPRs, LDS latency on the MFMA chain)
-  if (!HOIST) asm volatile("" : "+v"(off));
-  v4i b[kRing][NB];
+template <int K, int Q, int R = kRing>
+__device__ __forceinline__ v16i TileMfma(const uint32_t* codes, const v4i* lut, int off,
+                                         const v4i* oh_tab) {
+  asm volatile("" : "+v"(off));
+  v4i b[R], o[R];
 #pragma unroll
-  for (int p = 0; p < kRing; ++p)
-#pragma unroll
-    for (int t = 0; t < NB; ++t)
-      if (p < K) b[p][t] = lut[2 * p * Q + off + 32 * t];
-#pragma unroll
-  for (int t = 0; t < NB; ++t) acc[t] = v16i{0};
+  for (int p = 0; p < R; ++p)
+    if (p < K) {
+      b[p] = lut[2 * p * Q + off];
+      o[p] = oh_tab[(codes[p >> 3] >> ((p & 7) * 4)) & 15u];
+    }
+  v16i acc = v16i{0};
 #pragma unroll
   for (int s = 0; s < K; ++s) {
-    const v4i oh = OneHotNibble(codes[s >> 3], (s & 7) * 4);
-#pragma unroll
-    for (int t = 0; t < NB; ++t)
-      acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(oh, b[s % kRing][t], acc[t], 0, 0, 0);
-    if (s + kRing < K) {
-#pragma unroll
-      for (int t = 0; t < NB; ++t) b[s % kRing][t] = lut[2 * (s + kRing) * Q + off + 32 * t];
+    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(o[s % R], b[s % R], acc, 0, 0, 0);
+    if (s + R < K) {
+      const int t = s + R;
+      b[s % R] = lut[2 * t * Q + off];
+      o[s % R] = oh_tab[(codes[t >> 3] >> ((t & 7) * 4)) & 15u];
     }
-    // pin the interleave: one-hot VALU, the MFMA(s), then the ring refill
-    __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, NB, 0);
-    if (s + kRing < K) __builtin_amdgcn_sched_group_barrier(0x100, NB, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
-}
-
-// K MFMAs of one tile with the LUT fragments already in registers.
-template <int K>
-__device__ __forceinline__ v16i TileMfmaReg(const uint32_t* codes, const v4i* frag) {
-  v16i acc = {0};
-#pragma unroll
-  for (int s = 0; s < K; ++s)
-    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(OneHotNibble(codes[s >> 3], (s & 7) * 4), frag[s],
-                                                acc, 0, 0, 0);
   return acc;
 }
 
-// ABL: 8 = LUT fragments held in VGPRs for the whole item (3 waves/SIMD);
-// timing ablations only (results invalid): 2 = no code loads, 4 = no
-// epilogue, 16 = nothing passes the threshold, 32 = no flush.
-template <int K, int QT, int NWV, int ABL = 0>
-__global__ void __launch_bounds__(64 * NWV, ((ABL & 8) ? 3 : BlockOccupancy(K, QT, NWV)))
-    lut16_scan_block_kernel(ScanArgs a) {
-  using B = BlockScan<K, QT>;
-  constexpr int NW = B::NW, W = B::W, Q = B::Q, SL = B::SL, NT = 64 * NWV;
-  __shared__ v4i lut_s[2 * K * Q];
-  // per-lane survivor slots: [wave][query tile][lane][SL] of (sum << 16 | dp)
-  __shared__ uint32_t lstage[NWV * QT * 64 * SL];
-  __shared__ uint32_t lcnt[NWV * QT * 64], loff[NWV * QT * 64];
-  __shared__ uint32_t q_id[Q];
-  __shared__ float q_bias[Q], q_inv[Q];
-  __shared__ int q_amax[Q];
-  __shared__ uint64_t q_T[Q];
-  __shared__ uint32_t s_w;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int c = lane & 31;
-  const int h = lane >> 5;
-  const uint32_t total = a.tile_prefix[a.nl];
-  const int smin = -128 * a.nb, smax = 128 * a.nb;
-  for (;;) {
-    if (tid == 0) s_w = atomicAdd(a.work_counter, 1u);
-    __syncthreads();
-    const uint32_t w = s_w;
-    if (w >= total) break;
-    const uint2 item = a.work[w];
-    const int leaf = int(item.x);
-    const uint32_t t = item.y >> 16;
-    const uint32_t chunk = item.y & 0xFFFFu;
-    const uint32_t pbeg = a.pair_off[leaf] + t * uint32_t(Q);
-    const int nvalid = int(min(uint32_t(Q), a.pair_off[leaf] + a.leaf_count[leaf] - pbeg));
-    // per-query-slot metadata, then the LUT rows ([2K][Q] step-major)
-    for (int i = tid; i < Q; i += NT) {
-      const bool v = i < nvalid;
-      const uint32_t pidx = pbeg + uint32_t(v ? i : 0);
-      const uint32_t qid = a.pair_q[pidx];
-      const float bias = a.residual ? a.pair_bias[pidx] : 0.0f;
-      const float inv = a.inv[qid];
-      const uint64_t T = a.tau_key[qid];
-      q_id[i] = qid;
-      q_bias[i] = bias;
-      q_inv[i] = inv;
-      q_T[i] = T;
-      q_amax[i] = !v ? smin - 1
-                : (T == kNoThreshold) ? smax
-                : SumLimit(FromOrdered(uint32_t(T >> 32)), inv, bias, smin, smax);
-    }
-    for (int e = tid; e < K * Q; e += NT) {
-      const int qs = e % Q, rp = e / Q;   // rows 2rp, 2rp+1 of query slot qs
-      const uint32_t pidx = pbeg + uint32_t(qs < nvalid ? qs : 0);
-      const v4i* src = reinterpret_cast<const v4i*>(a.lut) + size_t(a.pair_q[pidx]) * 2 * K + 2 * rp;
-      const v4i r0 = src[0], r1 = src[1];
-      lut_s[(2 * rp) * Q + qs] = r0;
-      lut_s[(2 * rp + 1) * Q + qs] = r1;
-    }
-    __syncthreads();
-    const bool two = QT == 2 && nvalid > 32;   // block-uniform
-    uint32_t qid[QT], ns[QT];
-    float bias[QT], inv[QT];
-    int amax[QT];
-    uint64_t T[QT];
-#pragma unroll
-    for (int u = 0; u < QT; ++u) {
-      qid[u] = q_id[u * 32 + c];
-      bias[u] = q_bias[u * 32 + c];
-      inv[u] = q_inv[u * 32 + c];
-      amax[u] = (ABL & 16) ? smin - 1 : q_amax[u * 32 + c];
-      T[u] = q_T[u * 32 + c];
-      ns[u] = 0;
-    }
-    const uint32_t n = a.leaf_size[leaf];
-    const uint32_t ntile_leaf = (n + kDpPerTile - 1) / kDpPerTile;
-    const uint32_t j0 = chunk * a.chunk_tiles;
-    const uint32_t jend = min(ntile_leaf, j0 + a.chunk_tiles);
-    const uint8_t* tb = a.tiles + a.tile_off[leaf] * 64ull * W + size_t(lane) * W;
-    const uint64_t moff = a.member_off[leaf];
-
-    constexpr bool kRegFrag = QT == 1 && (ABL & 8);
-    v4i frag[kRegFrag ? K : 1];
-    if (kRegFrag) {
-#pragma unroll
-      for (int s2 = 0; s2 < K; ++s2) frag[s2] = lut_s[(2 * s2 + h) * Q + c];
-    }
-    auto body = [&](const uint32_t (&codes)[NW], uint32_t j) {
-      v16i acc[QT];
-      if (kRegFrag)
-        acc[0] = TileMfmaReg<K>(codes, frag);
-      else if (QT == 2 && two)
-        TileMfma<K, Q, 2, QT, false>(codes, lut_s, h * Q + c, acc);
-      else
-        TileMfma<K, Q, 1, QT, false>(codes, lut_s, h * Q + c, acc);
-      if (ABL & 4) {
-        int m = acc[0][0];
-#pragma unroll
-        for (int i = 1; i < 16; ++i) m ^= acc[0][i];
-        if (m == 0x7fffffff) a.cand_count[0] = m;
-        return;
-      }
-      const uint32_t rows_left = n - j * kDpPerTile;
-      const bool full = rows_left >= uint32_t(kDpPerTile);   // wave-uniform
-#pragma unroll
-      for (int u = 0; u < QT; ++u) {
-        if (u == 1 && !two) break;
-        // one compare per lane on the tile minimum; survivors are rare, so
-        // the per-element tests below run under a mostly empty exec mask
-        int m = min(min(acc[u][0], acc[u][1]), acc[u][2]);
-#pragma unroll
-        for (int i = 3; i < 15; i += 2) m = min(min(m, acc[u][i]), acc[u][i + 1]);
-        m = min(m, acc[u][15]);
-        if (m > amax[u]) continue;
-        uint32_t* st = lstage + ((wave * QT + u) * 64 + lane) * SL;
-        // wave-uniform list of the elements some lane passes (ballots), then
-        // a scalar loop over just those: no per-element branch structure
-        if (!full) {  // last tile of the leaf: rows past its end never pass
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const uint32_t row = (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (row >= rows_left) acc[u][i] = INT_MAX;
-          }
-        }
-        uint32_t emask = 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          emask |= (__builtin_amdgcn_ballot_w64(acc[u][i] <= amax[u]) != 0 ? 1u : 0u) << i;
-        while (emask) {
-          const int i = __builtin_ctz(emask);
-          emask &= emask - 1;
-          int v = acc[u][0];
-#pragma unroll
-          for (int k = 1; k < 16; ++k) v = (k == i) ? acc[u][k] : v;
-          const uint32_t row = (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (v <= amax[u]) {
-            // slot = (sum, local dp) packed in 32 bits; the distance, the key
-            // and the exact threshold test are applied at the flush
-            const uint32_t dp = j * kDpPerTile + row;
-            if (ns[u] < uint32_t(SL)) {
-              st[ns[u]] = (uint32_t(v) << 16) | dp;
-            } else {  // lane slots full (rare): straight to the global list
-              const float d = DistOf(v, inv[u], bias[u]);
-              const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp)
-                                               : a.members[moff + dp];
-              const uint64_t key = (uint64_t(OrderedBits(d)) << 32) | tie;
-              if (key <= T[u]) {
-                const uint32_t gs = atomicAdd(&a.cand_count[qid[u]], 1u);
-                if (gs < a.cap) a.cand[size_t(qid[u]) * a.cap + gs] = key;
-              }
-            }
-            ++ns[u];
-          }
-        }
-      }
-    };
-
-    // codes of the next tile are loaded while the current one is scored
-    uint32_t codes[NW], next[NW];
-    uint32_t j = j0 + wave;
-    if (j < jend) LoadCodes<K>(tb + size_t(j) * 64 * W, codes);
-    for (; j < jend; j += NWV) {
-      if (ABL & 2) {
-#pragma unroll
-        for (int i = 0; i < NW; ++i) next[i] = codes[i] * 0x9E3779B9u + j;
-      } else if (j + NWV < jend) LoadCodes<K>(tb + size_t(j + NWV) * 64 * W, next);
-      body(codes, j);
-#pragma unroll
-      for (int i = 0; i < NW; ++i) codes[i] = next[i];
-    }
-    // exact threshold test on this lane's slots (keys at the threshold
-    // distance are decided by the tie id); survivors are compacted in place
-#pragma unroll
-    for (int u = 0; u < QT; ++u) {
-      uint32_t* st = lstage + ((wave * QT + u) * 64 + lane) * SL;
-      const uint32_t m = min(ns[u], uint32_t(SL));
-      uint32_t kept = 0;
-      for (uint32_t k = 0; k < m; ++k) {
-        const uint32_t v = st[k];
-        const int sum = int(v) >> 16;
-        const uint32_t dp = v & 0xFFFFu;
-        const uint32_t ob = OrderedBits(DistOf(sum, inv[u], bias[u]));
-        const uint32_t tob = uint32_t(T[u] >> 32);
-        bool ok = ob < tob;
-        if (ob == tob) {
-          const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp)
-                                           : a.members[moff + dp];
-          ok = tie <= uint32_t(T[u]);
-        }
-        if (ok) st[kept++] = v;
-      }
-      lcnt[(wave * QT + u) * 64 + lane] = kept;
-    }
-    __syncthreads();
-    // flush: per query slot, one global atomic for the survivors its 2*NWV
-    // lanes kept; each lane's slots then land at their running offset
-    for (int i = tid; i < Q; i += NT) {
-      const int u = i >> 5, cc = i & 31;
-      uint32_t tot = 0;
-      for (int wv = 0; wv < NWV; ++wv)
-        for (int hh = 0; hh < 2; ++hh) {
-          const int src = (wv * QT + u) * 64 + hh * 32 + cc;
-          loff[src] = tot;
-          tot += lcnt[src];
-        }
-      const uint32_t base = tot ? atomicAdd(&a.cand_count[q_id[i]], tot) : 0u;
-      for (int wv = 0; wv < NWV; ++wv)
-        for (int hh = 0; hh < 2; ++hh) loff[(wv * QT + u) * 64 + hh * 32 + cc] += base;
-    }
-    __syncthreads();
-    for (int e = tid; e < NWV * QT * 64 * SL; e += NT) {
-      const int src = e / SL, k = e - src * SL;
-      if (uint32_t(k) < lcnt[src]) {
-        const int u = (src / 64) % QT, l = src & 63;
-        const int qs = u * 32 + (l & 31);
-        const uint32_t slot = loff[src] + k;
-        const uint32_t v = lstage[e];
-        const uint32_t dp = v & 0xFFFFu;
-        const float d = DistOf(int(v) >> 16, q_inv[qs], q_bias[qs]);
-        const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp) : a.members[moff + dp];
-        if (slot < a.cap)
-          a.cand[size_t(q_id[qs]) * a.cap + slot] = (uint64_t(OrderedBits(d)) << 32) | tie;
-      }
-    }
-    __syncthreads();
-  }
-}
-
 // ---------------------------------------------------------------------------
-// Default scan (variant 0): block items as above, but the threshold epilogue
-// is split in two.  In the tile loop a lane whose tile minimum passes only
-// appends its 16 sums (packed int16) and a tag to its wave's LDS hit list
-// (~20 instructions for the whole wave, once per tile with a hit); the
-// per-element test, the key and the exact threshold compare run in drain(),
-// lane-parallel over hits, once per item (or when the list fills).
+// The scan kernel.  Persistent blocks claim items from a work counter
+// (largest leaves first).  Per item: the 32 queries' parameters and LUT rows
+// go to LDS ([row][query] x 16 B), the 4 waves take the chunk's tiles
+// round-robin (code tile j+4 prefetched while tile j computes).  The
+// threshold epilogue is split in two: in the tile loop a lane whose 16-sum
+// minimum passes only appends its sums (packed int16) and a tag to its wave's
+// LDS hit list; drain() runs the per-element test, the key and the exact
+// threshold compare lane-parallel over the hits, once per item (or when the
+// list fills), and stages survivors per query in LDS: one global atomic per
+// query per item.
+// ABL = 4: timing ablation without the epilogue (results invalid).
 // ---------------------------------------------------------------------------
 constexpr int kHitsPerWave = 64;   // >= 64: a tile may add a hit per lane right after a drain
 constexpr int kQStageHits = 16;
 
 template <int K, int ABL = 0>
-__global__ void __launch_bounds__(256, (K <= 25 ? 4 : 3)) lut16_scan_hits_kernel(ScanArgs a) {
+__global__ void __launch_bounds__(256, (K <= 25 ? 4 : 3)) lut16_scan_kernel(ScanArgs a) {
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
   constexpr int W = 4 * NW;
   constexpr int Q = 32, NWV = 4, NT = 256, HW = kHitsPerWave, S = kQStageHits;
-  __shared__ v4i lut_s[2 * K * Q];
+  constexpr int ROWS = 2 * K * Q, PER = (ROWS + NT - 1) / NT;
+  __shared__ v4i lut_s[ROWS];
   __shared__ uint4 hsum[NWV][HW][2];     // 16 sums as int16 pairs
   __shared__ uint32_t hmeta[NWV][HW];    // tile << 6 | lane
   __shared__ uint64_t qstage[Q * S];
@@ -1101,11 +722,17 @@ __global__ void __launch_bounds__(256, (K <= 25 ? 4 : 3)) lut16_scan_hits_kernel
   __shared__ int q_amax[Q];
   __shared__ uint64_t q_T[Q];
   __shared__ uint32_t s_w;
+  __shared__ v4i oh_tab[16];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int c = lane & 31;
   const int h = lane >> 5;
+  if (tid < 16) {
+    v4i t = {0, 0, 0, 0};
+    t[tid >> 2] = int(1u << (8 * (tid & 3)));
+    oh_tab[tid] = t;
+  }
   const uint32_t total = a.tile_prefix[a.nl];
   const int smin = -128 * a.nb, smax = 128 * a.nb;
   for (;;) {
@@ -1120,11 +747,11 @@ __global__ void __launch_bounds__(256, (K <= 25 ? 4 : 3)) lut16_scan_hits_kernel
     const uint32_t chunk = item.y & 0xFFFFu;
     const uint32_t pbeg = a.pair_off[leaf] + t * uint32_t(Q);
     const int nvalid = int(min(uint32_t(Q), a.pair_off[leaf] + a.leaf_count[leaf] - pbeg));
+    // this thread's query slot is fixed (NT is a multiple of Q): one id load
+    const uint32_t qid = a.pair_q[pbeg + uint32_t(c < nvalid ? c : 0)];
     if (tid < Q) {
       const bool v = tid < nvalid;
-      const uint32_t pidx = pbeg + uint32_t(v ? tid : 0);
-      const uint32_t qid = a.pair_q[pidx];
-      const float bias = a.residual ? a.pair_bias[pidx] : 0.0f;
+      const float bias = a.residual ? a.pair_bias[pbeg + uint32_t(v ? tid : 0)] : 0.0f;
       const float inv = a.inv[qid];
       const uint64_t T = a.tau_key[qid];
       q_id[tid] = qid;
@@ -1135,13 +762,18 @@ __global__ void __launch_bounds__(256, (K <= 25 ? 4 : 3)) lut16_scan_hits_kernel
                   : (T == kNoThreshold) ? smax
                   : SumLimit(FromOrdered(uint32_t(T >> 32)), inv, bias, smin, smax);
     }
-    for (int e = tid; e < K * Q; e += NT) {
-      const int qs = e % Q, rp = e / Q;   // rows 2rp, 2rp+1 of query slot qs
-      const uint32_t pidx = pbeg + uint32_t(qs < nvalid ? qs : 0);
-      const v4i* src = reinterpret_cast<const v4i*>(a.lut) + size_t(a.pair_q[pidx]) * 2 * K + 2 * rp;
-      const v4i r0 = src[0], r1 = src[1];
-      lut_s[(2 * rp) * Q + qs] = r0;
-      lut_s[(2 * rp + 1) * Q + qs] = r1;
+    {
+      // LUT rows of the 32 queries into LDS ([row][query] x 16 B); the loads
+      // are unconditional (clamped row) so they are all in flight together
+      const v4i* src = reinterpret_cast<const v4i*>(a.lut) + size_t(qid) * 2 * K;
+      v4i stg[PER];
+#pragma unroll
+      for (int i = 0; i < PER; ++i) stg[i] = src[min(tid + i * NT, ROWS - 1) / Q];
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int e = tid + i * NT;
+        if (e < ROWS) lut_s[e] = stg[i];
+      }
     }
     __syncthreads();
     const int amax = q_amax[c];
@@ -1190,12 +822,11 @@ __global__ void __launch_bounds__(256, (K <= 25 ? 4 : 3)) lut16_scan_hits_kernel
     };
 
     auto body = [&](const uint32_t (&codes)[NW], uint32_t j) {
-      v16i acc[1];
-      TileMfma<K, Q, 1, 1, false>(codes, lut_s, h * Q + c, acc);
+      v16i acc = TileMfma<K, Q>(codes, lut_s, h * Q + c, oh_tab);
       if (ABL & 4) {
-        int x = acc[0][0];
+        int x = acc[0];
 #pragma unroll
-        for (int i = 1; i < 16; ++i) x ^= acc[0][i];
+        for (int i = 1; i < 16; ++i) x ^= acc[i];
         if (x == 0x7fffffff) a.cand_count[0] = x;
         return;
       }
@@ -1204,13 +835,13 @@ __global__ void __launch_bounds__(256, (K <= 25 ? 4 : 3)) lut16_scan_hits_kernel
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const uint32_t row = (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (row >= rows_left) acc[0][i] = 0x7FFF;
+          if (row >= rows_left) acc[i] = 0x7FFF;
         }
       }
-      int m = min(min(acc[0][0], acc[0][1]), acc[0][2]);
+      int m = min(min(acc[0], acc[1]), acc[2]);
 #pragma unroll
-      for (int i = 3; i < 15; i += 2) m = min(min(m, acc[0][i]), acc[0][i + 1]);
-      m = min(m, acc[0][15]);
+      for (int i = 3; i < 15; i += 2) m = min(min(m, acc[i]), acc[i + 1]);
+      m = min(m, acc[15]);
       const bool hit = m <= amax;
       const uint64_t hb = __builtin_amdgcn_ballot_w64(hit);
       if (hb) {
@@ -1226,7 +857,7 @@ __global__ void __launch_bounds__(256, (K <= 25 ? 4 : 3)) lut16_scan_hits_kernel
           uint32_t pk[8];
 #pragma unroll
           for (int k = 0; k < 8; ++k)
-            pk[k] = (uint32_t(acc[0][2 * k]) & 0xFFFFu) | (uint32_t(acc[0][2 * k + 1]) << 16);
+            pk[k] = (uint32_t(acc[2 * k]) & 0xFFFFu) | (uint32_t(acc[2 * k + 1]) << 16);
           hsum[wave][slot][0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
           hsum[wave][slot][1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
           hmeta[wave][slot] = (j << 6) | uint32_t(lane);
@@ -1235,14 +866,20 @@ __global__ void __launch_bounds__(256, (K <= 25 ? 4 : 3)) lut16_scan_hits_kernel
       }
     };
 
-    uint32_t codes[NW], next[NW];
+    // tiles j, j+4, ... of the chunk; the prefetch of tile j+4 is
+    // unconditional (clamped to the chunk's last tile) so no exec branch
+    // sits around the load and the wait before the next tile is counted
     uint32_t j = j0 + wave;
-    if (j < jend) LoadCodes<K>(tb + size_t(j) * 64 * W, codes);
-    for (; j < jend; j += NWV) {
-      if (j + NWV < jend) LoadCodes<K>(tb + size_t(j + NWV) * 64 * W, next);
-      body(codes, j);
+    if (j < jend) {
+      uint32_t codes[NW], next[NW];
+      const uint32_t jl = jend - 1;
+      LoadCodes<K>(tb + size_t(j) * 64 * W, codes);
+      for (; j < jend; j += NWV) {
+        LoadCodes<K>(tb + size_t(min(j + NWV, jl)) * 64 * W, next);
+        body(codes, j);
 #pragma unroll
-      for (int i = 0; i < NW; ++i) codes[i] = next[i];
+        for (int i = 0; i < NW; ++i) codes[i] = next[i];
+      }
     }
     drain();
     __syncthreads();
@@ -1930,7 +1567,8 @@ hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq, i
   return hipGetLastError();
 }
 
-hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf, const float* topl_dist,
+hipError_t LaunchPairs(const DeviceIndex& ix, const uint32_t* order, const int32_t* topl_leaf,
+                       const float* topl_dist,
                        int nq, int L, uint32_t* cnt, uint32_t* block_cnt, uint32_t* pair_off,
                        uint32_t* tile_prefix, uint32_t* pair_q, float* pair_bias, uint2* work,
                        uint32_t* totals, unsigned long long* code_bytes, uint32_t chunk_tiles,
@@ -1942,7 +1580,7 @@ hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf, const fl
   if (n > 0)
     hipLaunchKernelGGL(pairs_count_kernel, dim3(nblocks), dim3(256), lds, s, topl_leaf, n, ix.nl,
                        block_cnt, cnt);
-  hipLaunchKernelGGL(pairs_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, ix.leaf_order,
+  hipLaunchKernelGGL(pairs_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, order,
                      ix.leaf_size, ix.nl, ix.nb, chunk_tiles, queries_per_item, pair_off,
                      tile_prefix, totals, code_bytes);
   if (n > 0) {
@@ -1952,20 +1590,16 @@ hipError_t LaunchPairs(const DeviceIndex& ix, const int32_t* topl_leaf, const fl
                        topl_dist, n, L, ix.nl, pair_off, block_cnt, pair_q, pair_bias);
   }
   hipLaunchKernelGGL(pairs_work_kernel, dim3((ix.nl + 255) / 256), dim3(256), 0, s, tile_prefix,
-                     ix.leaf_order, ix.leaf_size, ix.nl, chunk_tiles, work);
+                     order, ix.leaf_size, ix.nl, chunk_tiles, work);
   return hipGetLastError();
 }
 
 #define SMX_SCAN_CASE(KV)                                                          \
   case KV:                                                                         \
-    if (variant == 0)                                                              \
-      hipLaunchKernelGGL((lut16_scan_hits_kernel<KV, 0>), dim3(grid), dim3(256), 0, s, a); \
-    else if (variant == 2)                                                         \
-      hipLaunchKernelGGL((lut16_scan_block_kernel<KV, 1, 4, 0>), dim3(grid), dim3(256), 0, s, a); \
-    else if (variant == 4)                                                         \
-      hipLaunchKernelGGL((lut16_scan_hits_kernel<KV, 4>), dim3(grid), dim3(256), 0, s, a); \
+    if (variant == 4)                                                              \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 4>), dim3(grid), dim3(256), 0, s, a); \
     else                                                                           \
-      hipLaunchKernelGGL(lut16_scan_kernel<KV>, dim3(grid), dim3(256), 0, s, a);   \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(256), 0, s, a); \
     break;
 
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,

@@ -120,9 +120,8 @@ struct smx_index {
   uint32_t cap_per_query = 4096;   // candidate list capacity
   int seed_leaves = 4;
   int scan_variant = 0;            // see smx::LaunchScan
-  uint32_t chunk_tiles[5] = {32, 32, 32, 32, 32};
-  int grid = 0;                    // wave-variant scan grid (blocks of 4 waves)
-  int grid_block = 0;              // block-variant scan grid
+  uint32_t chunk_tiles = 32;       // tiles per work item
+  int grid = 0;                    // scan grid: 4 blocks of 4 waves per CU (LDS-limited)
   bool profiling = false;
   smx_timings timings{};
   hipEvent_t ev[16] = {};
@@ -378,13 +377,10 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   Mark(h, 1, s);
   SMX_HIP(smx::LaunchLutBuild(ix, queries, nq, w.lut, w.mult, w.inv, nullptr, s));
   Mark(h, 2, s);
-  // the per-lane-slot block scan stages 16-bit local datapoint numbers:
-  // larger leaves use the default scan
-  const int variant = (ix.max_leaf > 65535u && h->scan_variant == 2) ? 0 : h->scan_variant;
-  SMX_HIP(smx::LaunchPairs(ix, w.topl_leaf, w.topl_dist, nq, L, cnt, w.block_cnt, w.pair_off,
-                           w.tile_prefix, w.pair_q, w.pair_bias, w.work, stats + 3, code_bytes,
-                           h->chunk_tiles[variant], 32u,
-                           s));
+  const int variant = h->scan_variant;
+  SMX_HIP(smx::LaunchPairs(ix, ix.leaf_order, w.topl_leaf, w.topl_dist, nq, L, cnt, w.block_cnt,
+                           w.pair_off, w.tile_prefix, w.pair_q, w.pair_bias, w.work, stats + 3,
+                           code_bytes, h->chunk_tiles, 32u, s));
   Mark(h, 3, s);
   smx::SeedArgs sa{};
   sa.topl_leaf = w.topl_leaf;
@@ -422,7 +418,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   a.cand_count = w.cand_count;
   a.work_counter = work;
   a.cap = w.cap;
-  a.chunk_tiles = h->chunk_tiles[variant];
+  a.chunk_tiles = h->chunk_tiles;
   a.nl = nl;
   a.nb = ix.nb;
   a.shift = ix.shift;
@@ -459,7 +455,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   int retries = 0;
   uint32_t st[10] = {0};
   for (;;) {
-    SMX_HIP(smx::LaunchScan(ix, a, variant == 1 ? h->grid : h->grid_block, variant, s));
+    SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s));
     Mark(h, 6, s);
     SMX_HIP(smx::LaunchFinalSelect(sel, nq, s));
     Mark(h, 7, s);
@@ -565,7 +561,6 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
   hipDeviceProp_t prop;
   SMX_HIP(hipGetDeviceProperties(&prop, device));
   h->grid = prop.multiProcessorCount * 4;
-  h->grid_block = prop.multiProcessorCount * 4;
   *out = h;
   return SMX_OK;
 }
@@ -859,8 +854,8 @@ int smx_get_timings(const smx_index* h, smx_timings* out) {
 int smx_set_tuning(smx_index* h, int32_t candidates_per_query, int32_t seed_leaves,
                    int32_t scan_variant, int32_t chunk_tiles) {
   if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
-  if (scan_variant < 0 || scan_variant > 4 || scan_variant == 3)
-    return Fail(SMX_INVALID_ARGUMENT, "scan_variant is 0, 1, 2 or 4");
+  if (scan_variant != 0 && scan_variant != 4)
+    return Fail(SMX_INVALID_ARGUMENT, "scan_variant is 0 (scan) or 4 (timing ablation)");
   if (chunk_tiles != 0 && (chunk_tiles < 16 || chunk_tiles > 65535))
     return Fail(SMX_INVALID_ARGUMENT, "chunk_tiles must be 0 (default) or in [16, 65535]");
   if (candidates_per_query < 32 || candidates_per_query > 16384)
@@ -870,7 +865,7 @@ int smx_set_tuning(smx_index* h, int32_t candidates_per_query, int32_t seed_leav
   h->cap_per_query = uint32_t(candidates_per_query);
   h->seed_leaves = seed_leaves;
   h->scan_variant = scan_variant;
-  if (chunk_tiles) h->chunk_tiles[scan_variant] = uint32_t(chunk_tiles);
+  if (chunk_tiles) h->chunk_tiles = uint32_t(chunk_tiles);
   return SMX_OK;
 }
 

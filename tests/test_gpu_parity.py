@@ -110,12 +110,12 @@ def test_exact_distances_bit_exact(native, oracle, small_dot):
             assert np.float32(want).view(np.uint32) == got[i, j].view(np.uint32)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
-def test_overflow_tightening_is_exact(native, oracle, small_dot, variant):
+@pytest.mark.parametrize("chunk", [16, 32])
+def test_overflow_tightening_is_exact(native, oracle, small_dot, chunk):
     """A tiny candidate capacity forces the tightening loop; results unchanged."""
     ix, db, q = small_dot
     n = _nat(native, ix)
-    n.set_tuning(128, 0, variant)   # no seed pass: every candidate is emitted -> overflow
+    n.set_tuning(128, 0, 0, chunk)   # no seed pass: every candidate is emitted -> overflow
     n.set_profiling(True)
     gi, gd, gc = n.search_pre_reorder(q, 48, 100)
     t = n.timings()
@@ -191,12 +191,12 @@ def test_errors_surface_as_status(native, small_dot):
         n.search_batched(bad, 4, 10, 10)
 
 
-@pytest.mark.parametrize("variant,chunk", [(0, 16), (0, 64), (1, 16), (1, 32), (2, 16), (2, 32)])
-def test_scan_variants_match_oracle(native, oracle, small_l2, variant, chunk):
-    """Both scan kernels (block items / wave items) at several item sizes."""
+@pytest.mark.parametrize("chunk", [16, 32, 64, 200])
+def test_scan_chunks_match_oracle(native, oracle, small_l2, chunk):
+    """The scan at several work-item sizes (tiles per item)."""
     ix, db, q = small_l2
     n = _nat(native, ix)
-    n.set_tuning(4096, 2, variant, chunk)
+    n.set_tuning(4096, 2, 0, chunk)
     gi, gd, gc = n.search_pre_reorder(q, 12, 60)
     oi, od, oc = oracle.search_pre_reorder(ix, q, 12, 60, oracle.MODE_IDEAL)
     np.testing.assert_array_equal(gc, oc)

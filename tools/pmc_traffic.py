@@ -14,7 +14,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "lut16_scan_hits_kernel"
+KERNEL = "lut16_scan_kernel"
 
 
 def kernel_sha():
