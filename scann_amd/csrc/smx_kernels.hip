@@ -544,50 +544,87 @@ __device__ __forceinline__ void LoadCodes(const uint8_t* p, uint32_t* codes) {
 }
 
 // ---------------------------------------------------------------------------
-// Per-query threshold from the query's first `seed` leaves: every datapoint
-// there is scored with the int8 LUT held in LDS, and the k'-th smallest
-// distance (radix select over the order-preserving bits) bounds the final
-// k'-th from above.  The main pass rescans those leaves, so storing only the
-// first kSeedCap values is still correct (a subset's k'-th is a bound).
+// Per-query threshold from the query's first `seed` leaves (one block per
+// query).  Every datapoint there is scored with the int8 LUT in LDS; the
+// exact k'-th smallest of those distances bounds the final k'-th from above
+// (the main pass rescans those leaves and every stored key is a genuine
+// candidate), so the threshold key admits every datapoint at that distance.
+// The seed datapoints are numbered across the seed leaves (a wave prefix sum
+// of their sizes), thread t scores numbers t, t+256, ... into registers (at
+// most kSeedCap per query: a subset's k'-th is still a bound), and rounds of
+// a 256-bin histogram over the order-preserving bits narrow down to the
+// exact k'-th value.
 // ---------------------------------------------------------------------------
-constexpr int kSeedCap = 8192;
-constexpr uint32_t kSeedBins = 2048;
+constexpr int kSeedPerThread = 32;
+constexpr uint32_t kSeedCap = 256u * kSeedPerThread;
+constexpr int kSeedMaxLeaves = 64;   // one wave of leaf slots
+
+// Inclusive block scan of one value per thread (256 threads).
+__device__ __forceinline__ uint32_t BlockInclusiveScan256(uint32_t v, uint32_t* wsum) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = uint32_t(__shfl_up(int(v), off));
+    if (lane >= off) v += t;
+  }
+  if (lane == 63) wsum[wid] = v;
+  __syncthreads();
+  for (int w = 0; w < wid; ++w) v += wsum[w];
+  return v;
+}
 
 template <int K>
 __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
   constexpr int W = 4 * NW;
+  constexpr int U = 4;   // datapoints whose code loads are in flight together
   __shared__ int8_t lut[2 * K * 16];
-  __shared__ uint32_t vals[kSeedCap];
-  __shared__ uint32_t hist[kSeedBins];
-  __shared__ uint32_t binmax[kSeedBins];
-  __shared__ uint32_t scan_buf[256];
-  const int qi = blockIdx.x;
-  for (int e = threadIdx.x; e < 2 * K * 16; e += blockDim.x)
-    lut[e] = a.lut[size_t(qi) * 2 * K * 16 + e];
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t s_start[kSeedMaxLeaves + 1];
+  __shared__ uint64_t s_tile0[kSeedMaxLeaves];
+  __shared__ float s_bias[kSeedMaxLeaves];
+  __shared__ uint32_t wsum[4], s_lo[4], s_hi[4], s_bin, s_below;
+  const int qi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int e = tid; e < 2 * K * 16; e += 256) lut[e] = a.lut[size_t(qi) * 2 * K * 16 + e];
   const float inv = a.inv[qi];
+  const int nseed = min(a.seed, min(a.L, kSeedMaxLeaves));
+  if (wid == 0) {
+    // seed leaves and the exclusive prefix of their sizes (lanes >= nseed add 0)
+    const int leaf = lane < nseed ? a.topl_leaf[size_t(qi) * a.L + lane] : -1;
+    const uint32_t sz = leaf >= 0 ? a.leaf_size[leaf] : 0u;
+    uint32_t inc = sz;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t t = uint32_t(__shfl_up(int(inc), off));
+      if (lane >= off) inc += t;
+    }
+    s_start[lane] = inc - sz;
+    s_tile0[lane] = leaf >= 0 ? a.tile_off[leaf] : 0ull;
+    s_bias[lane] = (leaf >= 0 && a.residual) ? a.topl_dist[size_t(qi) * a.L + lane] : 0.0f;
+    if (lane == 63) s_start[kSeedMaxLeaves] = inc;
+  }
   __syncthreads();
-  uint32_t base = 0;
-  for (int r = 0; r < a.seed && base < uint32_t(kSeedCap); ++r) {
-    const int leaf = a.topl_leaf[size_t(qi) * a.L + r];
-    if (leaf < 0) break;
-    const float bias = a.residual ? a.topl_dist[size_t(qi) * a.L + r] : 0.0f;
-    const uint32_t n = min(a.leaf_size[leaf], uint32_t(kSeedCap) - base);
-    const uint8_t* tb = a.tiles + a.tile_off[leaf] * 64ull * W;
-    // 4 datapoints per thread per round, all code loads issued first
-    constexpr int U = 4;
-    for (uint32_t d0 = threadIdx.x; d0 < n; d0 += U * blockDim.x) {
+  const uint32_t total = min(s_start[kSeedMaxLeaves], kSeedCap);
+  const uint32_t kk = uint32_t(a.kk);
+  if (kk == 0 || total < kk) return;   // no bound: the threshold stays open
+
+  uint32_t vals[kSeedPerThread];
+  int r = 0;   // seed leaf of this thread's current number (numbers only grow)
+#pragma unroll
+  for (int i0 = 0; i0 < kSeedPerThread; i0 += U) {
+    if (uint32_t(i0) * 256u < total) {   // block-uniform
       uint32_t c0[U][NW], c1[U][NW];
+      int ru[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t dp = min(d0 + u * blockDim.x, n - 1);
-        const uint8_t* t0 = tb + ((dp >> 5) * 64 + (dp & 31)) * W;
+        const uint32_t g = min(uint32_t(tid) + 256u * uint32_t(i0 + u), total - 1);
+        while (g >= s_start[r + 1]) ++r;
+        ru[u] = r;
+        const uint32_t dp = g - s_start[r];
+        const uint8_t* t0 = a.tiles + ((s_tile0[r] + (dp >> 5)) * 64 + (dp & 31)) * W;
         LoadCodes<K>(t0, c0[u]);
         LoadCodes<K>(t0 + 32 * W, c1[u]);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t dp = d0 + u * blockDim.x;
         int acc = 0;
 #pragma unroll
         for (int s = 0; s < K; ++s) {
@@ -595,66 +632,60 @@ __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
           const uint32_t n1 = (c1[u][s >> 3] >> ((s & 7) * 4)) & 15u;
           acc += int(lut[(2 * s) * 16 + n0]) + int(lut[(2 * s + 1) * 16 + n1]);
         }
-        if (dp < n) vals[base + dp] = OrderedBits(DistOf(acc, inv, bias));
+        const uint32_t g = uint32_t(tid) + 256u * uint32_t(i0 + u);
+        vals[i0 + u] = g < total ? OrderedBits(DistOf(acc, inv, s_bias[ru[u]])) : 0xFFFFFFFFu;
       }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) vals[i0 + u] = 0xFFFFFFFFu;   // no datapoint
     }
-    base += n;
   }
-  __syncthreads();
-  const uint32_t total = base;
-  const uint32_t kk = uint32_t(a.kk);
-  if (kk == 0 || total < kk) return;  // no bound: the threshold stays open
-  // Any value >= the kk-th smallest is a valid threshold.  Bin the values
-  // linearly between their min and max (order-preserving bits), find the bin
-  // holding the kk-th smallest and take the largest value in it.
+  // range of the values, then histogram rounds down to the kk-th value
   uint32_t lo = 0xFFFFFFFFu, hi = 0;
-  for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) {
-    lo = min(lo, vals[i]);
-    hi = max(hi, vals[i]);
-  }
+#pragma unroll
+  for (int i = 0; i < kSeedPerThread; ++i)
+    if (vals[i] != 0xFFFFFFFFu) {
+      lo = min(lo, vals[i]);
+      hi = max(hi, vals[i]);
+    }
   for (int off = 32; off > 0; off >>= 1) {
-    lo = min(lo, __shfl_xor(lo, off));
-    hi = max(hi, __shfl_xor(hi, off));
+    lo = min(lo, uint32_t(__shfl_xor(int(lo), off)));
+    hi = max(hi, uint32_t(__shfl_xor(int(hi), off)));
   }
-  __shared__ uint32_t s_lo[4], s_hi[4];
-  const int wid = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { s_lo[wid] = lo; s_hi[wid] = hi; }
-  for (uint32_t b = threadIdx.x; b < kSeedBins; b += blockDim.x) { hist[b] = 0; binmax[b] = 0; }
+  if (lane == 0) { s_lo[wid] = lo; s_hi[wid] = hi; }
   __syncthreads();
   lo = min(min(s_lo[0], s_lo[1]), min(s_lo[2], s_lo[3]));
   hi = max(max(s_hi[0], s_hi[1]), max(s_hi[2], s_hi[3]));
-  const uint64_t span = uint64_t(hi - lo) + 1;
-  for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) {
-    const uint32_t v = vals[i];
-    const uint32_t b = uint32_t((uint64_t(v - lo) * kSeedBins) / span);
-    atomicAdd(&hist[b], 1u);
-    atomicMax(&binmax[b], v);
-  }
-  __syncthreads();
-  // Block prefix over the bins: thread t owns kSeedBins / 256 consecutive bins.
-  constexpr uint32_t per = kSeedBins / 256;
-  uint32_t local = 0;
-  for (uint32_t u = 0; u < per; ++u) local += hist[threadIdx.x * per + u];
-  scan_buf[threadIdx.x] = local;
-  __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {
-    const uint32_t v = int(threadIdx.x) >= off ? scan_buf[threadIdx.x - off] : 0u;
+  uint32_t below = 0;   // values smaller than lo
+  while (lo < hi) {     // block-uniform; each round shrinks [lo, hi] 256-fold
+    const uint64_t span = uint64_t(hi - lo) + 1;
+    hist[tid] = 0;
     __syncthreads();
-    scan_buf[threadIdx.x] += v;
-    __syncthreads();
-  }
-  const uint32_t before = threadIdx.x ? scan_buf[threadIdx.x - 1] : 0u;
-  if (before < kk && before + local >= kk) {
-    uint32_t cum = before;
-    for (uint32_t u = 0; u < per; ++u) {
-      const uint32_t b = threadIdx.x * per + u;
-      cum += hist[b];
-      if (cum >= kk) {
-        const uint64_t t = (uint64_t(binmax[b]) << 32) | 0xFFFFFFFFull;
-        if (t < a.tau_key[qi]) a.tau_key[qi] = t;
-        break;
-      }
+#pragma unroll
+    for (int i = 0; i < kSeedPerThread; ++i) {
+      const uint32_t v = vals[i];
+      if (v >= lo && v <= hi) atomicAdd(&hist[uint32_t((uint64_t(v - lo) * 256u) / span)], 1u);
     }
+    __syncthreads();
+    const uint32_t hv = hist[tid];
+    const uint32_t inc = BlockInclusiveScan256(hv, wsum);
+    if (below + inc - hv < kk && below + inc >= kk) {
+      s_bin = uint32_t(tid);
+      s_below = below + inc - hv;
+    }
+    __syncthreads();
+    const uint32_t b = s_bin;
+    below = s_below;
+    // values of bin b: [lo + ceil(b*span/256), lo + ceil((b+1)*span/256) - 1]
+    const uint32_t blo = lo + uint32_t((uint64_t(b) * span + 255u) / 256u);
+    const uint32_t bhi = lo + uint32_t((uint64_t(b + 1) * span + 255u) / 256u) - 1u;
+    lo = blo;
+    hi = bhi;
+    __syncthreads();   // hist, wsum and s_bin are rewritten by the next round
+  }
+  if (tid == 0) {
+    const uint64_t t = (uint64_t(hi) << 32) | 0xFFFFFFFFull;
+    if (t < a.tau_key[qi]) a.tau_key[qi] = t;
   }
 }
 
@@ -1129,19 +1160,6 @@ __global__ void __launch_bounds__(256) final_select_kernel(SelectArgs a) {
 // ---------------------------------------------------------------------------
 constexpr int kSelMax = 256;
 constexpr int kFsBins = 256;
-
-// Inclusive block scan of one value per thread (256 threads).
-__device__ __forceinline__ uint32_t BlockInclusiveScan256(uint32_t v, uint32_t* wsum) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t t = uint32_t(__shfl_up(int(v), off));
-    if (lane >= off) v += t;
-  }
-  if (lane == 63) wsum[wid] = v;
-  __syncthreads();
-  for (int w = 0; w < wid; ++w) v += wsum[w];
-  return v;
-}
 
 // Exact distances of m candidates (rows + rowid[i] * dim) into dist[], 8
 // lanes per candidate: lane l of a group owns accumulator l of the A.8 layout

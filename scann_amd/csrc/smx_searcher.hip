@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -74,6 +75,7 @@ int EffectiveKSteps(int nb) {
 
 struct Workspace {
   int nq = 0, L = 0, kk = 0, dim = 0, width = 0;
+  uint64_t gen = 0;                 // bumped on every (re)allocation
   uint32_t cap = 0, max_items = 0;
   float* queries = nullptr;
   int32_t* topl_leaf = nullptr;
@@ -123,11 +125,18 @@ struct smx_index {
   uint32_t chunk_tiles = 32;       // tiles per work item
   int grid = 0;                    // scan grid: 4 blocks of 4 waves per CU (LDS-limited)
   bool profiling = false;
+  bool use_graph = true;           // replay the first pass as a hipGraph
+  hipGraphExec_t graph_exec = nullptr;
+  uint64_t graph_key[12] = {};
+  uint64_t ws_generation = 0;
+  uint32_t* host_stats = nullptr;  // pinned copy of the stats words
   smx_timings timings{};
   hipEvent_t ev[16] = {};
 };
 
 namespace {
+
+constexpr int GraphKeyWords = 12;
 
 int UploadIndex(const smx_index_desc* d, smx_index* h) {
   smx::DeviceIndex& ix = h->ix;
@@ -325,6 +334,7 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
     return rc;
   }
   w.nq = nq; w.L = L; w.kk = kk; w.width = width; w.dim = ix.dim;
+  w.gen = ++h->ws_generation;
   w.cap = cap; w.max_items = max_items;
   return SMX_OK;
 }
@@ -369,19 +379,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   unsigned long long* code_bytes = reinterpret_cast<unsigned long long*>(stats + 6);
   const int seed = std::min(h->seed_leaves, L);
 
-  Mark(h, 0, s);
-  SMX_HIP(hipMemsetAsync(w.counters, 0, sizeof(uint32_t) * (2 * nl + 20), s));
-  SMX_HIP(hipMemsetAsync(w.cand_count, 0, sizeof(uint32_t) * nq, s));
-  SMX_HIP(smx::LaunchFill64(w.tau, smx::kNoThreshold, nq, s));
-  SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s));
-  Mark(h, 1, s);
-  SMX_HIP(smx::LaunchLutBuild(ix, queries, nq, w.lut, w.mult, w.inv, nullptr, s));
-  Mark(h, 2, s);
   const int variant = h->scan_variant;
-  SMX_HIP(smx::LaunchPairs(ix, ix.leaf_order, w.topl_leaf, w.topl_dist, nq, L, cnt, w.block_cnt,
-                           w.pair_off, w.tile_prefix, w.pair_q, w.pair_bias, w.work, stats + 3,
-                           code_bytes, h->chunk_tiles, 32u, s));
-  Mark(h, 3, s);
   smx::SeedArgs sa{};
   sa.topl_leaf = w.topl_leaf;
   sa.topl_dist = w.topl_dist;
@@ -395,9 +393,6 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sa.seed = seed;
   sa.kk = kk;
   sa.residual = ix.residual;
-  SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
-  Mark(h, 4, s);
-  Mark(h, 5, s);
 
   smx::ScanArgs a{};
   a.tiles = ix.tiles;
@@ -452,15 +447,71 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sel.row_base = ix.row_base;
   sel.member_rows = ix.member_rows;
 
-  int retries = 0;
-  uint32_t st[10] = {0};
-  for (;;) {
+  // First pass: everything up to the stats copy.  Replayed as a captured
+  // hipGraph when the call shape, buffers and stream repeat (one launch
+  // instead of ~20, no per-kernel host overhead); eager otherwise.
+  auto first_pass = [&]() -> int {
+    Mark(h, 0, s);
+    SMX_HIP(hipMemsetAsync(w.counters, 0, sizeof(uint32_t) * (2 * nl + 20), s));
+    SMX_HIP(hipMemsetAsync(w.cand_count, 0, sizeof(uint32_t) * nq, s));
+    SMX_HIP(smx::LaunchFill64(w.tau, smx::kNoThreshold, nq, s));
+    SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s));
+    Mark(h, 1, s);
+    SMX_HIP(smx::LaunchLutBuild(ix, queries, nq, w.lut, w.mult, w.inv, nullptr, s));
+    Mark(h, 2, s);
+    SMX_HIP(smx::LaunchPairs(ix, ix.leaf_order, w.topl_leaf, w.topl_dist, nq, L, cnt, w.block_cnt,
+                             w.pair_off, w.tile_prefix, w.pair_q, w.pair_bias, w.work, stats + 3,
+                             code_bytes, h->chunk_tiles, 32u, s));
+    Mark(h, 3, s);
+    SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
+    Mark(h, 4, s);
+    Mark(h, 5, s);
     SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s));
     Mark(h, 6, s);
     SMX_HIP(smx::LaunchFinalSelect(sel, nq, s));
     Mark(h, 7, s);
-    SMX_HIP(hipMemcpyAsync(st, stats, sizeof(st), hipMemcpyDeviceToHost, s));
-    SMX_HIP(hipStreamSynchronize(s));
+    SMX_HIP(hipMemcpyAsync(h->host_stats, stats, 10 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    return SMX_OK;
+  };
+  bool ran = false;
+  // (profiled calls run eagerly: HIP events recorded inside a captured graph
+  // carry no timestamps)
+  if (h->use_graph && !h->profiling && s) {
+    const uint64_t key[GraphKeyWords] = {
+        uint64_t(reinterpret_cast<uintptr_t>(queries)), uint64_t(nq), uint64_t(L), uint64_t(pnn),
+        uint64_t(final_nn), uint64_t(reorder) | uint64_t(pre_only) << 1 | uint64_t(h->profiling) << 2,
+        uint64_t(reinterpret_cast<uintptr_t>(out_idx)), uint64_t(reinterpret_cast<uintptr_t>(out_dist)),
+        uint64_t(reinterpret_cast<uintptr_t>(out_count)), uint64_t(reinterpret_cast<uintptr_t>(shard_out)),
+        uint64_t(reinterpret_cast<uintptr_t>(s)),
+        w.gen ^ (uint64_t(w.cap) << 20) ^ (uint64_t(seed) << 40) ^ (uint64_t(h->chunk_tiles) << 48) ^
+            (uint64_t(variant) << 60)};
+    if (!h->graph_exec || std::memcmp(key, h->graph_key, sizeof(key)) != 0) {
+      if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
+      h->graph_exec = nullptr;
+      if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+        const int prc = first_pass();
+        hipGraph_t g = nullptr;
+        const hipError_t e = hipStreamEndCapture(s, &g);
+        if (prc == SMX_OK && e == hipSuccess && g &&
+            hipGraphInstantiate(&h->graph_exec, g, nullptr, nullptr, 0) == hipSuccess)
+          std::memcpy(h->graph_key, key, sizeof(key));
+        else
+          h->graph_exec = nullptr;   // capture unsupported here: run eagerly
+        if (g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+      }
+    }
+    if (h->graph_exec) {
+      SMX_HIP(hipGraphLaunch(h->graph_exec, s));
+      ran = true;
+    }
+  }
+  if (!ran && (rc = first_pass())) return rc;
+  SMX_HIP(hipStreamSynchronize(s));
+  int retries = 0;
+  uint32_t st[10];
+  std::memcpy(st, h->host_stats, sizeof(st));
+  for (;;) {
     if (!st[0]) {
       if (st[9]) {  // queries the wave final select could not narrow
         smx::SelectArgs fb = sel;
@@ -470,12 +521,20 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
       }
       break;
     }
+    // a candidate list overflowed: tighten the thresholds and rescan
     if (++retries > 64) return Fail(SMX_INTERNAL, "candidate tightening did not converge");
     SMX_HIP(smx::LaunchTighten(w.cand, w.cand_count, w.cap, nq, kk, w.tau, s));
     SMX_HIP(hipMemsetAsync(w.cand_count, 0, sizeof(uint32_t) * nq, s));
     SMX_HIP(hipMemsetAsync(stats, 0, sizeof(uint32_t) * 3, s));
     SMX_HIP(hipMemsetAsync(stats + 8, 0, 2 * sizeof(uint32_t), s));
     SMX_HIP(hipMemsetAsync(work, 0, sizeof(uint32_t), s));
+    SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s));
+    Mark(h, 6, s);
+    SMX_HIP(smx::LaunchFinalSelect(sel, nq, s));
+    Mark(h, 7, s);
+    SMX_HIP(hipMemcpyAsync(h->host_stats, stats, sizeof(st), hipMemcpyDeviceToHost, s));
+    SMX_HIP(hipStreamSynchronize(s));
+    std::memcpy(st, h->host_stats, sizeof(st));
   }
   smx_timings& t = h->timings;
   if (h->profiling) {
@@ -561,6 +620,12 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
   hipDeviceProp_t prop;
   SMX_HIP(hipGetDeviceProperties(&prop, device));
   h->grid = prop.multiProcessorCount * 4;
+  if (hipHostMalloc(reinterpret_cast<void**>(&h->host_stats), 16 * sizeof(uint32_t)) != hipSuccess) {
+    smx_index_destroy(h);
+    return Fail(SMX_OUT_OF_MEMORY, "hipHostMalloc failed");
+  }
+  const char* ng = std::getenv("SMX_NO_GRAPH");
+  h->use_graph = !(ng && ng[0] == '1');
   *out = h;
   return SMX_OK;
 }
@@ -569,6 +634,8 @@ int smx_index_destroy(smx_index* h) {
   if (!h) return SMX_OK;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
+  if (h->host_stats) (void)hipHostFree(h->host_stats);
   h->ws.Release();
   FreeIndex(h->ix);
   for (auto& e : h->ev)

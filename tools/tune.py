@@ -35,12 +35,24 @@ def main():
             if i >= 2:
                 for k, v in t.items():
                     acc[k] = acc.get(k, 0.0) + float(v) / steps
+        nat.set_profiling(False)
+        for _ in range(3):
+            nat.search_batched_device(qd.data_ptr(), NQ, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True,
+                                      oi.data_ptr(), od.data_ptr(), None)
+        torch.cuda.synchronize()
+        tw = time.perf_counter()
+        for _ in range(50):
+            nat.search_batched_device(qd.data_ptr(), NQ, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True,
+                                      oi.data_ptr(), od.data_ptr(), None)
+        torch.cuda.synchronize()
+        wall_ms = (time.perf_counter() - tw) * 1000.0 / 50
+        nat.set_profiling(True)
         mfma_tops = acc["scan_item_tiles"] * 25 * 65536 / (acc["scan_ms"] * 1e-3) / 1e12
         print(f"var={variant} chunk={chunk:3d} cap={cap:5d} seed={seed:2d} total={acc['total_ms']:.3f} part={acc['partition_ms']:.3f} "
               f"lut={acc['lut_ms']:.3f} inv={acc['invert_ms']:.3f} seed={acc['seed_scan_ms']:.3f} "
               f"scan={acc['scan_ms']:.3f} sel={acc['select_ms']:.3f} retries={acc['overflow_retries']:.1f} "
               f"cand_mean={acc['mean_candidates']:.0f} cand_max={acc['max_candidates']:.0f} "
-              f"item_tiles={acc['scan_item_tiles']:.0f} mfma={mfma_tops:.0f}TOPS", flush=True)
+              f"item_tiles={acc['scan_item_tiles']:.0f} mfma={mfma_tops:.0f}TOPS wall={wall_ms:.3f}ms", flush=True)
 
 
 if __name__ == "__main__":
