@@ -126,7 +126,12 @@ _DISTANCES = {"DotProductDistance": "dot_product", "SquaredL2Distance": "squared
 
 
 def search_config_from_text(text: str) -> SearchConfig:
-    tree = parse_text_proto(text)
+    return search_config_from_tree(parse_text_proto(text))
+
+
+def search_config_from_tree(tree: Dict[str, List[Any]]) -> SearchConfig:
+    """SearchConfig of a parsed config: a text proto (parse_text_proto) or a
+    binary scann_config.pb decoded by scann_amd.assets."""
     nn = _get(tree, "num_neighbors")
     if nn is None:
         raise ValueError("config has no num_neighbors")

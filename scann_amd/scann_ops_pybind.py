@@ -115,15 +115,41 @@ def create_searcher(db, scann_config, training_threads=0, docids=None, **kwargs)
 
 
 def load_searcher(artifacts_dir, assets_backcompat_shim=True, device=0):
-    """Loads searcher assets from artifacts_dir and returns a ScaNN searcher."""
-    del assets_backcompat_shim
+    """Loads searcher assets from artifacts_dir and returns a ScaNN searcher
+    (scann_ops_pybind.py:250-270 of the reference).  Without a
+    scann_assets.pbtxt the backcompat shim lists the asset files present
+    (scann_ops_pybind_backcompat.py:30-70) and writes that list."""
     if not os.path.isdir(artifacts_dir):
         raise ValueError(f"{artifacts_dir} is not a directory.")
-    if not os.path.exists(os.path.join(artifacts_dir, "scann_assets.pbtxt")):
-        raise ValueError("No scann_assets.pbtxt found.")
+    assets_pbtxt = os.path.join(artifacts_dir, "scann_assets.pbtxt")
+    if not os.path.exists(assets_pbtxt):
+        if not assets_backcompat_shim:
+            raise ValueError("No scann_assets.pbtxt found.")
+        _populate_and_save_assets_proto(artifacts_dir)
     docids = None
     p = os.path.join(artifacts_dir, "scann_docids.json")
     if os.path.isfile(p):
         with open(p) as f:
             docids = json.load(f)
-    return ScannSearcher(ScannNumpy(artifacts_dir, "", device=device), docids)
+    elif os.path.isfile(os.path.join(artifacts_dir, "scann_docids.pkl")):
+        # loading a pickle executes code from the file; never done here
+        raise ValueError("scann_docids.pkl is a pickle and is not loaded; "
+                         "convert the docids to scann_docids.json (a JSON list)")
+    with open(assets_pbtxt) as f:
+        return ScannSearcher(ScannNumpy(artifacts_dir, f.read(), device=device), docids)
+
+
+_BACKCOMPAT_ASSETS = (
+    ("ah_codebook.pb", "AH_CENTERS"), ("serialized_partitioner.pb", "PARTITIONER"),
+    ("datapoint_to_token.npy", "TOKENIZATION_NPY"), ("hashed_dataset.npy", "AH_DATASET_NPY"),
+    ("int8_dataset.npy", "INT8_DATASET_NPY"), ("int8_multipliers.npy", "INT8_MULTIPLIERS_NPY"),
+    ("dp_norms.npy", "INT8_NORMS_NPY"), ("dataset.npy", "DATASET_NPY"))
+
+
+def _populate_and_save_assets_proto(artifacts_dir):
+    from .assets import format_message
+    found = [{"asset_type": [kind], "asset_path": [os.path.join(artifacts_dir, name)]}
+             for name, kind in _BACKCOMPAT_ASSETS
+             if os.path.exists(os.path.join(artifacts_dir, name))]
+    with open(os.path.join(artifacts_dir, "scann_assets.pbtxt"), "w") as f:
+        f.write(format_message({"assets": found}, "ScannAssets"))

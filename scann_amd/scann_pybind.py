@@ -7,7 +7,12 @@ tree-AH LUT16 path:
 * ``ScannNumpy(db, config, training_threads)`` trains an index with
   scann_amd.index_builder and uploads it (scann_npy.cc:67-77);
 * ``ScannNumpy(artifacts_dir, assets_pbtxt)`` reloads a serialized searcher
-  (scann_npy.cc:57-65; this build's own asset format, see TreeAHIndex.save);
+  (scann_npy.cc:57-65) from the reference's artifacts layout
+  (scann_amd.assets; an empty ``assets_pbtxt`` reads the directory's
+  scann_assets.pbtxt, scann.cc:246-264), or from this build's earlier own
+  format (TreeAHIndex.save, recognised by its smx_index.json);
+* ``serialize`` writes the reference's layout (scann.cc:504-601,
+  scann_npy.cc:272-282);
 * ``search`` / ``search_batched`` keep the argument order, the -1 = "config
   default" convention (scann.cc:384-430), the float32 C-order cast, the
   2-D check, the (0, NaN) padding and the x(-1) of dot-product distances
@@ -21,7 +26,7 @@ from typing import Optional
 
 import numpy as np
 
-from . import _native
+from . import _native, assets
 from .config import SearchConfig, search_config_from_text
 from .index import METRIC_NAMES, TreeAHIndex
 
@@ -31,10 +36,14 @@ class ScannNumpy:
                  seed: int = 0):
         if isinstance(db_or_dir, str):
             directory = db_or_dir
-            with open(os.path.join(directory, "scann_config.pb")) as f:
-                config = f.read()
-            self._cfg = search_config_from_text(config)
-            index = TreeAHIndex.load(directory)
+            if os.path.exists(os.path.join(directory, "smx_index.json")):
+                with open(os.path.join(directory, "scann_config.pb")) as f:
+                    config = f.read()
+                self._cfg = search_config_from_text(config)
+                index = TreeAHIndex.load(directory)
+            else:
+                index, tree, self._cfg = assets.load_artifacts(directory, config or None)
+                config = assets.config_text(tree)
         else:
             self._cfg = search_config_from_text(config)
             db = np.ascontiguousarray(db_or_dir, dtype=np.float32)
@@ -98,13 +107,10 @@ class ScannNumpy:
         return self._run(q, final_nn, pre_reorder_nn, leaves)
 
     def serialize(self, path: str, relative_path: bool = False) -> None:
-        del relative_path
-        os.makedirs(path, exist_ok=True)
-        self._index.save(path)
-        with open(os.path.join(path, "scann_config.pb"), "w") as f:
-            f.write(self._config_text)
-        with open(os.path.join(path, "scann_assets.pbtxt"), "w") as f:
-            f.write('assets { asset_type: SMX_TREE_AH_INDEX asset_path: "smx_index.json" }\n')
+        try:
+            assets.save_artifacts(self._index, self._config_text, path, relative_path)
+        except (OSError, ValueError) as e:
+            raise RuntimeError(f"Failed to extract SingleMachineFactoryOptions: {e}") from None
 
     def config(self) -> str:
         return self._config_text

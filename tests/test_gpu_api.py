@@ -2,6 +2,8 @@
 path, mirroring the reference's own tests (scann_ops_pybind_test.py):
 search vs search_batched, batched vs parallel, serialization round trip,
 result shapes, and the recall of tree-AH + reorder against brute force."""
+import os
+
 import numpy as np
 import pytest
 
@@ -89,3 +91,22 @@ def test_soar_searcher(data):
         assert len(set(row.tolist())) == 10
     truth = synthetic.brute_force_topk(db, q, 10, 0)
     assert synthetic.recall_at_k(idx.astype(np.int64), truth, 10) > 0.9
+
+
+def test_soar_serialization_in_reference_layout(data, tmp_path):
+    """serialize -> load_searcher through the reference's artifacts layout
+    (scann.cc:504-601): SOAR 2N tokenization, the soar hashed dataset and a
+    relative-path assets file; results identical before and after."""
+    db, q = data
+    s = scann_ops_pybind.builder(db, 10, "dot_product").tree(
+        100, 20, soar_lambda=1.5, overretrieve_factor=2.0).score_ah(2).reorder(100).build()
+    s.serialize(str(tmp_path), relative_path=True)
+    names = set(os.listdir(tmp_path))
+    assert {"scann_config.pb", "scann_assets.pbtxt", "hashed_dataset_soar.npy",
+            "serialized_partitioner.pb", "ah_codebook.pb", "dataset.npy"} <= names
+    s2 = scann_ops_pybind.load_searcher(str(tmp_path))
+    a = s.search_batched(q[:64])
+    b = s2.search_batched(q[:64])
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    assert "INT8_LUT16" in s2.config()
