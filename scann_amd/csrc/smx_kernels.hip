@@ -247,6 +247,99 @@ __global__ void __launch_bounds__(256) topl_select_kernel(const float* __restric
   }
 }
 
+// Above this many leaves the score row is selected from global memory.
+constexpr int kLdsSelectLeaves = 16384;
+
+// Exact top-L per query when the score row does not fit in LDS (more than
+// kLdsSelectLeaves leaves, e.g. Deep1B's 50000): four 8-bit radix passes over
+// the row in global memory (L2-resident, nl*4 bytes) find the ordered bits T
+// of the L-th smallest score and how many of the L are ties at T; the keys
+// below T plus the lowest-index ties (the reference's (distance, index)
+// order) are compacted into LDS and bitonic-sorted.  Same output as
+// topl_select_kernel.  LDS: lcap = NextPow2(min(L, nl)) u64 keys.
+__global__ void __launch_bounds__(256) topl_select_global_kernel(const float* __restrict__ scores,
+                                                                 int nl, int L, uint32_t lcap,
+                                                                 int32_t* __restrict__ out_leaf,
+                                                                 float* __restrict__ out_dist) {
+  extern __shared__ uint64_t lds64[];
+  uint64_t* sel = lds64;
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t s_prefix, s_need, s_eq, s_cnt, s_tie;
+  __shared__ uint32_t s_wave[4];
+  const int qi = blockIdx.x;
+  const float* row = scores + size_t(qi) * nl;
+  const uint32_t m = min(uint32_t(L), uint32_t(nl));
+  if (threadIdx.x == 0) { s_prefix = 0; s_need = m; s_cnt = 0; s_tie = 0; }
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t prefix = s_prefix;
+    for (int c = threadIdx.x; c < nl; c += blockDim.x) {
+      const uint32_t v = OrderedBits(row[c]);
+      if (pass == 0 || (v >> (shift + 8)) == (prefix >> (shift + 8)))
+        atomicAdd(&hist[(v >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {   // wave 0: inclusive scan of 4 bins per lane
+      const int lane = threadIdx.x;
+      const uint32_t h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2],
+                     h3 = hist[4 * lane + 3];
+      uint32_t incl = h0 + h1 + h2 + h3;
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(incl, off);
+        if (lane >= off) incl += t;
+      }
+      const uint32_t excl = incl - (h0 + h1 + h2 + h3);
+      const uint32_t need = s_need;
+      if (excl < need && incl >= need) {
+        uint32_t cum = excl, b = 4 * lane;
+        const uint32_t h[4] = {h0, h1, h2, h3};
+        int u = 0;
+        while (cum + h[u] < need) { cum += h[u]; ++u; }
+        b += u;
+        s_prefix = prefix | (b << shift);
+        s_need = need - cum;   // rank of the L-th key among the keys in bin b
+        s_eq = h[u];
+      }
+    }
+    __syncthreads();
+  }
+  const uint32_t T = s_prefix, need = s_need, eq = s_eq;   // need ties at T of eq
+  const bool all_ties = need == eq;
+  for (int c = threadIdx.x; c < nl; c += blockDim.x) {
+    const uint32_t v = OrderedBits(row[c]);
+    if (v < T || (all_ties && v == T)) sel[atomicAdd(&s_cnt, 1u)] = (uint64_t(v) << 32) | uint32_t(c);
+  }
+  if (!all_ties) {   // only the `need` lowest-index ties: ordered chunk scan
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int base = 0; base < nl; base += blockDim.x) {
+      const int c = base + threadIdx.x;
+      const bool is_eq = c < nl && OrderedBits(row[c]) == T;
+      const uint64_t bal = __ballot(is_eq);
+      if (lane == 0) s_wave[wid] = uint32_t(__popcll(bal));
+      __syncthreads();
+      uint32_t before = s_tie;
+      for (int w = 0; w < wid; ++w) before += s_wave[w];
+      before += uint32_t(__popcll(bal & ((1ull << lane) - 1ull)));
+      if (is_eq && before < need) sel[atomicAdd(&s_cnt, 1u)] = (uint64_t(T) << 32) | uint32_t(c);
+      __syncthreads();
+      if (threadIdx.x == 0) s_tie += s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+      __syncthreads();
+      if (s_tie >= need) break;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = m + threadIdx.x; i < lcap; i += blockDim.x) sel[i] = ~0ull;
+  __syncthreads();
+  BitonicSort(sel, lcap);
+  for (int i = threadIdx.x; i < L; i += blockDim.x) {
+    const bool has = uint32_t(i) < m;
+    out_leaf[size_t(qi) * L + i] = has ? int32_t(sel[i] & 0xFFFFFFFFu) : -1;
+    out_dist[size_t(qi) * L + i] = has ? FromOrdered(uint32_t(sel[i] >> 32)) : __int_as_float(0x7fc00000);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // LUT build: raw[b][c] = -(fl(q0*c0) + fl(q1*c1)) (dot) or
 // fl(t0*t0) + fl(t1*t1), t = q - c (squared L2); multiplier
@@ -327,25 +420,29 @@ __device__ __forceinline__ uint32_t LeafChunks(uint32_t n, uint32_t chunk_tiles)
 // Block-local counting: every block histograms kPairsPerBlock pairs in LDS and
 // publishes one count per (block, leaf) -- no contended global atomics.
 constexpr int kPairsPerBlock = 4096;
+constexpr int kLeafRange = 16384;   // leaves per LDS counter range (64 KiB)
 
 __global__ void __launch_bounds__(256) pairs_count_kernel(const int32_t* __restrict__ topl_leaf,
                                                           int n, int nl,
                                                           uint32_t* __restrict__ block_cnt,
                                                           uint32_t* __restrict__ cnt) {
   extern __shared__ uint32_t hist[];
-  for (int l = threadIdx.x; l < nl; l += blockDim.x) hist[l] = 0;
+  // blockIdx.y selects a range of kLeafRange leaves (indexes whose per-leaf
+  // counters exceed LDS, e.g. 50000 leaves)
+  const int l0 = blockIdx.y * kLeafRange, nr = min(kLeafRange, nl - l0);
+  for (int l = threadIdx.x; l < nr; l += blockDim.x) hist[l] = 0;
   __syncthreads();
   const int beg = blockIdx.x * kPairsPerBlock, end = min(n, beg + kPairsPerBlock);
   for (int i = beg + threadIdx.x; i < end; i += blockDim.x) {
-    const int leaf = topl_leaf[i];
-    if (leaf >= 0) atomicAdd(&hist[leaf], 1u);
+    const int leaf = topl_leaf[i] - l0;
+    if (leaf >= 0 && leaf < nr) atomicAdd(&hist[leaf], 1u);
   }
   __syncthreads();
-  uint32_t* bc = block_cnt + size_t(blockIdx.x) * nl;
-  for (int l = threadIdx.x; l < nl; l += blockDim.x) {
+  uint32_t* bc = block_cnt + size_t(blockIdx.x) * nl + l0;
+  for (int l = threadIdx.x; l < nr; l += blockDim.x) {
     const uint32_t c = hist[l];
     bc[l] = c;
-    if (c) atomicAdd(&cnt[l], c);
+    if (c) atomicAdd(&cnt[l0 + l], c);
   }
 }
 
@@ -439,14 +536,15 @@ __global__ void __launch_bounds__(256) pairs_scatter_kernel(
     const uint32_t* __restrict__ pair_off, const uint32_t* __restrict__ block_off,
     uint32_t* __restrict__ pair_q, float* __restrict__ pair_bias) {
   extern __shared__ uint32_t fill[];
-  for (int l = threadIdx.x; l < nl; l += blockDim.x) fill[l] = 0;
+  const int l0 = blockIdx.y * kLeafRange, nr = min(kLeafRange, nl - l0);
+  for (int l = threadIdx.x; l < nr; l += blockDim.x) fill[l] = 0;
   __syncthreads();
   const uint32_t* bo = block_off + size_t(blockIdx.x) * nl;
   const int beg = blockIdx.x * kPairsPerBlock, end = min(n, beg + kPairsPerBlock);
   for (int i = beg + threadIdx.x; i < end; i += blockDim.x) {
     const int leaf = topl_leaf[i];
-    if (leaf < 0) continue;
-    const uint32_t pos = pair_off[leaf] + bo[leaf] + atomicAdd(&fill[leaf], 1u);
+    if (leaf < l0 || leaf >= l0 + nr) continue;
+    const uint32_t pos = pair_off[leaf] + bo[leaf] + atomicAdd(&fill[leaf - l0], 1u);
     pair_q[pos] = uint32_t(i / L);
     pair_bias[pos] = topl_dist[i];
   }
@@ -1569,11 +1667,18 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   while (lp2 < uint32_t(L)) lp2 <<= 1;
   const uint32_t selcap = std::max<uint32_t>(2048u, 2 * lp2);
   const size_t lds = size_t(kcap) * 8 + size_t(selcap) * 8 + (kSelBins + 256) * 4;
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(partition_scores_kernel, dim3((nq + 31) / 32, (ix.nl + 31) / 32), dim3(64), 0,
                      s, queries, nq, ix.dim, ix.centers, ix.cnorm, ix.nl, ix.metric, scores);
-  hipLaunchKernelGGL(topl_select_kernel, dim3(nq), dim3(256), lds, s, scores, ix.nl, L, kcap,
-                     out_leaf, out_dist);
+  if (ix.nl <= kLdsSelectLeaves && lds <= 160 * 1024) {
+    hipLaunchKernelGGL(topl_select_kernel, dim3(nq), dim3(256), lds, s, scores, ix.nl, L, kcap,
+                       out_leaf, out_dist);
+  } else {
+    uint32_t lcap = 1;
+    while (lcap < uint32_t(std::min(L, ix.nl))) lcap <<= 1;
+    if (size_t(lcap) * 8 > 128 * 1024) return hipErrorInvalidValue;   // L > 16384
+    hipLaunchKernelGGL(topl_select_global_kernel, dim3(nq), dim3(256), size_t(lcap) * 8, s, scores,
+                       ix.nl, L, lcap, out_leaf, out_dist);
+  }
   return hipGetLastError();
 }
 
@@ -1593,18 +1698,18 @@ hipError_t LaunchPairs(const DeviceIndex& ix, const uint32_t* order, const int32
                        uint32_t queries_per_item, hipStream_t s) {
   const int n = nq * L;
   const int nblocks = (n + kPairsPerBlock - 1) / kPairsPerBlock;
-  const size_t lds = size_t(ix.nl) * 4;
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const int ranges = (ix.nl + kLeafRange - 1) / kLeafRange;
+  const size_t lds = size_t(std::min(ix.nl, kLeafRange)) * 4;
   if (n > 0)
-    hipLaunchKernelGGL(pairs_count_kernel, dim3(nblocks), dim3(256), lds, s, topl_leaf, n, ix.nl,
-                       block_cnt, cnt);
+    hipLaunchKernelGGL(pairs_count_kernel, dim3(nblocks, ranges), dim3(256), lds, s, topl_leaf, n,
+                       ix.nl, block_cnt, cnt);
   hipLaunchKernelGGL(pairs_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, order,
                      ix.leaf_size, ix.nl, ix.nb, chunk_tiles, queries_per_item, pair_off,
                      tile_prefix, totals, code_bytes);
   if (n > 0) {
     hipLaunchKernelGGL(pairs_block_offsets_kernel, dim3((ix.nl + 255) / 256), dim3(256), 0, s,
                        block_cnt, nblocks, ix.nl);
-    hipLaunchKernelGGL(pairs_scatter_kernel, dim3(nblocks), dim3(256), lds, s, topl_leaf,
+    hipLaunchKernelGGL(pairs_scatter_kernel, dim3(nblocks, ranges), dim3(256), lds, s, topl_leaf,
                        topl_dist, n, L, ix.nl, pair_off, block_cnt, pair_q, pair_bias);
   }
   hipLaunchKernelGGL(pairs_work_kernel, dim3((ix.nl + 255) / 256), dim3(256), 0, s, tile_prefix,

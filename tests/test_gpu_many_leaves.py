@@ -1,0 +1,87 @@
+"""GPU parity for indexes with more leaves than one LDS-resident selection holds.
+
+Deep1B's configuration (BASELINE.json configs[4]) has 50000 leaves: the
+per-query top-L over 50000 partition scores (KMeansTreePartitioner::
+TokensForDatapointWithSpillingBatched, kmeans_tree_partitioner.cc:643-730) is
+selected from global memory (topl_select_global_kernel) and the query-by-leaf
+inversion (InvertCentersToSearch, tree_ah_hybrid_residual.cc:610-622) counts
+in LDS leaf ranges.  The indexes here are synthetic but valid: random centers
+(with exact duplicates, so partition scores tie and the (distance, leaf index)
+order decides), random leaf assignment (many empty leaves), a random codebook
+and codes -- the parity bar is the oracle on the same index, bit for bit.
+"""
+import numpy as np
+import pytest
+
+from scann_amd.index import TreeAHIndex
+
+pytestmark = pytest.mark.gpu
+
+
+def _random_index(nl, n, dim, metric, seed, dup=True):
+    rng = np.random.default_rng(seed)
+    centers = rng.standard_normal((nl, dim)).astype(np.float32)
+    if dup:   # every center of the second half repeats one of the first half
+        h = nl // 2
+        centers[h:2 * h] = centers[rng.permutation(h)]
+    labels = np.sort(rng.integers(0, nl, n))
+    ids = np.arange(n, dtype=np.uint32)
+    counts = np.bincount(labels, minlength=nl)
+    offsets = np.zeros(nl + 1, np.uint64)
+    offsets[1:] = np.cumsum(counts)
+    nb = dim // 2
+    codebook = (0.3 * rng.standard_normal((nb, 16, 2))).astype(np.float32)
+    codes = rng.integers(0, 16, (n, nb)).astype(np.uint8)
+    db = rng.standard_normal((n, dim)).astype(np.float32)
+    ix = TreeAHIndex(metric=metric, dim=dim, num_blocks=nb, dims_per_block=2,
+                     residual=metric == 0, centers=centers, codebook=codebook,
+                     leaf_offsets=offsets, leaf_members=ids, member_codes=codes,
+                     num_datapoints=n, dataset=db)
+    q = rng.standard_normal((24, dim)).astype(np.float32)
+    return ix, q
+
+
+@pytest.fixture(scope="module")
+def native():
+    from scann_amd import _native
+    return _native
+
+
+@pytest.mark.parametrize("nl,metric", [(20000, 0), (20000, 1), (50000, 0)])
+def test_partition_topl_many_leaves(native, oracle, nl, metric):
+    ix, q = _random_index(nl, 2 * nl, 16, metric, seed=nl + metric)
+    n = native.NativeIndex(ix)
+    for L in (1, 2, 99, 100, 1000, 4096):
+        gl, gd = n.partition_topl(q, L)
+        ol, od = oracle.partition_topl(q, ix.centers, ix.metric, L)
+        np.testing.assert_array_equal(gl, ol)
+        np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+
+
+def test_partition_topl_all_ties(native, oracle):
+    """Every center identical: the L lowest leaf indices, in index order."""
+    ix, q = _random_index(20000, 30000, 16, 0, seed=5, dup=False)
+    ix.centers[:] = ix.centers[0]
+    n = native.NativeIndex(ix)
+    for L in (1, 37, 300):
+        gl, gd = n.partition_topl(q, L)
+        ol, od = oracle.partition_topl(q, ix.centers, ix.metric, L)
+        np.testing.assert_array_equal(gl, ol)
+        np.testing.assert_array_equal(gl[0], np.arange(L))
+        np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+
+
+@pytest.mark.parametrize("nl,metric", [(20000, 0), (50000, 0), (20000, 1)])
+def test_search_many_leaves_matches_oracle(native, oracle, nl, metric):
+    ix, q = _random_index(nl, 2 * nl, 16, metric, seed=7 * nl + metric)
+    n = native.NativeIndex(ix)
+    for leaves, pre in ((50, 100), (400, 100)):
+        gi, gd, gc = n.search_pre_reorder(q, leaves, pre)
+        oi, od, oc = oracle.search_pre_reorder(ix, q, leaves, pre, oracle.MODE_IDEAL)
+        np.testing.assert_array_equal(gc, oc)
+        np.testing.assert_array_equal(gi, oi)
+        np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+        gi, gd, gc = n.search_batched(q, leaves, pre, 10, True)
+        oi, od, oc = oracle.search(ix, q, leaves, pre, 10, True, oracle.MODE_IDEAL)
+        np.testing.assert_array_equal(gi, oi)
+        np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
