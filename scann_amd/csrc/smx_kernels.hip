@@ -171,48 +171,60 @@ __device__ uint32_t SelectSmallest(uint64_t* keys, uint32_t n, uint32_t k, uint6
 // ---------------------------------------------------------------------------
 typedef float v16f __attribute__((ext_vector_type(16)));
 
-__global__ void __launch_bounds__(64) partition_scores_kernel(
+// A 256-thread block computes 64 queries x 64 centers (wave w: query half
+// w & 1, center half w >> 1); the operands are staged in LDS 32 dims at a time
+// with coalesced row loads (-q and c or 2c, zero-padded past dim), so every
+// MFMA reads its two floats per lane from LDS instead of a strided global row.
+constexpr int kPartTile = 64, kPartChunk = 32;
+
+__global__ void __launch_bounds__(256) partition_scores_kernel(
     const float* __restrict__ queries, int nq, int dim, const float* __restrict__ centers,
     const float* __restrict__ cnorm, int nl, int metric, float* __restrict__ scores) {
-  const int lane = threadIdx.x;
+  __shared__ float qs[kPartTile][kPartChunk + 1];
+  __shared__ float cs[kPartTile][kPartChunk + 1];
+  __shared__ float qn[kPartTile];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, k = lane >> 5;
-  const int q0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
-  const int qa = min(q0 + r, nq - 1);     // A row (query) of this lane
+  const int qt = blockIdx.x * kPartTile, ct = blockIdx.y * kPartTile;
+  const int qw = (wave & 1) * 32, cw = (wave >> 1) * 32;   // this wave's sub-tile
+  const int q0 = qt + qw, c0 = ct + cw;
   const int cb = min(c0 + r, nl - 1);     // B column (center) of this lane
-  const float* qrow = queries + size_t(qa) * dim;
-  const float* crow = centers + size_t(cb) * dim;
   v16f acc;
-  __shared__ float qn[32];
   if (metric == 1) {
-    if (lane < 32) {
+    if (tid < kPartTile) {
       double s = 0.0;
-      const float* qq = queries + size_t(min(q0 + lane, nq - 1)) * dim;
+      const float* qq = queries + size_t(min(qt + tid, nq - 1)) * dim;
       for (int d = 0; d < dim; ++d) s += double(qq[d]) * double(qq[d]);
-      qn[lane] = float(s);
+      qn[tid] = float(s);
     }
     __syncthreads();
     // C layout: col = lane & 31 (center), row = (i&3) + 8*(i>>2) + 4*(lane>>5)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int row = (i & 3) + 8 * (i >> 2) + 4 * k;
-      acc[i] = __fadd_rn(cnorm[cb], qn[row]);
+      acc[i] = __fadd_rn(cnorm[cb], qn[qw + row]);
     }
   } else {
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
   }
   const float cscale = metric == 1 ? 2.0f : 1.0f;
-  for (int d = 0; d < dim; d += 2) {
-    const int dd = d + k;
-    float av, bv;
-    if (dd < dim) {
-      av = -qrow[dd];
-      bv = __fmul_rn(crow[dd], cscale);
-    } else {
-      av = -0.0f;
-      bv = 0.0f;
+  for (int d0 = 0; d0 < dim; d0 += kPartChunk) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < (kPartTile * kPartChunk) / 256; ++i) {
+      const int e = tid + i * 256;
+      const int row = e / kPartChunk, col = e % kPartChunk, d = d0 + col;
+      const float* qrow = queries + size_t(min(qt + row, nq - 1)) * dim;
+      const float* crow = centers + size_t(min(ct + row, nl - 1)) * dim;
+      qs[row][col] = d < dim ? -qrow[d] : -0.0f;
+      cs[row][col] = d < dim ? __fmul_rn(crow[d], cscale) : 0.0f;
     }
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    __syncthreads();
+    const int steps = min(kPartChunk, ((dim - d0) + 1) & ~1);
+    for (int s = 0; s < steps; s += 2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qs[qw + r][s + k], cs[cw + r][s + k], acc, 0, 0,
+                                                 0);
   }
   const int col = c0 + r;
   if (col < nl) {
@@ -1667,8 +1679,10 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   while (lp2 < uint32_t(L)) lp2 <<= 1;
   const uint32_t selcap = std::max<uint32_t>(2048u, 2 * lp2);
   const size_t lds = size_t(kcap) * 8 + size_t(selcap) * 8 + (kSelBins + 256) * 4;
-  hipLaunchKernelGGL(partition_scores_kernel, dim3((nq + 31) / 32, (ix.nl + 31) / 32), dim3(64), 0,
-                     s, queries, nq, ix.dim, ix.centers, ix.cnorm, ix.nl, ix.metric, scores);
+  hipLaunchKernelGGL(partition_scores_kernel,
+                     dim3((nq + kPartTile - 1) / kPartTile, (ix.nl + kPartTile - 1) / kPartTile),
+                     dim3(256), 0, s, queries, nq, ix.dim, ix.centers, ix.cnorm, ix.nl, ix.metric,
+                     scores);
   if (ix.nl <= kLdsSelectLeaves && lds <= 160 * 1024) {
     hipLaunchKernelGGL(topl_select_kernel, dim3(nq), dim3(256), lds, s, scores, ix.nl, L, kcap,
                        out_leaf, out_dist);
