@@ -47,7 +47,8 @@ def native():
     return _native
 
 
-@pytest.mark.parametrize("nl,metric", [(20000, 0), (20000, 1), (50000, 0)])
+@pytest.mark.parametrize("nl,metric", [(1000, 0), (2048, 1), (5000, 0), (20000, 0), (20000, 1),
+                                       (50000, 0)])
 def test_partition_topl_many_leaves(native, oracle, nl, metric):
     ix, q = _random_index(nl, 2 * nl, 16, metric, seed=nl + metric)
     n = native.NativeIndex(ix)
@@ -58,12 +59,14 @@ def test_partition_topl_many_leaves(native, oracle, nl, metric):
         np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
 
 
-def test_partition_topl_all_ties(native, oracle):
-    """Every center identical: the L lowest leaf indices, in index order."""
-    ix, q = _random_index(20000, 30000, 16, 0, seed=5, dup=False)
+@pytest.mark.parametrize("nl", [1000, 5000, 20000])
+def test_partition_topl_all_ties(native, oracle, nl):
+    """Every center identical: the L lowest leaf indices, in index order
+    (wave select, block select and global-memory select)."""
+    ix, q = _random_index(nl, 30000, 16, 0, seed=5, dup=False)
     ix.centers[:] = ix.centers[0]
     n = native.NativeIndex(ix)
-    for L in (1, 37, 300):
+    for L in (1, 37, 300, 700):
         gl, gd = n.partition_topl(q, L)
         ol, od = oracle.partition_topl(q, ix.centers, ix.metric, L)
         np.testing.assert_array_equal(gl, ol)
