@@ -8,7 +8,10 @@ search_batched over the 1000 device-resident queries, results written to
 device memory (partition selection, LUT build, LUT16 scan + top-k, SOAR-free
 dedupe, exact reorder and sort all inside the step).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config glove|sift]
+
+`--config sift` measures BASELINE.json configs[2] (SIFT1M shape, squared L2,
+2000 leaves) as a secondary line; the default is the metric's configuration.
 
 For N > 1 the driver starts one rank per GPU with torch.distributed.run;
 every rank holds a replica of the index and searches its own batch of 1000
@@ -41,14 +44,53 @@ def log(msg):
         print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+# --config sift (BASELINE.json configs[2]) is a secondary measurement; the
+# default line is configs[1], the metric's own configuration.
+CONFIGS = {
+    "glove": dict(n=1_183_514, leaves=1000, leaves_to_search=100, metric=0, seed=2,
+                  workload="glove-100-angular shape: 1,183,514x100 dot product, tree-AH 1000 "
+                           "leaves, LUT16 AH 50 blocks x 2 dims, leaves_to_search=100, reorder "
+                           "100, k=10, batch=1000 queries per GPU",
+                  data="synthetic (glove-100-angular-shaped seeded unit-vector mixture; no "
+                       "datasets offline)",
+                  metric_name="QPS at recall@10>=0.95, glove-100-angular, batch=1000; HBM GB/s achieved"),
+    "sift": dict(n=1_000_000, leaves=2000, leaves_to_search=100, metric=1, seed=3,
+                 workload="SIFT1M shape: 1,000,000x128 squared L2, tree + AH (non-residual) "
+                          "2000 leaves, LUT16 AH 64 blocks x 2 dims, leaves_to_search=100, "
+                          "reorder 100, k=10, batch=1000 queries per GPU",
+                 data="synthetic (SIFT1M-shaped seeded non-negative rounded mixture; no "
+                      "datasets offline)",
+                 metric_name="QPS at recall@10, SIFT1M shape (BASELINE.json configs[2]), batch=1000"),
+}
+CFG = CONFIGS["glove"]
+
+
+def scan_k(num_blocks):
+    """MFMA steps of the compiled scan instantiation (EffectiveKSteps in smx_searcher.hip)."""
+    k = (num_blocks + 1) // 2
+    return next(v for v in (4, 8, 12, 16, 20, 24, 25, 28, 32) if v >= k)
+
+
+def queries_for_rank(dim, rank):
+    """This rank's 1000-query batch, drawn from the dataset's own mixture."""
+    from scann_amd import synthetic
+    if CFG["metric"] == 0:
+        return synthetic.mixture(NQ, dim, 2000, 0.9, seed=2 + 100 + 7919 * rank, means_seed=2)
+    x = synthetic.mixture(NQ, dim, 1000, 0.6, 3 + 100 + 7919 * rank, normalize=False,
+                          means_seed=3)
+    return np.clip(np.rint(np.abs(x) * 256.0), 0, 255).astype(np.float32)
+
+
 def build_index(n, seed):
     from scann_amd import index_builder, synthetic
-    from scann_amd.index import METRIC_DOT
     t = time.time()
-    db, q = synthetic.glove_like(n=n, nq=NQ, seed=seed)
+    if CFG["metric"] == 0:
+        db, q = synthetic.glove_like(n=n, nq=NQ, seed=seed)
+    else:
+        db, q = synthetic.sift_like(n=n, nq=NQ, seed=seed)
     log(f"data {db.shape} generated in {time.time() - t:.1f}s")
     t = time.time()
-    ix = index_builder.build_tree_ah(db, METRIC_DOT, LEAVES, DPB, training_iterations=12,
+    ix = index_builder.build_tree_ah(db, CFG["metric"], LEAVES, DPB, training_iterations=12,
                                      ah_training_iterations=10, seed=seed)
     sizes = ix.leaf_sizes()
     log(f"index built in {time.time() - t:.1f}s: leaves min/mean/max "
@@ -60,7 +102,10 @@ def cpu_baseline(ix, q, gpu_idx, threads):
     """The oracle's AVX2 port of the reference path on host cores (rank 0)."""
     from oracle import binding as oracle
     oracle.build()
-    port = oracle.Avx2Port(ix)
+    try:
+        port = oracle.Avx2Port(ix)
+    except ValueError:   # pipeline B (non-residual): the oracle's C restatement
+        return cpu_baseline_restatement(ix, q, gpu_idx, threads)
     port.search(q[:50], LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True, threads)  # warm-up
     reps, t_total, out = 0, 0.0, None
     while reps < 400 and (t_total < 10.0 or reps == 0):
@@ -78,6 +123,25 @@ def cpu_baseline(ix, q, gpu_idx, threads):
                 id_mismatch_vs_gpu=mismatch)
 
 
+def cpu_baseline_restatement(ix, q, gpu_idx, threads):
+    """Indexes the AVX2 port does not cover: the oracle's scalar C restatement
+    (ideal mode), multithreaded over queries."""
+    from oracle import binding as oracle
+    reps, t_total, out = 0, 0.0, None
+    while reps < 50 and (t_total < 10.0 or reps == 0):
+        t = time.perf_counter()
+        out = oracle.search(ix, q, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True, oracle.MODE_IDEAL,
+                            threads)
+        t_total += time.perf_counter() - t
+        reps += 1
+    return dict(value=round(reps * q.shape[0] / t_total, 1), unit="queries/s", cores=threads,
+                kind="port",
+                sample=f"{reps} x the same {q.shape[0]}-query batch through the oracle's scalar "
+                       f"C restatement (oracle/scann_oracle.cc, ideal mode; the AVX2 port covers "
+                       f"the residual global top-N path only), {threads} threads, {t_total:.1f}s",
+                id_mismatch_vs_gpu=float((out[0] != gpu_idx).mean()))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -86,7 +150,13 @@ def main():
     ap.add_argument("--n", type=int, default=1_183_514)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="glove")
     args = ap.parse_args()
+    global CFG, LEAVES, LEAVES_TO_SEARCH
+    CFG = CONFIGS[args.config]
+    LEAVES, LEAVES_TO_SEARCH = CFG["leaves"], CFG["leaves_to_search"]
+    if args.config != "glove" and args.n == 1_183_514:
+        args.n = CFG["n"]
 
     import torch
     rank = int(os.environ.get("RANK", "0"))
@@ -101,9 +171,9 @@ def main():
     torch.cuda.set_device(dev)
 
     from scann_amd import _native, synthetic
-    db, _, ix = build_index(args.n, seed=2)
+    db, _, ix = build_index(args.n, seed=CFG["seed"])
     # per-rank query batch from the same mixture (weak scaling)
-    q = synthetic.mixture(NQ, db.shape[1], 2000, 0.9, seed=2 + 100 + 7919 * rank, means_seed=2)
+    q = queries_for_rank(db.shape[1], rank)
     nat = _native.NativeIndex(ix, device=local)
     log(f"native index: {nat.info()}")
 
@@ -159,7 +229,7 @@ def main():
 
     # recall@10 of this rank's batch against exact brute force
     gidx = out_idx.cpu().numpy().astype(np.int64)
-    truth = synthetic.brute_force_topk(db, q, FINAL_NN, 0)
+    truth = synthetic.brute_force_topk(db, q, FINAL_NN, CFG["metric"])
     recall = synthetic.recall_at_k(gidx, truth, FINAL_NN)
 
     avg_scan_ms = float(np.mean(scan_ms))
@@ -176,7 +246,7 @@ def main():
     t_last = nat.timings()
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "scan_traffic.json")
-    if os.path.exists(tpath):
+    if os.path.exists(tpath) and args.config == "glove":   # measured on the glove workload
         import hashlib
         with open(tpath) as f:
             tr = json.load(f)
@@ -186,7 +256,7 @@ def main():
 
     if rank == 0:
         result = {
-            "metric": "QPS at recall@10>=0.95, glove-100-angular, batch=1000; HBM GB/s achieved",
+            "metric": CFG["metric_name"],
             "value": round(value, 1),
             "unit": "queries/s",
             "n_gpus": world,
@@ -197,11 +267,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int8",
-            "data": "synthetic (glove-100-angular-shaped seeded unit-vector mixture; no datasets offline)",
+            "data": CFG["data"],
             "config": {
-                "workload": "glove-100-angular shape: 1,183,514x100 dot product, tree-AH 1000 leaves, "
-                            "LUT16 AH 50 blocks x 2 dims, leaves_to_search=100, reorder 100, k=10, "
-                            "batch=1000 queries per GPU",
+                "workload": CFG["workload"],
                 "num_datapoints": int(args.n), "dim": int(db.shape[1]), "num_leaves": LEAVES,
                 "leaves_to_search": LEAVES_TO_SEARCH, "pre_reorder_nn": PRE_NN,
                 "final_nn": FINAL_NN, "batch": NQ, "parallelism": f"query-sharded replicas x{world}",
@@ -210,7 +278,7 @@ def main():
             "roofline": {
                 "bound": "mfma", "achieved": round(achieved, 1), "peak": peak,
                 "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-                "kernel": "lut16_scan_kernel<25> (main pass)",
+                "kernel": f"lut16_scan_kernel<{scan_k(ix.num_blocks)}> (main pass)",
                 "avg_launch_ms_source": "HIP events around every scan launch, profiled replay of the timed steps",
                 "op_type": "int8 MFMA ops (TOPS) of the one-hot LUT16 GEMM formulation",
                 "algorithmic_ops_per_launch": ops_per_launch,
