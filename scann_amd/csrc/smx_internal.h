@@ -141,9 +141,18 @@ struct MergeArgs {
 hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int nq,
                                int L, int32_t* out_leaf, float* out_dist,
                                float* scores /*[nq][nl] scratch*/, hipStream_t s);
+// Per-call state the LUT build kernel resets on its way (no memset nodes).
+struct LutInit {
+  uint32_t* counters = nullptr;
+  uint32_t n_counters = 0;
+  uint32_t* cand_count = nullptr;
+  uint32_t n_cand = 0;
+  uint64_t* tau = nullptr;
+  uint32_t n_tau = 0;
+};
 hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq,
                           int8_t* lut, float* mult, float* inv, uint8_t* lut_u8,
-                          hipStream_t s);
+                          hipStream_t s, const LutInit* init = nullptr);
 hipError_t LaunchPairs(const DeviceIndex& ix, const uint32_t* order /*[nl] work order*/,
                        const int32_t* topl_leaf, const float* topl_dist, int nq, int L, uint32_t* cnt /*[nl]*/,
                        uint32_t* block_cnt /*[ceil(nq*L/4096)][nl]*/,

@@ -364,9 +364,17 @@ __global__ void __launch_bounds__(256) lut_build_kernel(
     const float* __restrict__ queries, int dim, const float* __restrict__ codebook,
     int nb, int dpb, int padded_blocks, int metric, int residual,
     int8_t* __restrict__ lut, float* __restrict__ mult, float* __restrict__ inv,
-    uint8_t* __restrict__ lut_u8) {
+    uint8_t* __restrict__ lut_u8, LutInit init) {
   __shared__ float raw[kMaxBlocks * 16];
   __shared__ float red[256];
+  {
+    // the search's per-call state, reset here instead of by separate memset
+    // nodes: counters and candidate counts to 0, thresholds to "open"
+    const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x, gs = gridDim.x * blockDim.x;
+    for (uint32_t i = gt; i < init.n_counters; i += gs) init.counters[i] = 0u;
+    for (uint32_t i = gt; i < init.n_cand; i += gs) init.cand_count[i] = 0u;
+    for (uint32_t i = gt; i < init.n_tau; i += gs) init.tau[i] = kNoThreshold;
+  }
   const int qi = blockIdx.x;
   const float* q = queries + size_t(qi) * dim;
   const int nent = nb * 16;
@@ -1697,10 +1705,13 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
 }
 
 hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq, int8_t* lut,
-                          float* mult, float* inv, uint8_t* lut_u8, hipStream_t s) {
+                          float* mult, float* inv, uint8_t* lut_u8, hipStream_t s,
+                          const LutInit* init) {
   if (nq == 0) return hipSuccess;
+  const LutInit none{};
   hipLaunchKernelGGL(lut_build_kernel, dim3(nq), dim3(256), 0, s, queries, ix.dim, ix.codebook,
-                     ix.nb, ix.dpb, 2 * ix.ksteps, ix.metric, ix.residual, lut, mult, inv, lut_u8);
+                     ix.nb, ix.dpb, 2 * ix.ksteps, ix.metric, ix.residual, lut, mult, inv, lut_u8,
+                     init ? *init : none);
   return hipGetLastError();
 }
 

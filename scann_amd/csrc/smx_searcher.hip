@@ -132,12 +132,6 @@ struct smx_index {
   uint32_t* host_stats = nullptr;  // pinned copy of the stats words
   smx_timings timings{};
   hipEvent_t ev[16] = {};
-  // side branch of the first pass: the LUT build and the query-by-leaf
-  // inversion run on `side` while the main stream does partition selection
-  // and the seed thresholds (fork/join by events; captured as graph branches)
-  hipStream_t side = nullptr;
-  hipEvent_t fork[4] = {};
-  bool overlap = true;
 };
 
 namespace {
@@ -458,40 +452,25 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   // instead of ~20, no per-kernel host overhead); eager otherwise.
   auto first_pass = [&]() -> int {
     Mark(h, 0, s);
-    SMX_HIP(hipMemsetAsync(w.counters, 0, sizeof(uint32_t) * (2 * nl + 20), s));
-    SMX_HIP(hipMemsetAsync(w.cand_count, 0, sizeof(uint32_t) * nq, s));
-    SMX_HIP(smx::LaunchFill64(w.tau, smx::kNoThreshold, nq, s));
-    auto pairs = [&](hipStream_t st) {
-      return smx::LaunchPairs(ix, ix.leaf_order, w.topl_leaf, w.topl_dist, nq, L, cnt,
-                              w.block_cnt, w.pair_off, w.tile_prefix, w.pair_q, w.pair_bias,
-                              w.work, stats + 3, code_bytes, h->chunk_tiles, 32u, st);
-    };
-    if (h->overlap && !h->profiling && h->side) {
-      // main:  memsets -> partition -----------> seed -> (join) scan -> select
-      // side:        \-> LUT build -(partition)-> inversion --/
-      hipStream_t b = h->side;
-      SMX_HIP(hipEventRecord(h->fork[0], s));
-      SMX_HIP(hipStreamWaitEvent(b, h->fork[0], 0));
-      SMX_HIP(smx::LaunchLutBuild(ix, queries, nq, w.lut, w.mult, w.inv, nullptr, b));
-      SMX_HIP(hipEventRecord(h->fork[1], b));
-      SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s));
-      SMX_HIP(hipEventRecord(h->fork[2], s));
-      SMX_HIP(hipStreamWaitEvent(b, h->fork[2], 0));
-      SMX_HIP(pairs(b));
-      SMX_HIP(hipEventRecord(h->fork[3], b));
-      SMX_HIP(hipStreamWaitEvent(s, h->fork[1], 0));
-      SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
-      SMX_HIP(hipStreamWaitEvent(s, h->fork[3], 0));
-    } else {
-      SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s));
-      Mark(h, 1, s);
-      SMX_HIP(smx::LaunchLutBuild(ix, queries, nq, w.lut, w.mult, w.inv, nullptr, s));
-      Mark(h, 2, s);
-      SMX_HIP(pairs(s));
-      Mark(h, 3, s);
-      SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
-      Mark(h, 4, s);
-    }
+    // the LUT build also zeroes the counters / candidate counts and opens the
+    // thresholds; it precedes the inversion, the seed and the scan on every path
+    smx::LutInit init;
+    init.counters = w.counters;
+    init.n_counters = uint32_t(2 * nl + 20);
+    init.cand_count = w.cand_count;
+    init.n_cand = uint32_t(nq);
+    init.tau = w.tau;
+    init.n_tau = uint32_t(nq);
+    SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s));
+    Mark(h, 1, s);
+    SMX_HIP(smx::LaunchLutBuild(ix, queries, nq, w.lut, w.mult, w.inv, nullptr, s, &init));
+    Mark(h, 2, s);
+    SMX_HIP(smx::LaunchPairs(ix, ix.leaf_order, w.topl_leaf, w.topl_dist, nq, L, cnt, w.block_cnt,
+                             w.pair_off, w.tile_prefix, w.pair_q, w.pair_bias, w.work, stats + 3,
+                             code_bytes, h->chunk_tiles, 32u, s));
+    Mark(h, 3, s);
+    SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
+    Mark(h, 4, s);
     Mark(h, 5, s);
     SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s));
     Mark(h, 6, s);
@@ -511,7 +490,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
         uint64_t(reinterpret_cast<uintptr_t>(out_count)), uint64_t(reinterpret_cast<uintptr_t>(shard_out)),
         uint64_t(reinterpret_cast<uintptr_t>(s)),
         w.gen ^ (uint64_t(w.cap) << 20) ^ (uint64_t(seed) << 40) ^ (uint64_t(h->chunk_tiles) << 48) ^
-            (uint64_t(variant) << 60) ^ (uint64_t(h->overlap) << 63)};
+            (uint64_t(variant) << 60)};
     if (!h->graph_exec || std::memcmp(key, h->graph_key, sizeof(key)) != 0) {
       if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
       h->graph_exec = nullptr;
@@ -653,10 +632,7 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
   }
   const char* ng = std::getenv("SMX_NO_GRAPH");
   h->use_graph = !(ng && ng[0] == '1');
-  const char* no = std::getenv("SMX_NO_OVERLAP");
-  h->overlap = !(no && no[0] == '1');
-  if (hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess) h->side = nullptr;
-  for (auto& e : h->fork) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+
   *out = h;
   return SMX_OK;
 }
@@ -671,12 +647,6 @@ int smx_index_destroy(smx_index* h) {
   FreeIndex(h->ix);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
-  for (auto& e : h->fork)
-    if (e) (void)hipEventDestroy(e);
-  if (h->side) {
-    (void)hipStreamSynchronize(h->side);
-    (void)hipStreamDestroy(h->side);
-  }
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return SMX_OK;

@@ -1,8 +1,7 @@
-"""Graph replays with new query contents: the first pass is captured once per
-call shape (hipGraph, two stream branches) and replayed while the queries in
-the same device buffer change from call to call.  Every replay must see its
-own batch: results are compared with the oracle (ideal mode) batch by batch,
-for the overlapped graph, the serial graph and the eager pipeline."""
+"""Repeated calls with new query contents in the same device buffers: the
+first pass is captured once per call shape (hipGraph) and replayed.  Every
+call must see its own batch: results are compared with the oracle (ideal
+mode) batch by batch, for graph replays and for eager launches."""
 import os
 
 import numpy as np
@@ -18,11 +17,11 @@ def medium():
     return make_index(n=60000, d=32, leaves=120, seed=21, components=200)
 
 
-@pytest.mark.parametrize("env", [{}, {"SMX_NO_OVERLAP": "1"}, {"SMX_NO_GRAPH": "1"}])
+@pytest.mark.parametrize("env", [{}, {"SMX_NO_GRAPH": "1"}])   # graph replay, eager
 def test_replays_see_new_queries(oracle, medium, env):
     from scann_amd import _native, synthetic
     ix, db, _ = medium
-    old = {k: os.environ.get(k) for k in ("SMX_NO_OVERLAP", "SMX_NO_GRAPH")}
+    old = {k: os.environ.get(k) for k in ("SMX_NO_GRAPH",)}
     try:
         for k in old:
             os.environ.pop(k, None)
