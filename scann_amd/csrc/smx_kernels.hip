@@ -486,7 +486,27 @@ __global__ void __launch_bounds__(1024) pairs_scan_kernel(const uint32_t* __rest
                                                           uint32_t* __restrict__ pair_off,
                                                           uint32_t* __restrict__ tile_prefix,
                                                           uint32_t* __restrict__ totals,
-                                                          unsigned long long* __restrict__ code_bytes) {
+                                                          unsigned long long* __restrict__ code_bytes,
+                                                          uint2* __restrict__ work,
+                                                          uint32_t* __restrict__ block_cnt,
+                                                          int fused_blocks) {
+  // small trees: the per-leaf exclusive prefix over the counting blocks
+  // (pairs_block_offsets_kernel) is done here, 8 loads in flight per step
+  for (int l = threadIdx.x; l < nl && fused_blocks > 0; l += blockDim.x) {
+    uint32_t run = 0;
+    for (int b0 = 0; b0 < fused_blocks; b0 += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = b0 + u < fused_blocks ? block_cnt[size_t(b0 + u) * nl + l] : 0u;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (b0 + u < fused_blocks) {
+          block_cnt[size_t(b0 + u) * nl + l] = run;
+          run += v[u];
+        }
+    }
+  }
   __shared__ uint32_t s_pairs[1024];
   __shared__ uint32_t s_tiles[1024];
   __shared__ unsigned long long s_bytes[1024];
@@ -542,7 +562,12 @@ __global__ void __launch_bounds__(1024) pairs_scan_kernel(const uint32_t* __rest
     pair_off[leaf] = rp;
     tile_prefix[p] = rt;
     rp += c;
-    rt += ((c + qpi - 1) / qpi) * LeafChunks(leaf_size[leaf], chunk_tiles);
+    // this leaf's work items: (leaf, query tile << 16 | dp chunk)
+    const uint32_t chunks = LeafChunks(leaf_size[leaf], chunk_tiles);
+    const uint32_t items = ((c + qpi - 1) / qpi) * chunks;
+    for (uint32_t u = 0; u < items; ++u)
+      work[rt + u] = make_uint2(leaf, ((u / chunks) << 16) | (u % chunks));
+    rt += items;
   }
   if (threadIdx.x == blockDim.x - 1) {
     tile_prefix[nl] = s_tiles[blockDim.x - 1];
@@ -567,21 +592,6 @@ __global__ void __launch_bounds__(256) pairs_scatter_kernel(
     const uint32_t pos = pair_off[leaf] + bo[leaf] + atomicAdd(&fill[leaf - l0], 1u);
     pair_q[pos] = uint32_t(i / L);
     pair_bias[pos] = topl_dist[i];
-  }
-}
-
-__global__ void pairs_work_kernel(const uint32_t* __restrict__ tile_prefix,
-                                  const uint32_t* __restrict__ order,
-                                  const uint32_t* __restrict__ leaf_size, int nl,
-                                  uint32_t chunk_tiles, uint2* __restrict__ work) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= nl) return;
-  const uint32_t leaf = order[p];
-  const uint32_t chunks = LeafChunks(leaf_size[leaf], chunk_tiles);
-  // item = (leaf, query tile << 16 | dp chunk)
-  for (uint32_t w = tile_prefix[p]; w < tile_prefix[p + 1]; ++w) {
-    const uint32_t u = w - tile_prefix[p];
-    work[w] = make_uint2(leaf, ((u / chunks) << 16) | (u % chunks));
   }
 }
 
@@ -1728,17 +1738,18 @@ hipError_t LaunchPairs(const DeviceIndex& ix, const uint32_t* order, const int32
   if (n > 0)
     hipLaunchKernelGGL(pairs_count_kernel, dim3(nblocks, ranges), dim3(256), lds, s, topl_leaf, n,
                        ix.nl, block_cnt, cnt);
+  // up to 4096 leaves the block offsets ride in the one-block scan kernel
+  const int fused = (n > 0 && ix.nl <= 4096) ? nblocks : 0;
   hipLaunchKernelGGL(pairs_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, order,
                      ix.leaf_size, ix.nl, ix.nb, chunk_tiles, queries_per_item, pair_off,
-                     tile_prefix, totals, code_bytes);
+                     tile_prefix, totals, code_bytes, work, block_cnt, fused);
   if (n > 0) {
-    hipLaunchKernelGGL(pairs_block_offsets_kernel, dim3((ix.nl + 255) / 256), dim3(256), 0, s,
-                       block_cnt, nblocks, ix.nl);
+    if (!fused)
+      hipLaunchKernelGGL(pairs_block_offsets_kernel, dim3((ix.nl + 255) / 256), dim3(256), 0, s,
+                         block_cnt, nblocks, ix.nl);
     hipLaunchKernelGGL(pairs_scatter_kernel, dim3(nblocks, ranges), dim3(256), lds, s, topl_leaf,
                        topl_dist, n, L, ix.nl, pair_off, block_cnt, pair_q, pair_bias);
   }
-  hipLaunchKernelGGL(pairs_work_kernel, dim3((ix.nl + 255) / 256), dim3(256), 0, s, tile_prefix,
-                     order, ix.leaf_size, ix.nl, chunk_tiles, work);
   return hipGetLastError();
 }
 
