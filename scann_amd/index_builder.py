@@ -48,6 +48,8 @@ def _assign_l2(x: np.ndarray, centers: np.ndarray, chunk: int = 1 << 16) -> np.n
     """argmin_c ||x - c||^2 for every row of x (ties -> lowest index)."""
     torch, dev = _torch_device()
     out = np.empty(x.shape[0], dtype=np.int64)
+    # bound one distance block to ~2^28 entries (50000 centers: 5k rows)
+    chunk = max(1024, min(chunk, (1 << 28) // max(1, centers.shape[0])))
     if torch is not None:
         c = torch.from_numpy(centers).to(dev)
         cn = (c * c).sum(1)
@@ -78,9 +80,14 @@ def kmeans(x: np.ndarray, k: int, iterations: int, seed: int,
     centers = x[rng.choice(n, k, replace=False)].astype(np.float32, copy=True)
     for _ in range(iterations):
         lab = _assign_l2(x, centers)
-        sums = np.zeros_like(centers, dtype=np.float64)
-        np.add.at(sums, lab, x)
         cnt = np.bincount(lab, minlength=k)
+        # per-center sums: sort by label, reduce each run (np.add.at is slow)
+        order = np.argsort(lab, kind="stable")
+        starts = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+        nzs = cnt > 0
+        sums = np.zeros_like(centers, dtype=np.float64)
+        if nzs.any():
+            sums[nzs] = np.add.reduceat(x[order].astype(np.float64), starts[nzs], axis=0)
         nz = cnt > 0
         centers[nz] = (sums[nz] / cnt[nz, None]).astype(np.float32)
         if (~nz).any():
@@ -130,6 +137,7 @@ def soar_assign(x: np.ndarray, centers: np.ndarray, primary: np.ndarray, lam: fl
                 chunk: int = 1 << 15) -> np.ndarray:
     """Secondary leaf per row with the SOAR loss (never the primary leaf)."""
     out = np.empty(x.shape[0], dtype=np.int64)
+    chunk = max(1024, min(chunk, (1 << 27) // max(1, centers.shape[0])))
     torch, dev = _torch_device()
     if torch is not None:
         c = torch.from_numpy(centers).to(dev)

@@ -1,0 +1,145 @@
+"""GPU parity at the shapes of every BASELINE.json configuration the GPU runs.
+
+Each test builds a synthetic index of the configuration's shape (no datasets
+offline), runs the whole query batch through the C ABI, and
+compares a query subset with the CPU oracle in ideal mode (ids bit-exact,
+distance bits equal; the 1e-4 relative tolerance of the contract is asserted
+as well).  The oracle's result for a query does not depend on the other
+queries of the batch, so a subset is a complete check of those queries.
+
+  configs[1] glove-100-angular: 1,183,514 x 100 dot, 1000 leaves, L=100,
+             nq=1000, reorder 100, k=10 (lut16_scan_kernel<25>)
+  configs[2] SIFT1M: squared L2, non-residual, 2000 leaves, D=128
+             (lut16_scan_kernel<32>), 300k rows
+  configs[3] 100M x 96 dot + SOAR, 10000 leaves, range split over 8 ranks:
+             the 8 shards and the merge kernel on one GPU (K=24), 400k rows
+  configs[4] Deep1B 96-d, 50000 leaves (global-memory top-L, 16-bit global
+             top-N shift), 8-way shard + merge, 1M rows
+configs[0] (brute force on the CPU reference) is CPU plumbing, out of scope.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-4
+SUB = 128   # queries checked against the oracle
+
+
+def _check(gi, gd, oi, od):
+    np.testing.assert_array_equal(gi, oi)
+    np.testing.assert_allclose(gd, od, rtol=RTOL, equal_nan=True)
+    np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+
+
+def _shard_search(ix, q, world, leaves, pre, final, reorder):
+    """`world` range-split shards in one process, stacked as the all-gather
+    delivers them, then the merge kernel."""
+    from scann_amd.distributed import NativeShardEngine
+    engines = [NativeShardEngine(ix.shard(r, world), device=0) for r in range(world)]
+    qd = torch.from_numpy(q).cuda()
+    nq = q.shape[0]
+    k = engines[0].shard_width(leaves, pre, final, reorder)
+    entries = torch.empty((world, nq, k, 2), dtype=torch.int64, device="cuda")
+    for r, e in enumerate(engines):
+        e.search_shard(qd, leaves, pre, final, reorder, entries[r])
+    idx, dst, cnt = engines[0].merge(world, entries, nq, leaves, pre, final, reorder)
+    torch.cuda.synchronize()
+    out = idx.cpu().numpy().astype(np.uint32), dst.cpu().numpy(), cnt.cpu().numpy()
+    for e in engines:
+        e.nat.close()
+    return out
+
+
+def test_glove_full_shape(oracle):
+    """configs[1] at full size: the bench workload itself."""
+    from scann_amd import _native, index_builder, synthetic
+    db, q = synthetic.glove_like(seed=2)
+    ix = index_builder.build_tree_ah(db, 0, 1000, 2, training_iterations=8,
+                                     ah_training_iterations=6, seed=2)
+    assert ix.num_blocks == 50 and ix.global_topn_shift_value() == 22
+    nat = _native.NativeIndex(ix)
+    gi, gd, gc = nat.search_batched(q, 100, 100, 10, True)
+    oi, od, oc = oracle.search(ix, q[:SUB], 100, 100, 10, True, oracle.MODE_IDEAL, 16)
+    np.testing.assert_array_equal(gc[:SUB], oc)
+    _check(gi[:SUB], gd[:SUB], oi, od)
+    # the metric's recall gate on the whole batch (exact brute force)
+    truth = synthetic.brute_force_topk(db, q, 10, 0)
+    assert synthetic.recall_at_k(gi.astype(np.int64), truth, 10) >= 0.95
+    # pre-reorder candidates (the LUT16 scan + top-k' alone)
+    pi, pd, pc = nat.search_pre_reorder(q[:SUB], 100, 100)
+    oi, od, oc = oracle.search_pre_reorder(ix, q[:SUB], 100, 100, oracle.MODE_IDEAL, 16)
+    np.testing.assert_array_equal(pc, oc)
+    _check(pi, pd, oi, od)
+    nat.close()
+
+
+def test_sift_shape(oracle):
+    """configs[2]: squared L2, non-residual (pipeline B), B=64 -> K=32."""
+    from scann_amd import _native, index_builder, synthetic
+    db, q = synthetic.sift_like(n=300_000, seed=3)
+    ix = index_builder.build_tree_ah(db, 1, 2000, 2, training_iterations=6,
+                                     ah_training_iterations=6, seed=3)
+    assert ix.num_blocks == 64 and not ix.residual and ix.global_topn_shift_value() == 0
+    nat = _native.NativeIndex(ix)
+    for leaves, reorder in ((100, True), (40, False)):
+        gi, gd, gc = nat.search_batched(q, leaves, 100, 10, reorder)
+        oi, od, oc = oracle.search(ix, q[:SUB], leaves, 100, 10, reorder, oracle.MODE_IDEAL, 16)
+        np.testing.assert_array_equal(gc[:SUB], oc)
+        _check(gi[:SUB], gd[:SUB], oi, od)
+    pi, pd, pc = nat.search_pre_reorder(q[:SUB], 100, 100)
+    oi, od, oc = oracle.search_pre_reorder(ix, q[:SUB], 100, 100, oracle.MODE_IDEAL, 16)
+    _check(pi, pd, oi, od)
+    nat.close()
+
+
+def _dot96(n, leaves, seed, soar):
+    from scann_amd import index_builder, synthetic
+    db = synthetic.mixture(n, 96, 4000, 0.9, seed)
+    q = synthetic.mixture(1000, 96, 4000, 0.9, seed + 100, means_seed=seed)
+    ix = index_builder.build_tree_ah(db, 0, leaves, 2, training_iterations=4,
+                                     training_sample_size=max(100_000, 4 * leaves),
+                                     ah_training_iterations=4, seed=seed,
+                                     soar_lambda=1.5 if soar else None)
+    assert ix.num_blocks == 48
+    return ix, db, q
+
+
+def test_config4_soar_range_split(oracle):
+    """configs[3]: 96-d dot + SOAR, 10000 leaves, range split over 8 ranks
+    (shards + merge on one GPU) == unsharded GPU == ideal oracle."""
+    from scann_amd import _native
+    ix, db, q = _dot96(400_000, 10000, 4, soar=True)
+    assert not ix.disjoint and ix.global_topn_shift_value() == 18
+    whole = _native.NativeIndex(ix)
+    for leaves, pre, final in ((100, 100, 10), (40, 50, 20)):
+        wi, wd, wc = whole.search_batched(q, leaves, pre, final, True)
+        oi, od, oc = oracle.search(ix, q[:SUB], leaves, pre, final, True, oracle.MODE_IDEAL, 16)
+        np.testing.assert_array_equal(wc[:SUB], oc)
+        _check(wi[:SUB], wd[:SUB], oi, od)
+        si, sd, sc = _shard_search(ix, q, 8, leaves, pre, final, True)
+        np.testing.assert_array_equal(si, wi)
+        np.testing.assert_array_equal(sd.view(np.uint32), wd.view(np.uint32))
+        np.testing.assert_array_equal(sc, wc)
+    whole.close()
+
+
+def test_deep1b_shape_50000_leaves(oracle):
+    """configs[4]: 96-d, 50000 leaves (global-memory top-L, shift 16), 8-way
+    shard + merge == unsharded GPU == ideal oracle."""
+    from scann_amd import _native
+    ix, db, q = _dot96(1_000_000, 50000, 5, soar=False)
+    assert ix.global_topn_shift_value() == 16
+    whole = _native.NativeIndex(ix)
+    for leaves, pre, final in ((400, 100, 10), (1000, 100, 10)):
+        wi, wd, wc = whole.search_batched(q, leaves, pre, final, True)
+        oi, od, oc = oracle.search(ix, q[:SUB], leaves, pre, final, True, oracle.MODE_IDEAL, 16)
+        np.testing.assert_array_equal(wc[:SUB], oc)
+        _check(wi[:SUB], wd[:SUB], oi, od)
+        si, sd, sc = _shard_search(ix, q, 8, leaves, pre, final, True)
+        np.testing.assert_array_equal(si, wi)
+        np.testing.assert_array_equal(sd.view(np.uint32), wd.view(np.uint32))
+    pi, pd, pc = whole.search_pre_reorder(q[:SUB], 400, 100)
+    oi, od, oc = oracle.search_pre_reorder(ix, q[:SUB], 400, 100, oracle.MODE_IDEAL, 16)
+    _check(pi, pd, oi, od)
+    whole.close()
