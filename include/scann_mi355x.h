@@ -137,7 +137,7 @@ typedef struct smx_timings {
   int32_t max_candidates;   /* largest per-query survivor count              */
   double scan_item_tiles;   /* 32x32 MFMA tiles of the main scan (x K MFMAs)  */
   float mean_candidates;    /* survivors per query (last pass)               */
-  int32_t reserved_;
+  int32_t scan_workgroups;  /* persistent scan grid (one wave each)          */
 } smx_timings;
 
 /* Index lifecycle (ScannNumpy ctor / destructor; scann_npy.cc:57-77). */

@@ -15,7 +15,8 @@ import numpy as np
 from .index import IndexDesc
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libscann_mi355x.so")
+# SMX_LIB: an alternative build of the same library (tuning experiments)
+LIB_PATH = os.environ.get("SMX_LIB") or os.path.join(_HERE, "lib", "libscann_mi355x.so")
 
 SMX_OK = 0
 
@@ -34,7 +35,7 @@ class Timings(ctypes.Structure):
                 ("scan_pairs", ctypes.c_int32), ("seed_pairs", ctypes.c_int32),
                 ("overflow_retries", ctypes.c_int32), ("max_candidates", ctypes.c_int32),
                 ("scan_item_tiles", ctypes.c_double), ("mean_candidates", ctypes.c_float),
-                ("reserved_", ctypes.c_int32)]
+                ("scan_workgroups", ctypes.c_int32)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -14,6 +14,7 @@ constexpr int kQueriesPerTile = 32;
 constexpr int kDpPerTile = 32;
 constexpr int kMaxBlocks = 64;           // LUT16 blocks supported (K <= 32)
 constexpr uint64_t kNoThreshold = ~0ull;
+constexpr int kWorkGroups = 8;        // XCD groups of the scan's work list
 
 // Bytes of code data one lane holds per 32-datapoint tile: lane (r, h) keeps
 // the nibbles of datapoint r for blocks h, h+2, h+4, ... (K = ceil(B/2)).
@@ -53,35 +54,60 @@ struct ShardEntry {
   float exact;
 };
 
+// One work item of the scan: a chunk [j0, jend) of the 32-datapoint tiles of
+// a leaf, for one 32-query tile of that leaf's query list.
+struct WorkItem {
+  uint32_t leaf;
+  uint32_t n;            // leaf size (datapoints)
+  uint32_t j0, jend;     // tile range
+  uint64_t tile_off;     // the leaf's first code tile
+  uint64_t member_off;   // the leaf's first member
+};
+
+// Per (work item, query slot c < 32): everything the scan needs about that
+// (query, leaf) pair -- the query, the largest LUT16 sum whose distance can
+// pass its threshold (kNoSum for an empty slot), the partition distance
+// (residual bias), the query's 1/multiplier and threshold key -- so that an
+// item's setup has no dependent loads (32 B, two dwordx4 per lane).
+struct ItemLane {
+  uint32_t qid;
+  int32_t amax;
+  float bias;
+  float inv;
+  uint64_t tau;
+  uint64_t pad;
+};
+constexpr int32_t kNoSum = -2147483647 - 1;   // ItemLane::amax of an empty slot
+
 struct ScanArgs {
   const uint8_t* tiles;
-  const uint64_t* tile_off;
-  const uint32_t* leaf_size;
-  const uint64_t* member_off;
   const uint32_t* members;
   const int8_t* lut;          // [nq][2K][16]
   const float* inv;           // [nq]
-  const uint32_t* pair_q;     // queries grouped by leaf
-  const float* pair_bias;     // partition distance per pair (residual)
-  const uint32_t* pair_off;   // [nl] first pair of each leaf
-  const uint32_t* leaf_count; // [nl] pairs of each leaf
-  const uint32_t* tile_prefix;// [nl+1] work items, largest leaf first
-  const uint2* work;          // [work items] (leaf, query tile within leaf)
+  const WorkItem* work;       // [work items]
+  const ItemLane* lanes;      // [work items][32]
+  const uint4* wave_start;    // [grid] {first item, first tile, tiles, 0}
+  uint32_t num_items;
   const uint64_t* tau_key;    // [nq] emission threshold keys
   uint64_t* cand;             // [nq][cap]
   uint32_t* cand_count;       // [nq]
-  uint32_t* work_counter;
+  unsigned long long* stamps; // diagnostic variant 8 only: [cap][8] per-item stamps
+  uint32_t* stamp_count;
+  uint32_t stamp_cap;
   uint32_t cap;
-  uint32_t chunk_tiles;       // tiles per work item (LeafChunks)
   int nl;
   int nb;
   int shift;
-  int residual;
 };
 
 struct SeedArgs {
   const int32_t* topl_leaf;   // [nq][L]
   const float* topl_dist;     // [nq][L]
+  // the inversion: every (query, leaf) pair's slot in its leaf's work items
+  const uint32_t* rank;       // [nq][L] position inside the leaf's list
+  const uint32_t* leaf_item0; // [nl] the leaf's first work item
+  ItemLane* lanes;            // [work items][32]
+  uint32_t chunk_tiles;
   const int8_t* lut;          // [nq][2K][16]
   const float* inv;
   const uint8_t* tiles;
@@ -92,6 +118,7 @@ struct SeedArgs {
   int seed;
   int kk;
   int residual;
+  int nb;
 };
 
 struct SelectArgs {
@@ -138,11 +165,9 @@ struct MergeArgs {
 };
 
 // ---- launchers (smx_kernels.hip) ------------------------------------------
-hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int nq,
-                               int L, int32_t* out_leaf, float* out_dist,
-                               float* scores /*[nq][nl] scratch*/, hipStream_t s);
-// Per-call state the LUT build kernel resets on its way (no memset nodes).
-struct LutInit {
+// Per-call state the partition kernel resets on its way (no memset nodes):
+// counters to 0, candidate counts to 0, thresholds to "open".
+struct StateInit {
   uint32_t* counters = nullptr;
   uint32_t n_counters = 0;
   uint32_t* cand_count = nullptr;
@@ -150,22 +175,44 @@ struct LutInit {
   uint64_t* tau = nullptr;
   uint32_t n_tau = 0;
 };
+// The search's front end: the state reset, each (query, leaf) pair's rank in
+// the leaf's list (atomics on leaf_count) and the query's LUT16 table, all in
+// the partition / top-L launches.  NULL members are skipped.
+struct FrontArgs {
+  StateInit init;
+  uint32_t* leaf_count = nullptr;   // [nl], zeroed by init
+  uint32_t* rank = nullptr;         // [nq][L]
+  int8_t* lut = nullptr;            // [nq][2K][16]
+  float* mult = nullptr;            // [nq]
+  float* inv = nullptr;             // [nq]
+};
+hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int nq,
+                               int L, int32_t* out_leaf, float* out_dist,
+                               float* scores /*[nq][nl] scratch*/, hipStream_t s,
+                               const FrontArgs* front = nullptr);
 hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq,
                           int8_t* lut, float* mult, float* inv, uint8_t* lut_u8,
-                          hipStream_t s, const LutInit* init = nullptr);
-hipError_t LaunchPairs(const DeviceIndex& ix, const uint32_t* order /*[nl] work order*/,
-                       const int32_t* topl_leaf, const float* topl_dist, int nq, int L, uint32_t* cnt /*[nl]*/,
-                       uint32_t* block_cnt /*[ceil(nq*L/4096)][nl]*/,
-                       uint32_t* pair_off /*[nl]*/, uint32_t* tile_prefix /*[nl+1]*/,
-                       uint32_t* pair_q /*[nq*L]*/, float* pair_bias /*[nq*L]*/,
-                       uint2* work /*[max items]*/, uint32_t* totals /*[3]*/,
-                       unsigned long long* code_bytes /*[1]*/, uint32_t chunk_tiles,
-                       uint32_t queries_per_item /*32*/, hipStream_t s);
+                          hipStream_t s);
+// Leaf lists -> the scan's work items (8 XCD groups of equal MFMA work),
+// each leaf's first item, the empty query slots' lanes and every scan
+// wave's static share of its group's tiles (three launches).
+hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count,
+                          WorkItem* work /*[max items]*/, uint32_t* leaf_item0 /*[nl]*/,
+                          uint32_t* pos_unit0 /*[nl+1]*/, uint32_t* gunits /*[9]*/,
+                          ItemLane* lanes /*[max items][32]*/, uint4* wave_start /*[grid]*/,
+                          int grid, uint32_t* totals /*[3]*/,
+                          unsigned long long* code_bytes /*[1]*/, uint32_t chunk_tiles,
+                          hipStream_t s);
 // variant 0: the LUT16 scan (lut16_scan_kernel); 4: the same without its
 // threshold epilogue (timing ablation, results invalid).
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,
                       hipStream_t s);
+// Resident scan workgroups per CU (occupancy of the index's instantiation).
+hipError_t ScanBlocksPerCU(const DeviceIndex& ix, int* blocks);
 hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s);
+// After LaunchTighten: the items' lane records take the new thresholds.
+hipError_t LaunchRefreshLanes(ItemLane* lanes, uint32_t max_items, const uint32_t* totals,
+                              const uint64_t* tau_key, int nb, hipStream_t s);
 hipError_t LaunchTighten(const uint64_t* cand, const uint32_t* cand_count, uint32_t cap,
                          int nq, int kk, uint64_t* tau_key, hipStream_t s);
 // One wave per query when a.fallback is set and the buffers fit; the block

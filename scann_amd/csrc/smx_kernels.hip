@@ -5,13 +5,16 @@
 //
 //   partition_scores_kernel query tokenization on MFMA f32 32x32x2: the exact
 //                           fma chain of the transposed many-to-many path
-//                           (many_to_many_impl.inc:522-560)
+//                           (many_to_many_impl.inc:522-560); resets the
+//                           search's per-call state
 //   topl_select_kernel      exact top-L by (distance, leaf) per query
-//                           (kmeans_tree_partitioner.cc:703-728)
-//   lut_build_kernel        raw float LUT + uint8 fixed point
+//                           (kmeans_tree_partitioner.cc:703-728), each pair's
+//                           rank in its leaf's list, then the query's raw
+//                           float LUT + uint8 fixed point
 //                           (asymmetric_hashing_impl.cc:505-645)
-//   pairs_* kernels         InvertCentersToSearch on the GPU
-//                           (tree_ah_hybrid_residual.cc:610-622)
+//   worklist_kernel         InvertCentersToSearch on the GPU
+//                           (tree_ah_hybrid_residual.cc:610-622): list
+//                           offsets and the scan's work items
 //   lut16_scan_kernel<K>    THE hot loop (lut16_avx2.inc:403-526): LUT16 sums
 //                           on MFMA i32_32x32x32_i8 (one-hot codes x int8 LUT),
 //                           fused distance + threshold + candidate emission
@@ -179,7 +182,17 @@ constexpr int kPartTile = 64, kPartChunk = 32;
 
 __global__ void __launch_bounds__(256) partition_scores_kernel(
     const float* __restrict__ queries, int nq, int dim, const float* __restrict__ centers,
-    const float* __restrict__ cnorm, int nl, int metric, float* __restrict__ scores) {
+    const float* __restrict__ cnorm, int nl, int metric, float* __restrict__ scores,
+    StateInit init) {
+  {
+    // the search's per-call state (no separate memset nodes); nothing in this
+    // launch reads it, the top-L launch that follows does
+    const uint32_t gt = (blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint32_t gs = gridDim.x * gridDim.y * blockDim.x;
+    for (uint32_t i = gt; i < init.n_counters; i += gs) init.counters[i] = 0u;
+    for (uint32_t i = gt; i < init.n_cand; i += gs) init.cand_count[i] = 0u;
+    for (uint32_t i = gt; i < init.n_tau; i += gs) init.tau[i] = kNoThreshold;
+  }
   __shared__ float qs[kPartTile][kPartChunk + 1];
   __shared__ float cs[kPartTile][kPartChunk + 1];
   __shared__ float qn[kPartTile];
@@ -236,11 +249,110 @@ __global__ void __launch_bounds__(256) partition_scores_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// LUT build: raw[b][c] = -(fl(q0*c0) + fl(q1*c1)) (dot) or
+// fl(t0*t0) + fl(t1*t1), t = q - c (squared L2); multiplier
+// 127 / max(sqrt(FLT_EPSILON), max|raw|); int8 = round(raw * m) (the uint8
+// table minus its bias 128); inv = (float)(1.0/(double)m) for residual
+// indexes (lut16_avx2.inc:427-430), 1.0f/m otherwise (querying.h:450-454).
+// LUT rows are padded to 2*K blocks with zeros.
+// ---------------------------------------------------------------------------
+struct LutParams {
+  const float* queries;
+  int dim;
+  const float* codebook;
+  int nb, dpb, padded_blocks, metric, residual;
+  int8_t* lut;
+  float* mult;
+  float* inv;
+  uint8_t* lut_u8;   // optional biased uint8 copy (stage entry point)
+};
+
+// The LUT of query qi by one 256-thread block (all threads must call).
+__device__ void BuildLut(int qi, const LutParams& p) {
+  __shared__ float raw[kMaxBlocks * 16];
+  __shared__ float red[256];
+  const float* q = p.queries + size_t(qi) * p.dim;
+  const int nb = p.nb, dpb = p.dpb;
+  const int nent = nb * 16;
+  const int last = p.dim - dpb * (nb - 1);
+  float local_max = 0.0f;
+  for (int e = threadIdx.x; e < nent; e += blockDim.x) {
+    const int b = e >> 4, c = e & 15;
+    const int nd = (b == nb - 1) ? last : dpb;
+    const float* qb = q + size_t(b) * dpb;
+    const float* cb = p.codebook + (size_t(b) * 16 + c) * dpb;
+    float v;
+    if (p.metric == 0) {
+      float s = __fmul_rn(qb[0], cb[0]);
+      for (int i = 1; i < nd; ++i) s = __fadd_rn(s, __fmul_rn(qb[i], cb[i]));
+      v = -s;
+    } else {
+      float t = __fsub_rn(qb[0], cb[0]);
+      float s = __fmul_rn(t, t);
+      for (int i = 1; i < nd; ++i) {
+        const float u = __fsub_rn(qb[i], cb[i]);
+        s = __fadd_rn(s, __fmul_rn(u, u));
+      }
+      v = s;
+    }
+    raw[e] = v;
+    local_max = fmaxf(local_max, fabsf(v));
+  }
+  red[threadIdx.x] = local_max;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  const float m = __fdiv_rn(127.0f, fmaxf(SqrtFltEps(), red[0]));
+  const int tot = p.padded_blocks * 16;
+  for (int e = threadIdx.x; e < tot; e += blockDim.x) {
+    int8_t v8 = 0;
+    if (e < nent) {
+      const float r = roundf(__fmul_rn(raw[e], m));
+      v8 = int8_t(int(r));
+      if (p.lut_u8) p.lut_u8[size_t(qi) * nent + e] = uint8_t(int(r) + 128);
+    }
+    p.lut[size_t(qi) * tot + e] = v8;
+  }
+  if (threadIdx.x == 0) {
+    p.mult[qi] = m;
+    p.inv[qi] = p.residual ? float(1.0 / double(m)) : __fdiv_rn(1.0f, m);
+  }
+}
+
+__global__ void __launch_bounds__(256) lut_build_kernel(LutParams p) { BuildLut(blockIdx.x, p); }
+
 // Exact top-L per query by (score, center index) from the score matrix.
+// The front end's per-query tail, shared by both top-L kernels: the
+// selected pairs' ranks in their leaves' lists, then the query's LUT.
+struct TopLTail {
+  uint32_t* leaf_count;   // or NULL
+  uint32_t* rank;
+  LutParams lut;          // lut.lut NULL: no LUT
+};
+
+__device__ void TopLFinish(int qi, int L, uint32_t m, const uint64_t* sel, int32_t* out_leaf,
+                           float* out_dist, const TopLTail& tail) {
+  for (int i = threadIdx.x; i < L; i += blockDim.x) {
+    const bool has = uint32_t(i) < m;
+    const int32_t leaf = has ? int32_t(sel[i] & 0xFFFFFFFFu) : -1;
+    out_leaf[size_t(qi) * L + i] = leaf;
+    out_dist[size_t(qi) * L + i] = has ? FromOrdered(uint32_t(sel[i] >> 32)) : __int_as_float(0x7fc00000);
+    if (tail.leaf_count && has) tail.rank[size_t(qi) * L + i] = atomicAdd(&tail.leaf_count[leaf], 1u);
+  }
+  if (tail.lut.lut) {
+    __syncthreads();
+    BuildLut(qi, tail.lut);
+  }
+}
+
 __global__ void __launch_bounds__(256) topl_select_kernel(const float* __restrict__ scores, int nl,
                                                           int L, uint32_t kcap,
                                                           int32_t* __restrict__ out_leaf,
-                                                          float* __restrict__ out_dist) {
+                                                          float* __restrict__ out_dist,
+                                                          TopLTail tail) {
   extern __shared__ uint64_t lds64[];
   uint64_t* keys = lds64;
   uint64_t* sel = keys + kcap;
@@ -252,11 +364,7 @@ __global__ void __launch_bounds__(256) topl_select_kernel(const float* __restric
     keys[c] = (uint64_t(OrderedBits(scores[size_t(qi) * nl + c])) << 32) | uint32_t(c);
   __syncthreads();
   const uint32_t m = SelectSmallest(keys, uint32_t(nl), uint32_t(L), sel, selcap, hist, scan_buf);
-  for (int i = threadIdx.x; i < L; i += blockDim.x) {
-    const bool has = uint32_t(i) < m;
-    out_leaf[size_t(qi) * L + i] = has ? int32_t(sel[i] & 0xFFFFFFFFu) : -1;
-    out_dist[size_t(qi) * L + i] = has ? FromOrdered(uint32_t(sel[i] >> 32)) : __int_as_float(0x7fc00000);
-  }
+  TopLFinish(qi, L, m, sel, out_leaf, out_dist, tail);
 }
 
 // Above this many leaves the score row is selected from global memory.
@@ -272,7 +380,8 @@ constexpr int kLdsSelectLeaves = 16384;
 __global__ void __launch_bounds__(256) topl_select_global_kernel(const float* __restrict__ scores,
                                                                  int nl, int L, uint32_t lcap,
                                                                  int32_t* __restrict__ out_leaf,
-                                                                 float* __restrict__ out_dist) {
+                                                                 float* __restrict__ out_dist,
+                                                                 TopLTail tail) {
   extern __shared__ uint64_t lds64[];
   uint64_t* sel = lds64;
   __shared__ uint32_t hist[256];
@@ -345,254 +454,216 @@ __global__ void __launch_bounds__(256) topl_select_global_kernel(const float* __
   for (uint32_t i = m + threadIdx.x; i < lcap; i += blockDim.x) sel[i] = ~0ull;
   __syncthreads();
   BitonicSort(sel, lcap);
-  for (int i = threadIdx.x; i < L; i += blockDim.x) {
-    const bool has = uint32_t(i) < m;
-    out_leaf[size_t(qi) * L + i] = has ? int32_t(sel[i] & 0xFFFFFFFFu) : -1;
-    out_dist[size_t(qi) * L + i] = has ? FromOrdered(uint32_t(sel[i] >> 32)) : __int_as_float(0x7fc00000);
-  }
+  TopLFinish(qi, L, m, sel, out_leaf, out_dist, tail);
 }
 
-// ---------------------------------------------------------------------------
-// LUT build: raw[b][c] = -(fl(q0*c0) + fl(q1*c1)) (dot) or
-// fl(t0*t0) + fl(t1*t1), t = q - c (squared L2); multiplier
-// 127 / max(sqrt(FLT_EPSILON), max|raw|); int8 = round(raw * m) (the uint8
-// table minus its bias 128); inv = (float)(1.0/(double)m) for residual
-// indexes (lut16_avx2.inc:427-430), 1.0f/m otherwise (querying.h:450-454).
-// LUT rows are padded to 2*K blocks with zeros.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) lut_build_kernel(
-    const float* __restrict__ queries, int dim, const float* __restrict__ codebook,
-    int nb, int dpb, int padded_blocks, int metric, int residual,
-    int8_t* __restrict__ lut, float* __restrict__ mult, float* __restrict__ inv,
-    uint8_t* __restrict__ lut_u8, LutInit init) {
-  __shared__ float raw[kMaxBlocks * 16];
-  __shared__ float red[256];
-  {
-    // the search's per-call state, reset here instead of by separate memset
-    // nodes: counters and candidate counts to 0, thresholds to "open"
-    const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x, gs = gridDim.x * blockDim.x;
-    for (uint32_t i = gt; i < init.n_counters; i += gs) init.counters[i] = 0u;
-    for (uint32_t i = gt; i < init.n_cand; i += gs) init.cand_count[i] = 0u;
-    for (uint32_t i = gt; i < init.n_tau; i += gs) init.tau[i] = kNoThreshold;
-  }
-  const int qi = blockIdx.x;
-  const float* q = queries + size_t(qi) * dim;
-  const int nent = nb * 16;
-  const int last = dim - dpb * (nb - 1);
-  float local_max = 0.0f;
-  for (int e = threadIdx.x; e < nent; e += blockDim.x) {
-    const int b = e >> 4, c = e & 15;
-    const int nd = (b == nb - 1) ? last : dpb;
-    const float* qb = q + size_t(b) * dpb;
-    const float* cb = codebook + (size_t(b) * 16 + c) * dpb;
-    float v;
-    if (metric == 0) {
-      float s = __fmul_rn(qb[0], cb[0]);
-      for (int i = 1; i < nd; ++i) s = __fadd_rn(s, __fmul_rn(qb[i], cb[i]));
-      v = -s;
-    } else {
-      float t = __fsub_rn(qb[0], cb[0]);
-      float s = __fmul_rn(t, t);
-      for (int i = 1; i < nd; ++i) {
-        const float u = __fsub_rn(qb[i], cb[i]);
-        s = __fadd_rn(s, __fmul_rn(u, u));
-      }
-      v = s;
-    }
-    raw[e] = v;
-    local_max = fmaxf(local_max, fabsf(v));
-  }
-  red[threadIdx.x] = local_max;
-  __syncthreads();
-  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
-    __syncthreads();
-  }
-  const float m = __fdiv_rn(127.0f, fmaxf(SqrtFltEps(), red[0]));
-  const int tot = padded_blocks * 16;
-  for (int e = threadIdx.x; e < tot; e += blockDim.x) {
-    int8_t v8 = 0;
-    if (e < nent) {
-      const float r = roundf(__fmul_rn(raw[e], m));
-      v8 = int8_t(int(r));
-      if (lut_u8) lut_u8[size_t(qi) * nent + e] = uint8_t(int(r) + 128);
-    }
-    lut[size_t(qi) * tot + e] = v8;
-  }
-  if (threadIdx.x == 0) {
-    mult[qi] = m;
-    inv[qi] = residual ? float(1.0 / double(m)) : __fdiv_rn(1.0f, m);
-  }
-}
+constexpr int kGroups = kWorkGroups;   // XCD groups of the work list
 
-// Work items split a leaf's 32-datapoint tiles into chunks of at most
-// chunk_tiles so that no single wave (or block) owns a whole large leaf.
+// Work items split a leaf's 32-datapoint tiles into LeafChunks equal chunks
+// of at most chunk_tiles tiles (37 tiles at 32 -> 19 + 18, not 32 + 5), so
+// that no single wave owns a whole large leaf and no item is a short tail.
 __device__ __forceinline__ uint32_t LeafChunks(uint32_t n, uint32_t chunk_tiles) {
   const uint32_t tiles = (n + 31u) / 32u;
   return tiles == 0 ? 1u : (tiles + chunk_tiles - 1) / chunk_tiles;
 }
-
-// ---------------------------------------------------------------------------
-// Invert (query -> leaves) into (leaf -> queries) and cut every leaf's query
-// list into 32-query work items, listed largest leaf first (longest items
-// dequeued first).
-// ---------------------------------------------------------------------------
-// Block-local counting: every block histograms kPairsPerBlock pairs in LDS and
-// publishes one count per (block, leaf) -- no contended global atomics.
-constexpr int kPairsPerBlock = 4096;
-constexpr int kLeafRange = 16384;   // leaves per LDS counter range (64 KiB)
-
-__global__ void __launch_bounds__(256) pairs_count_kernel(const int32_t* __restrict__ topl_leaf,
-                                                          int n, int nl,
-                                                          uint32_t* __restrict__ block_cnt,
-                                                          uint32_t* __restrict__ cnt) {
-  extern __shared__ uint32_t hist[];
-  // blockIdx.y selects a range of kLeafRange leaves (indexes whose per-leaf
-  // counters exceed LDS, e.g. 50000 leaves)
-  const int l0 = blockIdx.y * kLeafRange, nr = min(kLeafRange, nl - l0);
-  for (int l = threadIdx.x; l < nr; l += blockDim.x) hist[l] = 0;
-  __syncthreads();
-  const int beg = blockIdx.x * kPairsPerBlock, end = min(n, beg + kPairsPerBlock);
-  for (int i = beg + threadIdx.x; i < end; i += blockDim.x) {
-    const int leaf = topl_leaf[i] - l0;
-    if (leaf >= 0 && leaf < nr) atomicAdd(&hist[leaf], 1u);
-  }
-  __syncthreads();
-  uint32_t* bc = block_cnt + size_t(blockIdx.x) * nl + l0;
-  for (int l = threadIdx.x; l < nr; l += blockDim.x) {
-    const uint32_t c = hist[l];
-    bc[l] = c;
-    if (c) atomicAdd(&cnt[l0 + l], c);
-  }
+// Tiles [begin, end) of chunk `chunk` of a leaf of n datapoints.
+__device__ __forceinline__ uint2 ChunkTiles(uint32_t n, uint32_t chunk_tiles, uint32_t chunk) {
+  const uint32_t tiles = (n + 31u) / 32u;
+  const uint32_t chunks = tiles == 0 ? 1u : (tiles + chunk_tiles - 1) / chunk_tiles;
+  return make_uint2((tiles * chunk) / chunks, (tiles * (chunk + 1)) / chunks);
 }
 
-// Exclusive prefix over blocks for every leaf: block b's first slot in leaf l.
-__global__ void pairs_block_offsets_kernel(uint32_t* __restrict__ block_cnt, int nblocks, int nl) {
-  const int l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= nl) return;
-  uint32_t run = 0;
-  for (int b = 0; b < nblocks; ++b) {
-    const uint32_t c = block_cnt[size_t(b) * nl + l];
-    block_cnt[size_t(b) * nl + l] = run;
-    run += c;
-  }
+// ---------------------------------------------------------------------------
+// Invert (query -> leaves) into (leaf -> queries): InvertCentersToSearch
+// (tree_ah_hybrid_residual.cc:610-622).  The top-L kernel gives every
+// (query, leaf) pair its rank inside the leaf's list (an atomic on the leaf's
+// count); worklist_kernel turns the counts into list offsets and the scan's
+// work items; the seed kernel scatters each query's pairs to
+// pair_off[leaf] + rank.  The order of the queries inside a leaf's list is
+// therefore not the query order; nothing depends on it (every result is an
+// exact top-k under a total order).
+//
+// Work items = (leaf, 32-query tile, chunk of <= chunk_tiles tiles), listed
+// largest leaf first, cut into 8 XCD groups of consecutive leaves with equal
+// MFMA work (exclusive work prefix x 8 / total work), so that all items of a
+// leaf share a group.
+// ---------------------------------------------------------------------------
+// Per leaf: its query tiles, MFMA tiles (= the scan's work units) and items.
+__device__ __forceinline__ uint32_t LeafUnits(uint32_t c, uint32_t n, uint32_t chunk_tiles,
+                                              uint32_t& items) {
+  const uint32_t qt = (c + kQueriesPerTile - 1) / kQueriesPerTile;
+  items = qt * LeafChunks(n, chunk_tiles);
+  return qt * ((n + 31u) / 32u);
 }
 
-__global__ void __launch_bounds__(1024) pairs_scan_kernel(const uint32_t* __restrict__ cnt,
-                                                          const uint32_t* __restrict__ order,
-                                                          const uint32_t* __restrict__ leaf_size,
-                                                          int nl, int nb, uint32_t chunk_tiles,
-                                                          uint32_t qpi,
-                                                          uint32_t* __restrict__ pair_off,
-                                                          uint32_t* __restrict__ tile_prefix,
-                                                          uint32_t* __restrict__ totals,
-                                                          unsigned long long* __restrict__ code_bytes,
-                                                          uint2* __restrict__ work,
-                                                          uint32_t* __restrict__ block_cnt,
-                                                          int fused_blocks) {
-  // small trees: the per-leaf exclusive prefix over the counting blocks
-  // (pairs_block_offsets_kernel) is done here, 8 loads in flight per step
-  for (int l = threadIdx.x; l < nl && fused_blocks > 0; l += blockDim.x) {
-    uint32_t run = 0;
-    for (int b0 = 0; b0 < fused_blocks; b0 += 8) {
-      uint32_t v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        v[u] = b0 + u < fused_blocks ? block_cnt[size_t(b0 + u) * nl + l] : 0u;
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (b0 + u < fused_blocks) {
-          block_cnt[size_t(b0 + u) * nl + l] = run;
-          run += v[u];
-        }
-    }
-  }
-  __shared__ uint32_t s_pairs[1024];
-  __shared__ uint32_t s_tiles[1024];
+// Phase 1 (one block): prefixes over the leaves in work order -- each leaf's
+// first item (leaf_item0) and first unit (pos_unit0, by position), the 8
+// groups' unit boundaries (gunits[0..8]; gunits[8] = all units) -- and the
+// totals.
+__global__ void __launch_bounds__(1024) worklist_kernel(
+    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ order,
+    const uint32_t* __restrict__ leaf_size, int nl, int nb, uint32_t chunk_tiles,
+    uint32_t* __restrict__ leaf_item0, uint32_t* __restrict__ pos_unit0,
+    uint32_t* __restrict__ gunits, uint32_t* __restrict__ totals,
+    unsigned long long* __restrict__ code_bytes) {
+  __shared__ uint32_t s_items[1024], s_wt[1024], s_pairs[1024];
   __shared__ unsigned long long s_bytes[1024];
-  const int per = (nl + blockDim.x - 1) / blockDim.x;
-  const int beg = threadIdx.x * per;
+  const int tid = threadIdx.x;
+  const int nt = blockDim.x;
+  const int per = (nl + nt - 1) / nt;
+  const int beg = tid * per;
   const int end = min(nl, beg + per);
-  uint32_t sp = 0, st = 0, sit = 0;
+  uint32_t sp = 0, st = 0, sw = 0;
   unsigned long long sb = 0;
   for (int p = beg; p < end; ++p) {
     const uint32_t leaf = order[p];
-    const uint32_t c = cnt[leaf];
+    const uint32_t c = cnt[leaf], n = leaf_size[leaf];
+    uint32_t items;
+    sw += LeafUnits(c, n, chunk_tiles, items);
+    st += items;
     sp += c;
-    st += ((c + qpi - 1) / qpi) * LeafChunks(leaf_size[leaf], chunk_tiles);
-    sit += ((c + kQueriesPerTile - 1) / kQueriesPerTile) * ((leaf_size[leaf] + 31u) / 32u);
     // algorithmic code bytes: 16 * B * ceil(n / 32) per (query, leaf) pair
-    sb += 16ull * nb * ((leaf_size[leaf] + 31u) / 32u) * c;
+    sb += 16ull * nb * ((n + 31u) / 32u) * c;
   }
-  s_pairs[threadIdx.x] = sp;
-  s_tiles[threadIdx.x] = st;
-  s_bytes[threadIdx.x] = sb;
+  s_items[tid] = st;
+  s_wt[tid] = sw;
+  s_pairs[tid] = sp;
+  s_bytes[tid] = sb;
   __syncthreads();
-  for (int off = int(blockDim.x) / 2; off > 0; off >>= 1) {
-    if (int(threadIdx.x) < off) s_bytes[threadIdx.x] += s_bytes[threadIdx.x + off];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) code_bytes[0] = s_bytes[0];
-  __syncthreads();
-  s_tiles[threadIdx.x] = sit;   // reuse: item-tiles (MFMA tile count) reduction
-  __syncthreads();
-  for (int off = int(blockDim.x) / 2; off > 0; off >>= 1) {
-    if (int(threadIdx.x) < off) s_tiles[threadIdx.x] += s_tiles[threadIdx.x + off];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) totals[2] = s_tiles[0];
-  __syncthreads();
-  s_tiles[threadIdx.x] = st;
-  for (int off = 1; off < int(blockDim.x); off <<= 1) {
-    uint32_t a = 0, b = 0;
-    if (int(threadIdx.x) >= off) {
-      a = s_pairs[threadIdx.x - off];
-      b = s_tiles[threadIdx.x - off];
+  for (int off = nt / 2; off > 0; off >>= 1) {
+    if (tid < off) {
+      s_bytes[tid] += s_bytes[tid + off];
+      s_pairs[tid] += s_pairs[tid + off];
     }
     __syncthreads();
-    s_pairs[threadIdx.x] += a;
-    s_tiles[threadIdx.x] += b;
+  }
+  if (tid == 0) {
+    code_bytes[0] = s_bytes[0];
+    totals[0] = s_pairs[0];
+  }
+  for (int off = 1; off < nt; off <<= 1) {
+    uint32_t y = 0, z = 0;
+    if (tid >= off) {
+      y = s_items[tid - off];
+      z = s_wt[tid - off];
+    }
+    __syncthreads();
+    s_items[tid] += y;
+    s_wt[tid] += z;
     __syncthreads();
   }
-  uint32_t rp = threadIdx.x ? s_pairs[threadIdx.x - 1] : 0;
-  uint32_t rt = threadIdx.x ? s_tiles[threadIdx.x - 1] : 0;
+  const uint32_t total_w = s_wt[nt - 1];
+  const uint64_t wdiv = max(1u, total_w);
+  uint32_t rt = tid ? s_items[tid - 1] : 0;
+  uint32_t rw = tid ? s_wt[tid - 1] : 0;
+  // group boundaries: the first position whose exclusive unit prefix puts it
+  // in group g (g = 8 * prefix / total); the groups are contiguous ranges
+  auto group_of = [&](uint32_t excl_w) {
+    return int(min<uint64_t>(kGroups - 1, (uint64_t(kGroups) * excl_w) / wdiv));
+  };
+  int prev = tid == 0 ? -1 : (beg < end ? group_of(rw) : kGroups);
+  if (tid > 0 && beg < end) {
+    // group of the previous thread's last position
+    const int pp = beg - 1;
+    const uint32_t leaf = order[pp];
+    uint32_t items;
+    prev = group_of(rw - LeafUnits(cnt[leaf], leaf_size[leaf], chunk_tiles, items));
+  }
   for (int p = beg; p < end; ++p) {
     const uint32_t leaf = order[p];
-    const uint32_t c = cnt[leaf];
-    pair_off[leaf] = rp;
-    tile_prefix[p] = rt;
-    rp += c;
-    // this leaf's work items: (leaf, query tile << 16 | dp chunk)
-    const uint32_t chunks = LeafChunks(leaf_size[leaf], chunk_tiles);
-    const uint32_t items = ((c + qpi - 1) / qpi) * chunks;
-    for (uint32_t u = 0; u < items; ++u)
-      work[rt + u] = make_uint2(leaf, ((u / chunks) << 16) | (u % chunks));
+    const int gp = group_of(rw);
+    for (int gg = prev + 1; gg <= gp; ++gg) gunits[gg] = rw;
+    prev = gp;
+    leaf_item0[leaf] = rt;
+    pos_unit0[p] = rw;
+    uint32_t items;
+    rw += LeafUnits(cnt[leaf], leaf_size[leaf], chunk_tiles, items);
     rt += items;
   }
-  if (threadIdx.x == blockDim.x - 1) {
-    tile_prefix[nl] = s_tiles[blockDim.x - 1];
-    totals[0] = s_pairs[blockDim.x - 1];
-    totals[1] = s_tiles[blockDim.x - 1];
+  if (beg < end && end == nl) {
+    for (int gg = prev + 1; gg <= kGroups; ++gg) gunits[gg] = total_w;
+    pos_unit0[nl] = total_w;
+  }
+  if (tid == 0) {
+    totals[1] = s_items[nt - 1];
+    totals[2] = total_w;
   }
 }
 
-__global__ void __launch_bounds__(256) pairs_scatter_kernel(
-    const int32_t* __restrict__ topl_leaf, const float* __restrict__ topl_dist, int n, int L, int nl,
-    const uint32_t* __restrict__ pair_off, const uint32_t* __restrict__ block_off,
-    uint32_t* __restrict__ pair_q, float* __restrict__ pair_bias) {
-  extern __shared__ uint32_t fill[];
-  const int l0 = blockIdx.y * kLeafRange, nr = min(kLeafRange, nl - l0);
-  for (int l = threadIdx.x; l < nr; l += blockDim.x) fill[l] = 0;
-  __syncthreads();
-  const uint32_t* bo = block_off + size_t(blockIdx.x) * nl;
-  const int beg = blockIdx.x * kPairsPerBlock, end = min(n, beg + kPairsPerBlock);
-  for (int i = beg + threadIdx.x; i < end; i += blockDim.x) {
-    const int leaf = topl_leaf[i];
-    if (leaf < l0 || leaf >= l0 + nr) continue;
-    const uint32_t pos = pair_off[leaf] + bo[leaf] + atomicAdd(&fill[leaf - l0], 1u);
-    pair_q[pos] = uint32_t(i / L);
-    pair_bias[pos] = topl_dist[i];
+// Phase 2 (one 64-thread block per leaf position): the leaf's work items,
+// the empty query slots of its last query tile, and the start of every scan
+// wave whose share begins inside this leaf.  Wave i of group g (i % 8 == g)
+// takes the units [U0 + span * k / n, U0 + span * (k + 1) / n) of its
+// group, k = i / 8 of the group's n waves.
+__global__ void __launch_bounds__(64) items_kernel(
+    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ order,
+    const uint32_t* __restrict__ leaf_size, const uint64_t* __restrict__ tile_off,
+    const uint64_t* __restrict__ member_off, uint32_t chunk_tiles, int grid,
+    const uint32_t* __restrict__ leaf_item0, const uint32_t* __restrict__ pos_unit0,
+    const uint32_t* __restrict__ gunits, WorkItem* __restrict__ work,
+    ItemLane* __restrict__ lanes, uint4* __restrict__ wave_start) {
+  const int p = blockIdx.x, lane = threadIdx.x;
+  const uint32_t leaf = order[p];
+  const uint32_t c = cnt[leaf], n = leaf_size[leaf];
+  const uint32_t chunks = LeafChunks(n, chunk_tiles);
+  const uint32_t qt = (c + kQueriesPerTile - 1) / kQueriesPerTile;
+  const uint32_t item0 = leaf_item0[leaf];
+  const uint64_t toff = tile_off[leaf], moff = member_off[leaf];
+  for (uint32_t u = lane; u < qt * chunks; u += 64) {
+    const uint2 cr = ChunkTiles(n, chunk_tiles, u % chunks);
+    WorkItem it;
+    it.leaf = leaf;
+    it.n = n;
+    it.j0 = cr.x;
+    it.jend = cr.y;
+    it.tile_off = toff;
+    it.member_off = moff;
+    work[item0 + u] = it;
   }
+  if (qt) {
+    const uint32_t first = c - (qt - 1) * kQueriesPerTile;   // empty slots [first, 32)
+    const uint32_t ne = kQueriesPerTile - first;
+    for (uint32_t e = lane; e < ne * chunks; e += 64) {
+      ItemLane v;
+      v.qid = 0;
+      v.amax = kNoSum;
+      v.bias = 0.0f;
+      v.inv = 0.0f;
+      v.tau = 0;
+      v.pad = 0;
+      lanes[size_t(item0 + (qt - 1) * chunks + e / ne) * kQueriesPerTile + first + e % ne] = v;
+    }
+  }
+  // the waves whose share starts in this leaf's units [ua, ub)
+  const uint32_t ua = pos_unit0[p], ub = pos_unit0[p + 1];
+  if (ua >= ub) return;
+  const uint32_t wdiv = max(1u, gunits[kGroups]);
+  const int g = int(min<uint64_t>(kGroups - 1, (uint64_t(kGroups) * ua) / wdiv));
+  const uint32_t nw = uint32_t(grid - g + kGroups - 1) / kGroups;
+  const uint32_t U0 = gunits[g], span = gunits[g + 1] - U0;
+  // the first k with U0 + span*k/nw >= ua
+  uint32_t k = uint32_t((uint64_t(ua - U0) * nw + span - 1) / span);
+  const uint32_t tiles = (n + 31u) / 32u;
+  for (k += lane;; k += 64) {
+    if (k >= nw) break;
+    const uint32_t us = U0 + uint32_t((uint64_t(span) * k) / nw);
+    if (us >= ub) break;
+    const uint32_t ue = U0 + uint32_t((uint64_t(span) * (k + 1)) / nw);
+    const uint32_t off = us - ua, tq = off / tiles, rem = off % tiles;
+    uint32_t ch = 0;
+    while (ChunkTiles(n, chunk_tiles, ch).y <= rem) ++ch;
+    wave_start[kGroups * k + g] = make_uint4(item0 + tq * chunks + ch, rem, ue - us, 0);
+  }
+}
+
+// Waves of groups with no units at all (or of a grid too short for the
+// snake above) get an empty share.
+__global__ void wave_clear_kernel(const uint32_t* __restrict__ gunits, int grid,
+                                  uint4* __restrict__ wave_start) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= grid) return;
+  const int g = i & (kGroups - 1);
+  if (gunits[g + 1] == gunits[g]) wave_start[i] = make_uint4(0, 0, 0, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -700,8 +771,10 @@ __device__ __forceinline__ uint32_t BlockInclusiveScan256(uint32_t v, uint32_t* 
   return v;
 }
 
+// The threshold key of query qi from its seed leaves, or kNoThreshold (no
+// bound); block-wide (256 threads, all call; the value is returned to all).
 template <int K>
-__global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
+__device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
   constexpr int W = 4 * NW;
   constexpr int U = 4;   // datapoints whose code loads are in flight together
@@ -711,7 +784,9 @@ __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
   __shared__ uint64_t s_tile0[kSeedMaxLeaves];
   __shared__ float s_bias[kSeedMaxLeaves];
   __shared__ uint32_t wsum[4], s_lo[4], s_hi[4], s_bin, s_below;
-  const int qi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ uint64_t s_T;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (a.seed <= 0) return kNoThreshold;
   for (int e = tid; e < 2 * K * 16; e += 256) lut[e] = a.lut[size_t(qi) * 2 * K * 16 + e];
   const float inv = a.inv[qi];
   const int nseed = min(a.seed, min(a.L, kSeedMaxLeaves));
@@ -732,7 +807,7 @@ __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
   __syncthreads();
   const uint32_t total = min(s_start[kSeedMaxLeaves], kSeedCap);
   const uint32_t kk = uint32_t(a.kk);
-  if (kk == 0 || total < kk) return;   // no bound: the threshold stays open
+  if (kk == 0 || total < kk) return kNoThreshold;   // no bound: the threshold stays open
 
   uint32_t vals[kSeedPerThread];
   int r = 0;   // seed leaf of this thread's current number (numbers only grow)
@@ -811,153 +886,273 @@ __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
     hi = bhi;
     __syncthreads();   // hist, wsum and s_bin are rewritten by the next round
   }
-  if (tid == 0) {
-    const uint64_t t = (uint64_t(hi) << 32) | 0xFFFFFFFFull;
-    if (t < a.tau_key[qi]) a.tau_key[qi] = t;
+  if (tid == 0) s_T = (uint64_t(hi) << 32) | 0xFFFFFFFFull;
+  __syncthreads();
+  return s_T;
+}
+
+// Per query: its threshold (SeedTau), then its (query, leaf) pairs into the
+// scan's work-item lanes -- slot rank % 32 of query tile rank / 32, in every
+// chunk of the leaf -- with the pair's bias and sum limit.  This is the
+// scatter half of InvertCentersToSearch (tree_ah_hybrid_residual.cc:610-622).
+template <int K>
+__global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
+  const int qi = blockIdx.x;
+  const uint64_t T = SeedTau<K>(a, qi);
+  if (threadIdx.x == 0) a.tau_key[qi] = T;
+  const float inv = a.inv[qi];
+  const int smin = -128 * a.nb, smax = 128 * a.nb;
+  for (int i = threadIdx.x; i < a.L; i += blockDim.x) {
+    const int32_t leaf = a.topl_leaf[size_t(qi) * a.L + i];
+    if (leaf < 0) continue;
+    const uint32_t r = a.rank[size_t(qi) * a.L + i];
+    const uint32_t n = a.leaf_size[leaf];
+    const uint32_t chunks = LeafChunks(n, a.chunk_tiles);
+    const float bias = a.residual ? a.topl_dist[size_t(qi) * a.L + i] : 0.0f;
+    ItemLane v;
+    v.qid = uint32_t(qi);
+    v.amax = T == kNoThreshold ? smax : SumLimit(FromOrdered(uint32_t(T >> 32)), inv, bias, smin, smax);
+    v.bias = bias;
+    v.inv = inv;
+    v.tau = T;
+    v.pad = 0;
+    const uint32_t w0 = a.leaf_item0[leaf] + (r / kQueriesPerTile) * chunks;
+    for (uint32_t ch = 0; ch < chunks; ++ch) a.lanes[size_t(w0 + ch) * kQueriesPerTile + (r % kQueriesPerTile)] = v;
   }
 }
 
 
-// K MFMAs of one tile.  The one-hot A fragments come from a 16-entry LDS
-// table (oh_tab[t] = 16 bytes with byte t = 1): per MFMA one nibble
-// extraction and two ds_read_b128, both conflict-free (the table spans the 64
-// banks exactly; a step's B rows are 1 KiB contiguous per wave).  Both are
-// read R steps ahead of their MFMA, and a full scheduling barrier closes each
-// step so the compiler cannot collapse the ring.
-constexpr int kRing = 4;
-template <int K, int Q, int R = kRing>
-__device__ __forceinline__ v16i TileMfma(const uint32_t* codes, const v4i* lut, int off,
+// K MFMAs of one tile with the item's B fragments (LUT rows) held in
+// registers.  The one-hot A fragments come from a 16-entry LDS table
+// (oh_tab[t] = 16 bytes with byte t = 1): per MFMA one nibble extraction and
+// one ds_read_b128 (conflict-free: the table spans the 64 banks exactly, and
+// equal entries broadcast), read R steps ahead of their MFMA; a scheduling
+// barrier closes each step so the compiler cannot collapse the ring.
+template <int K, int R>
+__device__ __forceinline__ v16i TileMfma(const uint32_t* codes, const v4i (&b)[K],
                                          const v4i* oh_tab) {
-  asm volatile("" : "+v"(off));
-  v4i b[R], o[R];
+  v4i o[R];
 #pragma unroll
   for (int p = 0; p < R; ++p)
-    if (p < K) {
-      b[p] = lut[2 * p * Q + off];
-      o[p] = oh_tab[(codes[p >> 3] >> ((p & 7) * 4)) & 15u];
-    }
+    if (p < K) o[p] = oh_tab[(codes[p >> 3] >> ((p & 7) * 4)) & 15u];
   v16i acc = v16i{0};
 #pragma unroll
   for (int s = 0; s < K; ++s) {
-    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(o[s % R], b[s % R], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(o[s % R], b[s], acc, 0, 0, 0);
     if (s + R < K) {
       const int t = s + R;
-      b[s % R] = lut[2 * t * Q + off];
       o[s % R] = oh_tab[(codes[t >> 3] >> ((t & 7) * 4)) & 15u];
     }
-    __builtin_amdgcn_sched_barrier(0);
+  }
+  // the order the machine scheduler must keep: the ring's first R reads,
+  // then MFMA s followed by the read of step s + R (the DAG builder would
+  // otherwise issue every read first and sink the MFMAs to their use); the
+  // next tile's code load (issued by the caller just before) goes right
+  // after the first MFMA -- after this tile's address arithmetic, so no wait
+  // for it is placed in front of that, and before the rest of the MFMAs, so
+  // that its latency hides behind them
+  __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if (s == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    if (s + R < K) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
   }
   return acc;
 }
 
 // ---------------------------------------------------------------------------
-// The scan kernel.  Persistent blocks claim items from a work counter
-// (largest leaves first).  Per item: the 32 queries' parameters and LUT rows
-// go to LDS ([row][query] x 16 B), the 4 waves take the chunk's tiles
-// round-robin (code tile j+4 prefetched while tile j computes).  The
-// threshold epilogue is split in two: in the tile loop a lane whose 16-sum
-// minimum passes only appends its sums (packed int16) and a tag to its wave's
-// LDS hit list; drain() runs the per-element test, the key and the exact
-// threshold compare lane-parallel over the hits, once per item (or when the
-// list fills), and stages survivors per query in LDS: one global atomic per
-// query per item.
+// The scan kernel: one wave per workgroup, every wave an independent
+// persistent worker with a static share of the work (no dequeue atomics --
+// a returning device-scope atomic costs microseconds under this load -- no
+// workgroup barriers, no LUT staging).
+//
+// Work items (leaf, 32-query tile of that leaf, chunk of <= chunk_tiles
+// 32-datapoint tiles) are listed in 8 groups of consecutive leaves with equal
+// MFMA work, one per XCD group (blockIdx % 8 share an XCD under the observed
+// round-robin placement; speed only, never correctness), so a leaf's query
+// tiles run on one XCD and re-read the leaf's codes from that XCD's L2.  The
+// worklist kernel cuts each group's tiles into equal contiguous shares, one
+// per wave of the group (wave_start): a share may begin and end inside an
+// item.  Each item's descriptor and lane record are loaded one item ahead.
+//
+// Per item: lane (c, h) takes its query slot's record (query, sum limit,
+// bias; written by the seed kernel), loads the int8 LUT rows 2s+h, s < K, of
+// query c into K registers (the MFMA B fragments for the whole item); then
+// for each tile K x MFMA i32_32x32x32_i8 with A = one-hot codes (row =
+// datapoint, 16 bytes per lane-half = one block's 16 centers) gives
+// S[dp][q] = sum_b LUT_q[b][code(dp, b)] exactly (|S| <= 127*B).  A datapoint
+// can only pass when S <= amax_q (the largest sum whose distance can pass the
+// query's threshold; d is monotone in S); a lane whose 16-sum minimum passes
+// appends its sums (packed int16) and a tag to the wave's LDS hit list;
+// drain() runs the per-element test, the distance
+//     d = fl(fl(float(S) * inv_q) + bias_{q,leaf})
+// and the key test (ordered(d) << 32 | tie) <= threshold key lane-parallel
+// over the hits, and stages the item's survivors in LDS: one global atomic per
+// query per item reserves their list slots (issued at the item's end, its
+// result consumed at the next item's start, behind that item's loads).
 // ABL = 4: timing ablation without the epilogue (results invalid).
 // ---------------------------------------------------------------------------
-constexpr int kHitsPerWave = 64;   // >= 64: a tile may add a hit per lane right after a drain
-constexpr int kQStageHits = 16;
+// LDS hand-off between the lanes of ONE wave (the scan's workgroups are a
+// single wave): a wave's DS instructions execute in issue order, so all that
+// is needed is that the compiler keeps them in program order and that the
+// wave's outstanding LDS operations are complete.  Unlike __syncthreads()
+// this does not wait for the wave's global loads (the code-tile and next-item
+// prefetches stay in flight).
+__device__ __forceinline__ void WaveLdsSync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
 
+constexpr int kHitsPerWave = 64;   // a tile adds at most one hit per lane
+constexpr int kItemKeys = 256;   // survivors one work item stages in LDS
+
+// Diagnostic stamps (ABL & 8; a separate buffer that nothing else reads):
+// per item {hw_id, xcc_id << 32 | item, realtime, memtime at the item's
+// start, after its setup, after its tiles, after its flush,
+// tiles | hit lanes << 16 | survivors << 40}.
+__device__ __forceinline__ void StampItem(const ScanArgs& a, uint32_t item, uint64_t rt,
+                                          uint64_t t0, uint64_t t1, uint64_t t2, uint64_t t3,
+                                          uint64_t tiles) {
+  const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID
+  const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (15 << 11));  // HW_REG_XCC_ID
+  const uint32_t slot = atomicAdd(a.stamp_count, 1u);
+  if (slot < a.stamp_cap) {
+    unsigned long long* p = a.stamps + size_t(slot) * 8;
+    p[0] = hw | (uint64_t(blockIdx.x) << 32);
+    p[1] = (uint64_t(xcc) << 32) | item;
+    p[2] = rt;
+    p[3] = t0;
+    p[4] = t1;
+    p[5] = t2;
+    p[6] = t3;
+    p[7] = tiles;
+  }
+}
+
+// The query parameters of an item's 32 slots, in LDS for the drain.
+struct QParam {
+  uint32_t qid;
+  int32_t amax;
+  float bias;
+  float inv;
+  uint64_t tau;
+};
+
+#ifndef SMX_SCAN_WAVES_PER_SIMD
+#define SMX_SCAN_WAVES_PER_SIMD 3
+#endif
 template <int K, int ABL = 0>
-__global__ void __launch_bounds__(256, (K <= 25 ? 4 : 3)) lut16_scan_kernel(ScanArgs a) {
+__global__ void __launch_bounds__(64, (K <= 25 ? SMX_SCAN_WAVES_PER_SIMD : 2))
+    lut16_scan_kernel(ScanArgs a) {
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
   constexpr int W = 4 * NW;
-  constexpr int Q = 32, NWV = 4, NT = 256, HW = kHitsPerWave, S = kQStageHits;
-  constexpr int ROWS = 2 * K * Q, PER = (ROWS + NT - 1) / NT;
-  __shared__ v4i lut_s[ROWS];
-  __shared__ uint4 hsum[NWV][HW][2];     // 16 sums as int16 pairs
-  __shared__ uint32_t hmeta[NWV][HW];    // tile << 6 | lane
-  __shared__ uint64_t qstage[Q * S];
-  __shared__ uint32_t qcnt[Q], q_slot[Q], q_id[Q];
-  __shared__ float q_bias[Q], q_inv[Q];
-  __shared__ int q_amax[Q];
-  __shared__ uint64_t q_T[Q];
-  __shared__ uint32_t s_w;
+  constexpr int Q = 32, HW = 2 * kHitsPerWave, KB = kItemKeys;
+  constexpr int R = 3;   // one-hot reads in flight ahead of their MFMA
+  __shared__ uint4 hsum[HW][2];     // 16 sums as int16 pairs
+  __shared__ uint32_t hmeta[HW];    // tile << 6 | lane
+  __shared__ uint64_t kbuf[KB];        // the item's survivors (all its queries)
+  __shared__ uint8_t kslot[KB];        // their query slots
+  __shared__ uint32_t qcnt[Q], q_slot[Q], s_kn;
+  __shared__ QParam qp[Q];
   __shared__ v4i oh_tab[16];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int lane = threadIdx.x;
   const int c = lane & 31;
   const int h = lane >> 5;
-  if (tid < 16) {
+  if (lane < 16) {
     v4i t = {0, 0, 0, 0};
-    t[tid >> 2] = int(1u << (8 * (tid & 3)));
-    oh_tab[tid] = t;
+    t[lane >> 2] = int(1u << (8 * (lane & 3)));
+    oh_tab[lane] = t;
   }
-  const uint32_t total = a.tile_prefix[a.nl];
-  const int smin = -128 * a.nb, smax = 128 * a.nb;
-  for (;;) {
-    if (tid == 0) s_w = atomicAdd(a.work_counter, 1u);
-    if (tid < Q) qcnt[tid] = 0;
-    __syncthreads();
-    const uint32_t w = s_w;
-    if (w >= total) break;
-    const uint2 item = a.work[w];
-    const int leaf = int(item.x);
-    const uint32_t t = item.y >> 16;
-    const uint32_t chunk = item.y & 0xFFFFu;
-    const uint32_t pbeg = a.pair_off[leaf] + t * uint32_t(Q);
-    const int nvalid = int(min(uint32_t(Q), a.pair_off[leaf] + a.leaf_count[leaf] - pbeg));
-    // this thread's query slot is fixed (NT is a multiple of Q): one id load
-    const uint32_t qid = a.pair_q[pbeg + uint32_t(c < nvalid ? c : 0)];
-    if (tid < Q) {
-      const bool v = tid < nvalid;
-      const float bias = a.residual ? a.pair_bias[pbeg + uint32_t(v ? tid : 0)] : 0.0f;
-      const float inv = a.inv[qid];
-      const uint64_t T = a.tau_key[qid];
-      q_id[tid] = qid;
-      q_bias[tid] = bias;
-      q_inv[tid] = inv;
-      q_T[tid] = T;
-      q_amax[tid] = !v ? smin - 1
-                  : (T == kNoThreshold) ? smax
-                  : SumLimit(FromOrdered(uint32_t(T >> 32)), inv, bias, smin, smax);
+  uint64_t st_rt = 0, st_t0 = 0, st_t1 = 0, st_t2 = 0;
+  uint32_t st_hits = 0, st_surv = 0;
+  const WorkItem* work = a.work;
+  // this wave's static share: `units` tiles from tile j of item w on
+  const uint4 ws = a.wave_start[blockIdx.x];
+  uint32_t w = __builtin_amdgcn_readfirstlane(ws.x);
+  uint32_t jfirst = __builtin_amdgcn_readfirstlane(ws.y);
+  uint32_t units = __builtin_amdgcn_readfirstlane(ws.z);
+  WorkItem cur = work[w];
+  ItemLane cl = a.lanes[size_t(w) * Q + c];
+  bool pending = false;   // the previous item's survivors await their copy
+  uint32_t slot = 0;      // that copy's first list slot (lanes < 32)
+  while (units > 0 || pending) {
+    const bool has = units > 0;
+    if (ABL & 8) {
+      st_rt = __builtin_amdgcn_s_memrealtime();
+      st_t0 = __builtin_amdgcn_s_memtime();
+      st_hits = st_surv = 0;
     }
-    {
-      // LUT rows of the 32 queries into LDS ([row][query] x 16 B); the loads
-      // are unconditional (clamped row) so they are all in flight together
-      const v4i* src = reinterpret_cast<const v4i*>(a.lut) + size_t(qid) * 2 * K;
-      v4i stg[PER];
+    // this item's B fragments (LUT rows 2s+h of query c) and first code tile
+    // go out first; the previous item's slot atomics (older) are waited for
+    // below without waiting for these
+    const uint32_t n = cur.n;
+    const uint32_t j0 = jfirst ? jfirst : cur.j0;
+    const uint32_t jend = min(cur.jend, j0 + units);
+    v4i b[K];
+    uint32_t codes[NW] = {};
+    const uint8_t* tb = a.tiles + cur.tile_off * 64ull * W + size_t(lane) * W;
+    if (has) {
+      const v4i* src = reinterpret_cast<const v4i*>(a.lut) + size_t(cl.qid) * 2 * K + h;
 #pragma unroll
-      for (int i = 0; i < PER; ++i) stg[i] = src[min(tid + i * NT, ROWS - 1) / Q];
-#pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const int e = tid + i * NT;
-        if (e < ROWS) lut_s[e] = stg[i];
+      for (int s = 0; s < K; ++s) b[s] = src[2 * s];
+      if (j0 < jend) LoadCodes<K>(tb + size_t(j0) * 64 * W, codes);   // (empty leaf: no tile)
+    }
+    if (pending) {
+      // the previous item's staged survivors to their queries' lists: each
+      // key's place = its query's reserved first slot + a running count
+      if (lane < Q) {
+        q_slot[lane] = slot;
+        qcnt[lane] = 0;
       }
+      WaveLdsSync();
+      const uint32_t kn = min(s_kn, uint32_t(KB));
+      for (uint32_t e = uint32_t(lane); e < kn; e += 64) {
+        const uint32_t qs = kslot[e];
+        const uint32_t sl = q_slot[qs] + atomicAdd(&qcnt[qs], 1u);
+        if (sl < a.cap) a.cand[size_t(qp[qs].qid) * a.cap + sl] = kbuf[e];
+      }
+      WaveLdsSync();
+      pending = false;
     }
-    __syncthreads();
-    const int amax = q_amax[c];
-    const uint32_t n = a.leaf_size[leaf];
-    const uint32_t ntile_leaf = (n + kDpPerTile - 1) / kDpPerTile;
-    const uint32_t j0 = chunk * a.chunk_tiles;
-    const uint32_t jend = min(ntile_leaf, j0 + a.chunk_tiles);
-    const uint8_t* tb = a.tiles + a.tile_off[leaf] * 64ull * W + size_t(lane) * W;
-    const uint64_t moff = a.member_off[leaf];
+    if (!has) break;
+    // the next item's descriptor and record, in flight during this item
+    const uint32_t wn = min(w + 1, a.num_items - 1);
+    const WorkItem nxt = work[wn];
+    const ItemLane nrec = a.lanes[size_t(wn) * Q + c];
+    const int leaf = int(cur.leaf);
+    const uint64_t moff = cur.member_off;
+    const int amax = cl.amax;
+    if (lane < Q) {
+      QParam v;
+      v.qid = cl.qid;
+      v.amax = cl.amax;
+      v.bias = cl.bias;
+      v.inv = cl.inv;
+      v.tau = cl.tau;
+      qp[lane] = v;
+      qcnt[lane] = 0;
+    }
+    if (lane == 0) s_kn = 0;
+    units -= jend - j0;
+    jfirst = 0;
+    WaveLdsSync();
     uint32_t whits = 0;   // wave-uniform
 
-    // lane k of the wave takes hit k: per-element test, key, exact
+    // lane k of the wave takes hits k, k+64: per-element test, key, exact
     // threshold compare, append to the query's LDS stage
     auto drain = [&]() {
-      if (uint32_t(lane) < whits) {
-        const uint32_t meta = hmeta[wave][lane];
+      for (uint32_t hidx = uint32_t(lane); hidx < whits; hidx += 64) {
+        const uint32_t meta = hmeta[hidx];
         const uint32_t jj = meta >> 6;
         const int cc = int(meta & 31u), hh = int((meta >> 5) & 1u);
-        const uint4 s0 = hsum[wave][lane][0], s1 = hsum[wave][lane][1];
+        const uint4 s0 = hsum[hidx][0], s1 = hsum[hidx][1];
         const uint32_t sw[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-        const int am = q_amax[cc];
-        const float iv = q_inv[cc], bs = q_bias[cc];
-        const uint64_t TT = q_T[cc];
-        const uint32_t qq = q_id[cc];
-#pragma unroll
+        const QParam pq = qp[cc];
+        const int am = pq.amax;
+        const float iv = pq.inv, bs = pq.bias;
+        const uint64_t TT = pq.tau;
+        const uint32_t qq = pq.qid;
+#pragma unroll 1
         for (int i = 0; i < 16; ++i) {
           const int sum = int(int16_t(uint16_t(sw[i >> 1] >> (16 * (i & 1)))));
           if (sum <= am) {
@@ -967,10 +1162,12 @@ __global__ void __launch_bounds__(256, (K <= 25 ? 4 : 3)) lut16_scan_kernel(Scan
                                              : a.members[moff + dp];
             const uint64_t key = (uint64_t(OrderedBits(d)) << 32) | tie;
             if (key <= TT) {
-              const uint32_t p = atomicAdd(&qcnt[cc], 1u);
-              if (p < uint32_t(S)) {
-                qstage[cc * S + p] = key;
-              } else {  // stage full: straight to the global list
+              const uint32_t p = atomicAdd(&s_kn, 1u);
+              if (p < uint32_t(KB)) {
+                kbuf[p] = key;
+                kslot[p] = uint8_t(cc);
+                atomicAdd(&qcnt[cc], 1u);
+              } else {  // item buffer full (rare): straight to the global list
                 const uint32_t gs = atomicAdd(&a.cand_count[qq], 1u);
                 if (gs < a.cap) a.cand[size_t(qq) * a.cap + gs] = key;
               }
@@ -978,10 +1175,13 @@ __global__ void __launch_bounds__(256, (K <= 25 ? 4 : 3)) lut16_scan_kernel(Scan
           }
         }
       }
+      WaveLdsSync();   // the hit list is rewritten next
     };
 
-    auto body = [&](const uint32_t (&codes)[NW], uint32_t j) {
-      v16i acc = TileMfma<K, Q>(codes, lut_s, h * Q + c, oh_tab);
+    // one tile: K MFMAs, then the hit test (and the drain when the list is
+    // over half full or after the chunk's last tile)
+    auto tile = [&](const uint32_t (&cd)[NW], uint32_t j) {
+      v16i acc = TileMfma<K, R>(cd, b, oh_tab);
       if (ABL & 4) {
         int x = acc[0];
 #pragma unroll
@@ -1004,58 +1204,67 @@ __global__ void __launch_bounds__(256, (K <= 25 ? 4 : 3)) lut16_scan_kernel(Scan
       const bool hit = m <= amax;
       const uint64_t hb = __builtin_amdgcn_ballot_w64(hit);
       if (hb) {
+        // whits <= 64 here and a tile adds at most 64: the list (HW = 128)
+        // always has room, so the sums are dead before any drain
         const uint32_t nh = uint32_t(__popcll(hb));
-        if (whits + nh > uint32_t(HW)) {
-          drain();
-          whits = 0;
-        }
         if (hit) {
-          const uint32_t slot =
+          const uint32_t hs =
               whits + __builtin_amdgcn_mbcnt_hi(uint32_t(hb >> 32),
                                                 __builtin_amdgcn_mbcnt_lo(uint32_t(hb), 0u));
           uint32_t pk[8];
 #pragma unroll
           for (int k = 0; k < 8; ++k)
             pk[k] = (uint32_t(acc[2 * k]) & 0xFFFFu) | (uint32_t(acc[2 * k + 1]) << 16);
-          hsum[wave][slot][0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-          hsum[wave][slot][1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
-          hmeta[wave][slot] = (j << 6) | uint32_t(lane);
+          hsum[hs][0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+          hsum[hs][1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+          hmeta[hs] = (j << 6) | uint32_t(lane);
         }
         whits += nh;
+        if (ABL & 8) st_hits += nh;
+        WaveLdsSync();
+      }
+      if (whits > 64u || (j + 1 == jend && whits)) {
+        drain();
+        whits = 0;
       }
     };
 
-    // tiles j, j+4, ... of the chunk; the prefetch of tile j+4 is
-    // unconditional (clamped to the chunk's last tile) so no exec branch
-    // sits around the load and the wait before the next tile is counted
-    uint32_t j = j0 + wave;
-    if (j < jend) {
-      uint32_t codes[NW], next[NW];
+    if (ABL & 8) st_t1 = __builtin_amdgcn_s_memtime();
+    // tiles j0 .. jend-1, two code buffers in turn: the load of tile j+1 is
+    // in flight while tile j computes (a rotating copy would force a wait
+    // for it at the copy); prefetches are clamped to the chunk's last tile so
+    // no exec branch sits around a load
+    if (j0 < jend) {
       const uint32_t jl = jend - 1;
-      LoadCodes<K>(tb + size_t(j) * 64 * W, codes);
-      for (; j < jend; j += NWV) {
-        LoadCodes<K>(tb + size_t(min(j + NWV, jl)) * 64 * W, next);
-        body(codes, j);
-#pragma unroll
-        for (int i = 0; i < NW; ++i) codes[i] = next[i];
+      uint32_t cb[NW];
+      for (uint32_t j = j0;; j += 2) {
+        LoadCodes<K>(tb + size_t(min(j + 1, jl)) * 64 * W, cb);
+        tile(codes, j);
+        if (j + 1 >= jend) break;
+        LoadCodes<K>(tb + size_t(min(j + 2, jl)) * 64 * W, codes);
+        tile(cb, j + 1);
+        if (j + 2 >= jend) break;
       }
     }
-    drain();
-    __syncthreads();
-    // one global atomic per query slot with survivors, then the copy
-    if (tid < Q) {
-      const uint32_t m = min(qcnt[tid], uint32_t(S));
-      q_slot[tid] = m ? atomicAdd(&a.cand_count[q_id[tid]], m) : 0u;
+    if (ABL & 8) st_t2 = __builtin_amdgcn_s_memtime();
+    if (ABL & 8) {
+      uint32_t sv = lane < Q ? qcnt[lane] : 0u;
+      for (int off = 32; off > 0; off >>= 1) sv += uint32_t(__shfl_xor(int(sv), off));
+      st_surv = sv;
     }
-    __syncthreads();
-    for (int e = tid; e < Q * S; e += NT) {
-      const int qs = e / S, u = e - qs * S;
-      if (uint32_t(u) < min(qcnt[qs], uint32_t(S))) {
-        const uint32_t slot = q_slot[qs] + u;
-        if (slot < a.cap) a.cand[size_t(q_id[qs]) * a.cap + slot] = qstage[e];
-      }
+    // one list-slot atomic per query slot with survivors; the copy waits for
+    // it at the next item's start (after that item's loads are issued)
+    if (lane < Q) {
+      const uint32_t m = qcnt[lane];
+      slot = m ? atomicAdd(&a.cand_count[cl.qid], m) : 0u;
     }
-    __syncthreads();
+    pending = true;
+    if ((ABL & 8) && lane == 0)
+      StampItem(a, w, st_rt, st_t0, st_t1, st_t2, __builtin_amdgcn_s_memtime(),
+                uint64_t(jend - j0) | (uint64_t(st_hits) << 16) | (uint64_t(st_surv) << 40));
+    cur = nxt;
+    cl = nrec;
+    ++w;
   }
 }
 
@@ -1087,6 +1296,21 @@ __global__ void __launch_bounds__(64) leaf_scores_kernel(const uint8_t* __restri
       }
     }
   }
+}
+
+// Overflow recovery, part 2: the items' lane records take the tightened
+// thresholds (the scan's sum limits and key tests read them there).
+__global__ void refresh_lanes_kernel(ItemLane* __restrict__ lanes, const uint32_t* __restrict__ totals,
+                                     const uint64_t* __restrict__ tau_key, int nb) {
+  const size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= size_t(totals[1]) * kQueriesPerTile) return;
+  ItemLane v = lanes[i];
+  if (v.amax == kNoSum) return;
+  const uint64_t T = tau_key[v.qid];
+  const int smin = -128 * nb, smax = 128 * nb;
+  v.tau = T;
+  v.amax = T == kNoThreshold ? smax : SumLimit(FromOrdered(uint32_t(T >> 32)), v.inv, v.bias, smin, smax);
+  lanes[i] = v;
 }
 
 // Overflow recovery: the k'-th smallest stored key is a valid (tighter)
@@ -1689,7 +1913,8 @@ __global__ void fill64_kernel(uint64_t* p, uint64_t v, size_t n) {
 // Launchers.
 // ---------------------------------------------------------------------------
 hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int nq, int L,
-                               int32_t* out_leaf, float* out_dist, float* scores, hipStream_t s) {
+                               int32_t* out_leaf, float* out_dist, float* scores, hipStream_t s,
+                               const FrontArgs* front) {
   if (nq == 0) return hipSuccess;
   uint32_t kcap = 1;
   while (kcap < uint32_t(ix.nl)) kcap <<= 1;
@@ -1697,68 +1922,65 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   while (lp2 < uint32_t(L)) lp2 <<= 1;
   const uint32_t selcap = std::max<uint32_t>(2048u, 2 * lp2);
   const size_t lds = size_t(kcap) * 8 + size_t(selcap) * 8 + (kSelBins + 256) * 4;
+  const FrontArgs none{};
+  const FrontArgs& f = front ? *front : none;
+  TopLTail tail{};
+  tail.leaf_count = f.leaf_count;
+  tail.rank = f.rank;
+  tail.lut = LutParams{queries, ix.dim, ix.codebook, ix.nb, ix.dpb, 2 * ix.ksteps, ix.metric,
+                       ix.residual, f.lut, f.mult, f.inv, nullptr};
   hipLaunchKernelGGL(partition_scores_kernel,
                      dim3((nq + kPartTile - 1) / kPartTile, (ix.nl + kPartTile - 1) / kPartTile),
                      dim3(256), 0, s, queries, nq, ix.dim, ix.centers, ix.cnorm, ix.nl, ix.metric,
-                     scores);
-  if (ix.nl <= kLdsSelectLeaves && lds <= 160 * 1024) {
+                     scores, f.init);
+  // static LDS of the kernel besides the dynamic key buffers: the LUT build's
+  // raw table and reduction (~5 KB) and the selection's words
+  constexpr size_t kStaticLds = 6 * 1024;
+  if (ix.nl <= kLdsSelectLeaves && lds + kStaticLds <= 160 * 1024) {
     hipLaunchKernelGGL(topl_select_kernel, dim3(nq), dim3(256), lds, s, scores, ix.nl, L, kcap,
-                       out_leaf, out_dist);
+                       out_leaf, out_dist, tail);
   } else {
     uint32_t lcap = 1;
     while (lcap < uint32_t(std::min(L, ix.nl))) lcap <<= 1;
     if (size_t(lcap) * 8 > 128 * 1024) return hipErrorInvalidValue;   // L > 16384
     hipLaunchKernelGGL(topl_select_global_kernel, dim3(nq), dim3(256), size_t(lcap) * 8, s, scores,
-                       ix.nl, L, lcap, out_leaf, out_dist);
+                       ix.nl, L, lcap, out_leaf, out_dist, tail);
   }
   return hipGetLastError();
 }
 
 hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq, int8_t* lut,
-                          float* mult, float* inv, uint8_t* lut_u8, hipStream_t s,
-                          const LutInit* init) {
+                          float* mult, float* inv, uint8_t* lut_u8, hipStream_t s) {
   if (nq == 0) return hipSuccess;
-  const LutInit none{};
-  hipLaunchKernelGGL(lut_build_kernel, dim3(nq), dim3(256), 0, s, queries, ix.dim, ix.codebook,
-                     ix.nb, ix.dpb, 2 * ix.ksteps, ix.metric, ix.residual, lut, mult, inv, lut_u8,
-                     init ? *init : none);
+  const LutParams p{queries, ix.dim, ix.codebook, ix.nb, ix.dpb, 2 * ix.ksteps, ix.metric,
+                    ix.residual, lut, mult, inv, lut_u8};
+  hipLaunchKernelGGL(lut_build_kernel, dim3(nq), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
-hipError_t LaunchPairs(const DeviceIndex& ix, const uint32_t* order, const int32_t* topl_leaf,
-                       const float* topl_dist,
-                       int nq, int L, uint32_t* cnt, uint32_t* block_cnt, uint32_t* pair_off,
-                       uint32_t* tile_prefix, uint32_t* pair_q, float* pair_bias, uint2* work,
-                       uint32_t* totals, unsigned long long* code_bytes, uint32_t chunk_tiles,
-                       uint32_t queries_per_item, hipStream_t s) {
-  const int n = nq * L;
-  const int nblocks = (n + kPairsPerBlock - 1) / kPairsPerBlock;
-  const int ranges = (ix.nl + kLeafRange - 1) / kLeafRange;
-  const size_t lds = size_t(std::min(ix.nl, kLeafRange)) * 4;
-  if (n > 0)
-    hipLaunchKernelGGL(pairs_count_kernel, dim3(nblocks, ranges), dim3(256), lds, s, topl_leaf, n,
-                       ix.nl, block_cnt, cnt);
-  // up to 4096 leaves the block offsets ride in the one-block scan kernel
-  const int fused = (n > 0 && ix.nl <= 4096) ? nblocks : 0;
-  hipLaunchKernelGGL(pairs_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, order,
-                     ix.leaf_size, ix.nl, ix.nb, chunk_tiles, queries_per_item, pair_off,
-                     tile_prefix, totals, code_bytes, work, block_cnt, fused);
-  if (n > 0) {
-    if (!fused)
-      hipLaunchKernelGGL(pairs_block_offsets_kernel, dim3((ix.nl + 255) / 256), dim3(256), 0, s,
-                         block_cnt, nblocks, ix.nl);
-    hipLaunchKernelGGL(pairs_scatter_kernel, dim3(nblocks, ranges), dim3(256), lds, s, topl_leaf,
-                       topl_dist, n, L, ix.nl, pair_off, block_cnt, pair_q, pair_bias);
-  }
+hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, WorkItem* work,
+                          uint32_t* leaf_item0, uint32_t* pos_unit0, uint32_t* gunits,
+                          ItemLane* lanes, uint4* wave_start, int grid, uint32_t* totals,
+                          unsigned long long* code_bytes, uint32_t chunk_tiles, hipStream_t s) {
+  hipLaunchKernelGGL(worklist_kernel, dim3(1), dim3(1024), 0, s, leaf_count, ix.leaf_order,
+                     ix.leaf_size, ix.nl, ix.nb, chunk_tiles, leaf_item0, pos_unit0, gunits, totals,
+                     code_bytes);
+  hipLaunchKernelGGL(wave_clear_kernel, dim3((grid + 255) / 256), dim3(256), 0, s, gunits, grid,
+                     wave_start);
+  hipLaunchKernelGGL(items_kernel, dim3(ix.nl), dim3(64), 0, s, leaf_count, ix.leaf_order,
+                     ix.leaf_size, ix.tile_off, ix.member_off, chunk_tiles, grid, leaf_item0,
+                     pos_unit0, gunits, work, lanes, wave_start);
   return hipGetLastError();
 }
 
 #define SMX_SCAN_CASE(KV)                                                          \
   case KV:                                                                         \
     if (variant == 4)                                                              \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 4>), dim3(grid), dim3(256), 0, s, a); \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 4>), dim3(grid), dim3(64), 0, s, a); \
+    else if (variant == 8)                                                         \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 8>), dim3(grid), dim3(64), 0, s, a); \
     else                                                                           \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(256), 0, s, a); \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64), 0, s, a); \
     break;
 
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,
@@ -1777,6 +1999,28 @@ hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int va
       return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+#define SMX_OCC_CASE(KV)                                                                 \
+  case KV:                                                                               \
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(                                 \
+        blocks, reinterpret_cast<const void*>(&lut16_scan_kernel<KV, 0>), 64, 0);
+
+hipError_t ScanBlocksPerCU(const DeviceIndex& ix, int* blocks) {
+  *blocks = 0;
+  switch (ix.ksteps) {
+    SMX_OCC_CASE(4)
+    SMX_OCC_CASE(8)
+    SMX_OCC_CASE(12)
+    SMX_OCC_CASE(16)
+    SMX_OCC_CASE(20)
+    SMX_OCC_CASE(24)
+    SMX_OCC_CASE(25)
+    SMX_OCC_CASE(28)
+    SMX_OCC_CASE(32)
+    default:
+      return hipErrorInvalidValue;
+  }
 }
 
 #define SMX_LEAF_CASE(KV)                                                                  \
@@ -1818,7 +2062,7 @@ hipError_t LaunchLeafScores(const DeviceIndex& ix, int leaf, const int8_t* lut, 
     break;
 
 hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s) {
-  if (nq == 0 || a.seed <= 0) return hipSuccess;
+  if (nq == 0) return hipSuccess;   // (seed <= 0 still scatters the pairs)
   switch (ix.ksteps) {
     SMX_SEED_CASE(4)
     SMX_SEED_CASE(8)
@@ -1844,6 +2088,15 @@ hipError_t LaunchTighten(const uint64_t* cand, const uint32_t* cand_count, uint3
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(tighten_kernel, dim3(nq), dim3(256), lds, s, cand, cand_count, cap, kk,
                      tau_key);
+  return hipGetLastError();
+}
+
+hipError_t LaunchRefreshLanes(ItemLane* lanes, uint32_t max_items, const uint32_t* totals,
+                              const uint64_t* tau_key, int nb, hipStream_t s) {
+  const size_t n = size_t(max_items) * kQueriesPerTile;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(refresh_lanes_kernel, dim3((n + 255) / 256), dim3(256), 0, s, lanes, totals,
+                     tau_key, nb);
   return hipGetLastError();
 }
 

@@ -73,6 +73,17 @@ int EffectiveKSteps(int nb) {
   return -1;
 }
 
+// Per-call counters (one buffer, zeroed by the partition kernel):
+//   [0, nl)            pairs per leaf
+//   [stats, +32)       stats words (SelectArgs::overflow and the work-list totals)
+struct CounterLayout {
+  uint32_t stats, words;
+  explicit CounterLayout(int nl) {
+    stats = (uint32_t(nl) + 31u) & ~31u;
+    words = stats + 32u;
+  }
+};
+
 struct Workspace {
   int nq = 0, L = 0, kk = 0, dim = 0, width = 0;
   uint64_t gen = 0;                 // bumped on every (re)allocation
@@ -84,13 +95,14 @@ struct Workspace {
   int8_t* lut = nullptr;
   float* mult = nullptr;
   float* inv = nullptr;
-  uint32_t* counters = nullptr;     // cnt[nl] | spare[nl] | work counter | stats[16]
-  uint32_t* block_cnt = nullptr;    // [ceil(nq*L/4096)][nl] per-block leaf counts
-  uint32_t* pair_off = nullptr;     // [nl+1]
-  uint32_t* tile_prefix = nullptr;  // [nl+1]
-  uint32_t* pair_q = nullptr;       // [nq*L]
-  float* pair_bias = nullptr;       // [nq*L]
-  uint2* work = nullptr;            // [max_items]
+  uint32_t* counters = nullptr;     // see CounterLayout
+  uint32_t* rank = nullptr;         // [nq*L] each pair's position in its leaf's list
+  uint32_t* leaf_item0 = nullptr;   // [nl] each leaf's first work item
+  smx::WorkItem* work = nullptr;    // [max_items]
+  smx::ItemLane* lanes = nullptr;   // [max_items][32]
+  uint4* wave_start = nullptr;      // [grid] each scan wave's static share
+  uint32_t* pos_unit0 = nullptr;    // [nl+1] work units before each leaf (work order)
+  uint32_t* gunits = nullptr;       // [16] the XCD groups' unit boundaries
   uint64_t* tau = nullptr;          // [nq]
   uint64_t* cand = nullptr;         // [nq][cap]
   uint32_t* cand_count = nullptr;   // [nq]
@@ -102,7 +114,8 @@ struct Workspace {
   void Release() {
     DFree(queries); DFree(topl_leaf); DFree(topl_dist); DFree(scores); DFree(lut); DFree(mult);
     DFree(inv);
-    DFree(counters); DFree(block_cnt); DFree(pair_off); DFree(tile_prefix); DFree(pair_q); DFree(pair_bias);
+    DFree(counters); DFree(rank); DFree(leaf_item0); DFree(lanes); DFree(wave_start);
+    DFree(pos_unit0); DFree(gunits);
     DFree(work); DFree(tau); DFree(cand); DFree(cand_count); DFree(fallback); DFree(out_idx);
     DFree(out_dist);
     DFree(out_count);
@@ -123,20 +136,23 @@ struct smx_index {
   int seed_leaves = 4;
   int scan_variant = 0;            // see smx::LaunchScan
   uint32_t chunk_tiles = 32;       // tiles per work item
-  int grid = 0;                    // scan grid: 4 blocks of 4 waves per CU (LDS-limited)
+  int grid = 0;                    // scan grid: resident one-wave workgroups (occupancy API)
   bool profiling = false;
   bool use_graph = true;           // replay the first pass as a hipGraph
   hipGraphExec_t graph_exec = nullptr;
-  uint64_t graph_key[12] = {};
+  uint64_t graph_key[16] = {};
   uint64_t ws_generation = 0;
   uint32_t* host_stats = nullptr;  // pinned copy of the stats words
   smx_timings timings{};
   hipEvent_t ev[16] = {};
+  // scan variant 8 (diagnostics): per-item stamps, dumped to $SMX_STAMPS
+  unsigned long long* stamps = nullptr;
+  uint32_t* stamp_count = nullptr;
 };
 
 namespace {
 
-constexpr int GraphKeyWords = 12;
+constexpr int GraphKeyWords = 16;
 
 int UploadIndex(const smx_index_desc* d, smx_index* h) {
   smx::DeviceIndex& ix = h->ix;
@@ -308,7 +324,10 @@ int ValidateDesc(const smx_index_desc* d) {
 int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
   Workspace& w = h->ws;
   const smx::DeviceIndex& ix = h->ix;
-  const uint32_t cap = std::max<uint32_t>(h->cap_per_query, uint32_t(kk));
+  // cap >= 2 k': when a list overflows, its k'-th stored key is strictly
+  // below the threshold (keys are unique and all <= it), so every
+  // tightening pass drops at least cap - k' keys
+  const uint32_t cap = std::max<uint32_t>(h->cap_per_query, 2u * uint32_t(kk));
   if (nq <= w.nq && L <= w.L && kk <= w.kk && width <= w.width && cap == w.cap &&
       ix.dim == w.dim)
     return SMX_OK;
@@ -321,10 +340,11 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
   if ((rc = DAlloc(&w.queries, size_t(nq) * ix.dim)) || (rc = DAlloc(&w.topl_leaf, pairs)) ||
       (rc = DAlloc(&w.topl_dist, pairs)) || (rc = DAlloc(&w.scores, size_t(nq) * nl)) ||
       (rc = DAlloc(&w.lut, size_t(nq) * 2 * ix.ksteps * 16)) || (rc = DAlloc(&w.mult, nq)) ||
-      (rc = DAlloc(&w.inv, nq)) || (rc = DAlloc(&w.counters, size_t(2) * nl + 20)) ||
-      (rc = DAlloc(&w.block_cnt, ((pairs + 4095) / 4096) * size_t(nl))) ||
-      (rc = DAlloc(&w.pair_off, size_t(nl + 1))) || (rc = DAlloc(&w.tile_prefix, size_t(nl + 1))) ||
-      (rc = DAlloc(&w.pair_q, pairs)) || (rc = DAlloc(&w.pair_bias, pairs)) ||
+      (rc = DAlloc(&w.inv, nq)) || (rc = DAlloc(&w.counters, CounterLayout(nl).words)) ||
+      (rc = DAlloc(&w.rank, pairs)) || (rc = DAlloc(&w.leaf_item0, size_t(nl))) ||
+      (rc = DAlloc(&w.lanes, size_t(max_items) * smx::kQueriesPerTile)) ||
+      (rc = DAlloc(&w.wave_start, size_t(std::max(h->grid, 1)))) ||
+      (rc = DAlloc(&w.pos_unit0, size_t(nl + 1))) || (rc = DAlloc(&w.gunits, 16)) ||
       (rc = DAlloc(&w.work, max_items)) || (rc = DAlloc(&w.tau, nq)) ||
       (rc = DAlloc(&w.cand, size_t(nq) * cap)) || (rc = DAlloc(&w.cand_count, nq)) ||
       (rc = DAlloc(&w.fallback, nq)) ||
@@ -370,12 +390,12 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   if (rc) return rc;
   Workspace& w = h->ws;
   const int nl = ix.nl;
+  const CounterLayout lay(nl);
   uint32_t* cnt = w.counters;
-  uint32_t* work = w.counters + 2 * nl;
   // stats: [0] overflow flag [1] max overflowing count [2] max count
   //        [3] pairs [4] work items [5] item-tiles (MFMA tiles of the scan)
-  //        [6..7] code bytes (u64) [8] survivors summed over queries
-  uint32_t* stats = ((reinterpret_cast<uintptr_t>(work + 1) & 7) == 0) ? work + 1 : work + 2;
+  //        [6..7] code bytes (u64) [8] survivors summed over queries [9] fallbacks
+  uint32_t* stats = w.counters + lay.stats;
   unsigned long long* code_bytes = reinterpret_cast<unsigned long long*>(stats + 6);
   const int seed = std::min(h->seed_leaves, L);
 
@@ -383,6 +403,11 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   smx::SeedArgs sa{};
   sa.topl_leaf = w.topl_leaf;
   sa.topl_dist = w.topl_dist;
+  sa.rank = w.rank;
+  sa.leaf_item0 = w.leaf_item0;
+  sa.lanes = w.lanes;
+  sa.chunk_tiles = h->chunk_tiles;
+  sa.nb = ix.nb;
   sa.lut = w.lut;
   sa.inv = w.inv;
   sa.tiles = ix.tiles;
@@ -396,28 +421,30 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
 
   smx::ScanArgs a{};
   a.tiles = ix.tiles;
-  a.tile_off = ix.tile_off;
-  a.leaf_size = ix.leaf_size;
-  a.member_off = ix.member_off;
   a.members = ix.members;
   a.lut = w.lut;
   a.inv = w.inv;
-  a.pair_q = w.pair_q;
-  a.pair_bias = w.pair_bias;
-  a.pair_off = w.pair_off;
-  a.leaf_count = cnt;
-  a.tile_prefix = w.tile_prefix;
   a.work = w.work;
+  a.lanes = w.lanes;
+  a.wave_start = w.wave_start;
+  a.num_items = w.max_items;   // bound of the one-ahead descriptor prefetch
   a.tau_key = w.tau;
   a.cand = w.cand;
   a.cand_count = w.cand_count;
-  a.work_counter = work;
+  constexpr uint32_t kStampCap = 1u << 16;
+  if (variant == 8 && !h->stamps) {
+    int rc2;
+    if ((rc2 = DAlloc(&h->stamps, size_t(kStampCap) * 8)) || (rc2 = DAlloc(&h->stamp_count, 1)))
+      return rc2;
+  }
+  a.stamps = h->stamps;
+  a.stamp_count = h->stamp_count;
+  a.stamp_cap = kStampCap;
+  if (variant == 8) SMX_HIP(hipMemsetAsync(h->stamp_count, 0, 4, s));
   a.cap = w.cap;
-  a.chunk_tiles = h->chunk_tiles;
   a.nl = nl;
   a.nb = ix.nb;
   a.shift = ix.shift;
-  a.residual = ix.residual;
 
   smx::SelectArgs sel{};
   sel.cand = w.cand;
@@ -452,24 +479,26 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   // instead of ~20, no per-kernel host overhead); eager otherwise.
   auto first_pass = [&]() -> int {
     Mark(h, 0, s);
-    // the LUT build also zeroes the counters / candidate counts and opens the
-    // thresholds; it precedes the inversion, the seed and the scan on every path
-    smx::LutInit init;
-    init.counters = w.counters;
-    init.n_counters = uint32_t(2 * nl + 20);
-    init.cand_count = w.cand_count;
-    init.n_cand = uint32_t(nq);
-    init.tau = w.tau;
-    init.n_tau = uint32_t(nq);
-    SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s));
+    // front end: state reset, partition scores, top-L + ranks + LUTs
+    smx::FrontArgs f;
+    f.init.counters = w.counters;
+    f.init.n_counters = lay.words;
+    f.init.cand_count = w.cand_count;
+    f.init.n_cand = uint32_t(nq);
+    f.init.tau = w.tau;
+    f.init.n_tau = uint32_t(nq);
+    f.leaf_count = cnt;
+    f.rank = w.rank;
+    f.lut = w.lut;
+    f.mult = w.mult;
+    f.inv = w.inv;
+    SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s, &f));
     Mark(h, 1, s);
-    SMX_HIP(smx::LaunchLutBuild(ix, queries, nq, w.lut, w.mult, w.inv, nullptr, s, &init));
     Mark(h, 2, s);
-    SMX_HIP(smx::LaunchPairs(ix, ix.leaf_order, w.topl_leaf, w.topl_dist, nq, L, cnt, w.block_cnt,
-                             w.pair_off, w.tile_prefix, w.pair_q, w.pair_bias, w.work, stats + 3,
-                             code_bytes, h->chunk_tiles, 32u, s));
+    SMX_HIP(smx::LaunchWorklist(ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes,
+                                w.wave_start, h->grid, stats + 3, code_bytes, h->chunk_tiles, s));
     Mark(h, 3, s);
-    SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
+    SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));   // thresholds + the pairs' item lanes
     Mark(h, 4, s);
     Mark(h, 5, s);
     SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s));
@@ -488,9 +517,8 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
         uint64_t(final_nn), uint64_t(reorder) | uint64_t(pre_only) << 1 | uint64_t(h->profiling) << 2,
         uint64_t(reinterpret_cast<uintptr_t>(out_idx)), uint64_t(reinterpret_cast<uintptr_t>(out_dist)),
         uint64_t(reinterpret_cast<uintptr_t>(out_count)), uint64_t(reinterpret_cast<uintptr_t>(shard_out)),
-        uint64_t(reinterpret_cast<uintptr_t>(s)),
-        w.gen ^ (uint64_t(w.cap) << 20) ^ (uint64_t(seed) << 40) ^ (uint64_t(h->chunk_tiles) << 48) ^
-            (uint64_t(variant) << 60)};
+        uint64_t(reinterpret_cast<uintptr_t>(s)), w.gen, uint64_t(w.cap), uint64_t(seed),
+        uint64_t(h->chunk_tiles), uint64_t(variant)};
     if (!h->graph_exec || std::memcmp(key, h->graph_key, sizeof(key)) != 0) {
       if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
       h->graph_exec = nullptr;
@@ -530,10 +558,10 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     // a candidate list overflowed: tighten the thresholds and rescan
     if (++retries > 64) return Fail(SMX_INTERNAL, "candidate tightening did not converge");
     SMX_HIP(smx::LaunchTighten(w.cand, w.cand_count, w.cap, nq, kk, w.tau, s));
+    SMX_HIP(smx::LaunchRefreshLanes(w.lanes, w.max_items, stats + 3, w.tau, ix.nb, s));
     SMX_HIP(hipMemsetAsync(w.cand_count, 0, sizeof(uint32_t) * nq, s));
     SMX_HIP(hipMemsetAsync(stats, 0, sizeof(uint32_t) * 3, s));
     SMX_HIP(hipMemsetAsync(stats + 8, 0, 2 * sizeof(uint32_t), s));
-    SMX_HIP(hipMemsetAsync(work, 0, sizeof(uint32_t), s));
     SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s));
     Mark(h, 6, s);
     SMX_HIP(smx::LaunchFinalSelect(sel, nq, s));
@@ -541,6 +569,22 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     SMX_HIP(hipMemcpyAsync(h->host_stats, stats, sizeof(st), hipMemcpyDeviceToHost, s));
     SMX_HIP(hipStreamSynchronize(s));
     std::memcpy(st, h->host_stats, sizeof(st));
+  }
+  if (variant == 8) {
+    // diagnostics: the last call's stamps to the file named by $SMX_STAMPS
+    const char* path = std::getenv("SMX_STAMPS");
+    uint32_t cnt_st = 0;
+    SMX_HIP(hipMemcpy(&cnt_st, h->stamp_count, 4, hipMemcpyDeviceToHost));
+    cnt_st = std::min(cnt_st, kStampCap);
+    std::vector<unsigned long long> buf(size_t(cnt_st) * 8);
+    if (cnt_st)
+      SMX_HIP(hipMemcpy(buf.data(), h->stamps, buf.size() * 8, hipMemcpyDeviceToHost));
+    if (path) {
+      if (FILE* f = std::fopen(path, "wb")) {
+        std::fwrite(buf.data(), 8, buf.size(), f);
+        std::fclose(f);
+      }
+    }
   }
   smx_timings& t = h->timings;
   if (h->profiling) {
@@ -564,8 +608,14 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   t.max_candidates = int32_t(st[2]);
   t.scan_item_tiles = double(st[5]);
   t.mean_candidates = float(st[8]) / float(nq);
+  t.scan_workgroups = h->grid;
   return SMX_OK;
 }
+
+// Largest k' (kept candidates per query before SOAR dedupe) the final
+// select supports: its block kernel holds the candidate list (cap <=
+// 8192 keys) plus 2 k' select buffers in LDS (LaunchFinalSelect).
+constexpr int kMaxKPrime = 2048;
 
 int CheckSearchArgs(smx_index* h, int nq, int dim, const smx_search_params* p) {
   if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
@@ -580,8 +630,10 @@ int CheckSearchArgs(smx_index* h, int nq, int dim, const smx_search_params* p) {
   if (p->reorder && !h->ix.dataset && !h->ix.member_rows)
     return Fail(SMX_FAILED_PRECONDITION, "exact reordering requested but index has no dataset");
   const int pnn = p->reorder ? p->pre_reorder_nn : p->final_nn;
-  if (SpillK(h->ix, pnn) > 8192)
-    return Fail(SMX_INVALID_ARGUMENT, "pre-reorder neighbors above 8192 are not supported");
+  if (SpillK(h->ix, pnn) > kMaxKPrime)
+    return Fail(SMX_INVALID_ARGUMENT,
+                "pre-reorder neighbors (x the spilling overretrieve factor) above 2048 are not "
+                "supported");
   return SMX_OK;
 }
 
@@ -625,7 +677,11 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
   for (auto& e : h->ev) (void)hipEventCreate(&e);
   hipDeviceProp_t prop;
   SMX_HIP(hipGetDeviceProperties(&prop, device));
-  h->grid = prop.multiProcessorCount * 4;
+  {
+    int per_cu = 0;
+    SMX_HIP(smx::ScanBlocksPerCU(h->ix, &per_cu));
+    h->grid = prop.multiProcessorCount * std::max(1, per_cu);
+  }
   if (hipHostMalloc(reinterpret_cast<void**>(&h->host_stats), 16 * sizeof(uint32_t)) != hipSuccess) {
     smx_index_destroy(h);
     return Fail(SMX_OUT_OF_MEMORY, "hipHostMalloc failed");
@@ -644,6 +700,8 @@ int smx_index_destroy(smx_index* h) {
   if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
   if (h->host_stats) (void)hipHostFree(h->host_stats);
   h->ws.Release();
+  DFree(h->stamps);
+  DFree(h->stamp_count);
   FreeIndex(h->ix);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
@@ -679,6 +737,8 @@ int smx_search_batched(smx_index* h, const float* queries, int32_t nq, int32_t d
                        int32_t* out_count) {
   int rc = CheckSearchArgs(h, nq, dim, p);
   if (rc) return rc;
+  if (nq > 0 && (!queries || !out_idx || !out_dist))
+    return Fail(SMX_INVALID_ARGUMENT, "null query or output buffer");
   if ((rc = CheckFinite(queries, size_t(nq) * dim))) return rc;
   if (nq == 0) return SMX_OK;
   std::lock_guard<std::mutex> lock(h->mu);
@@ -768,8 +828,12 @@ int smx_search_pre_reorder(smx_index* h, const float* queries, int32_t nq, int32
                            int32_t pre_nn, uint32_t* out_idx, float* out_dist,
                            int32_t* out_count) {
   if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
+  if (nq < 0) return Fail(SMX_INVALID_ARGUMENT, "negative batch size");
+  if (nq > 0 && (!queries || !out_idx || !out_dist))
+    return Fail(SMX_INVALID_ARGUMENT, "null query or output buffer");
   if (leaves <= 0 || pre_nn <= 0) return Fail(SMX_INVALID_ARGUMENT, "leaves and pre_nn must be > 0");
-  if (SpillK(h->ix, pre_nn) > 8192) return Fail(SMX_INVALID_ARGUMENT, "pre_nn too large");
+  if (SpillK(h->ix, pre_nn) > kMaxKPrime)
+    return Fail(SMX_INVALID_ARGUMENT, "pre_nn (x the spilling overretrieve factor) above 2048");
   int rc = CheckFinite(queries, size_t(nq) * h->ix.dim);
   if (rc) return rc;
   if (nq == 0) return SMX_OK;
@@ -800,6 +864,7 @@ int smx_partition_topl(smx_index* h, const float* queries, int32_t nq, int32_t L
   if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
   if (nq < 0 || L <= 0) return Fail(SMX_INVALID_ARGUMENT, "bad nq / L");
   if (nq == 0) return SMX_OK;
+  if (!queries || !out_leaf || !out_dist) return Fail(SMX_INVALID_ARGUMENT, "null buffer");
   std::lock_guard<std::mutex> lock(h->mu);
   SMX_HIP(hipSetDevice(h->device));
   hipStream_t s = h->stream;
@@ -828,6 +893,7 @@ int smx_create_lookup_tables(smx_index* h, const float* queries, int32_t nq, uin
                              float* out_mult) {
   if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
   if (nq <= 0) return nq == 0 ? SMX_OK : Fail(SMX_INVALID_ARGUMENT, "bad nq");
+  if (!queries || !out_lut || !out_mult) return Fail(SMX_INVALID_ARGUMENT, "null buffer");
   std::lock_guard<std::mutex> lock(h->mu);
   SMX_HIP(hipSetDevice(h->device));
   hipStream_t s = h->stream;
@@ -928,12 +994,13 @@ int smx_get_timings(const smx_index* h, smx_timings* out) {
 int smx_set_tuning(smx_index* h, int32_t candidates_per_query, int32_t seed_leaves,
                    int32_t scan_variant, int32_t chunk_tiles) {
   if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
-  if (scan_variant != 0 && scan_variant != 4)
-    return Fail(SMX_INVALID_ARGUMENT, "scan_variant is 0 (scan) or 4 (timing ablation)");
+  if (scan_variant != 0 && scan_variant != 4 && scan_variant != 8)
+    return Fail(SMX_INVALID_ARGUMENT,
+                "scan_variant is 0 (scan), 4 (timing ablation) or 8 (diagnostic stamps)");
   if (chunk_tiles != 0 && (chunk_tiles < 16 || chunk_tiles > 65535))
     return Fail(SMX_INVALID_ARGUMENT, "chunk_tiles must be 0 (default) or in [16, 65535]");
-  if (candidates_per_query < 32 || candidates_per_query > 16384)
-    return Fail(SMX_INVALID_ARGUMENT, "candidates_per_query must be in [32, 16384]");
+  if (candidates_per_query < 32 || candidates_per_query > 8192)
+    return Fail(SMX_INVALID_ARGUMENT, "candidates_per_query must be in [32, 8192]");
   if (seed_leaves < 0) return Fail(SMX_INVALID_ARGUMENT, "seed_leaves must be >= 0");
   std::lock_guard<std::mutex> lock(h->mu);
   h->cap_per_query = uint32_t(candidates_per_query);

@@ -9,8 +9,7 @@ tree-AH LUT16 path:
 * ``ScannNumpy(artifacts_dir, assets_pbtxt)`` reloads a serialized searcher
   (scann_npy.cc:57-65) from the reference's artifacts layout
   (scann_amd.assets; an empty ``assets_pbtxt`` reads the directory's
-  scann_assets.pbtxt, scann.cc:246-264), or from this build's earlier own
-  format (TreeAHIndex.save, recognised by its smx_index.json);
+  scann_assets.pbtxt, scann.cc:246-264);
 * ``serialize`` writes the reference's layout (scann.cc:504-601,
   scann_npy.cc:272-282);
 * ``search`` / ``search_batched`` keep the argument order, the -1 = "config
@@ -20,9 +19,6 @@ tree-AH LUT16 path:
   the reference's "Error during search: " prefix (scann_npy.cc:41-55).
 """
 from __future__ import annotations
-
-import os
-from typing import Optional
 
 import numpy as np
 
@@ -35,15 +31,8 @@ class ScannNumpy:
     def __init__(self, db_or_dir, config: str, training_threads: int = 0, device: int = 0,
                  seed: int = 0):
         if isinstance(db_or_dir, str):
-            directory = db_or_dir
-            if os.path.exists(os.path.join(directory, "smx_index.json")):
-                with open(os.path.join(directory, "scann_config.pb")) as f:
-                    config = f.read()
-                self._cfg = search_config_from_text(config)
-                index = TreeAHIndex.load(directory)
-            else:
-                index, tree, self._cfg = assets.load_artifacts(directory, config or None)
-                config = assets.config_text(tree)
+            index, tree, self._cfg = assets.load_artifacts(db_or_dir, config or None)
+            config = assets.config_text(tree)
         else:
             self._cfg = search_config_from_text(config)
             db = np.ascontiguousarray(db_or_dir, dtype=np.float32)

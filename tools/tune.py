@@ -52,7 +52,8 @@ def main():
               f"lut={acc['lut_ms']:.3f} inv={acc['invert_ms']:.3f} seed={acc['seed_scan_ms']:.3f} "
               f"scan={acc['scan_ms']:.3f} sel={acc['select_ms']:.3f} retries={acc['overflow_retries']:.1f} "
               f"cand_mean={acc['mean_candidates']:.0f} cand_max={acc['max_candidates']:.0f} "
-              f"item_tiles={acc['scan_item_tiles']:.0f} mfma={mfma_tops:.0f}TOPS wall={wall_ms:.3f}ms", flush=True)
+              f"item_tiles={acc['scan_item_tiles']:.0f} mfma={mfma_tops:.0f}TOPS wall={wall_ms:.3f}ms "
+              f"wgs={acc['scan_workgroups']:.0f}", flush=True)
 
 
 if __name__ == "__main__":
