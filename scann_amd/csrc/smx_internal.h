@@ -143,6 +143,7 @@ struct SelectArgs {
   int32_t* out_count;
   int out_width;
   uint32_t* overflow;         // stats: [0] flag [1] max overflow [2] max count [8] sum [9] fallbacks
+  int stats;                  // also compute [2] and [8] (profiled calls)
   uint32_t* fallback;         // [nq] queries the wave kernel hands to the block kernel (or NULL)
   const uint32_t* qlist;      // block kernel over these queries only (or NULL: all)
   ShardEntry* shard_out;      // shard mode: [nq][kk] local top-k' entries (or NULL)

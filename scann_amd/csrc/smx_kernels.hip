@@ -29,6 +29,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "smx_internal.h"
 
@@ -56,6 +57,29 @@ __device__ __forceinline__ float FromOrdered(uint32_t o) {
 
 __device__ __forceinline__ uint32_t NextPow2(uint32_t x) {
   return x <= 1 ? 1u : 1u << (32 - __clz(x - 1));
+}
+
+// LDS hand-off between the lanes of ONE wave (the scan's workgroups are a
+// single wave): a wave's DS instructions execute in issue order, so all that
+// is needed is that the compiler keeps them in program order and that the
+// wave's outstanding LDS operations are complete.  Unlike __syncthreads()
+// this does not wait for the wave's global loads (the code-tile and next-item
+// prefetches stay in flight).
+__device__ __forceinline__ void WaveLdsSync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// Number of keys[0..n) below key (LDS, all lanes read the same words:
+// broadcasts), two keys per step and eight steps in flight.
+__device__ __forceinline__ uint32_t CountLess(const uint64_t* keys, uint32_t n, uint64_t key) {
+  uint32_t r = 0, j = 0;
+#pragma unroll 8
+  for (; j + 1 < n; j += 2) {
+    const uint64_t k0 = keys[j], k1 = keys[j + 1];
+    r += (k0 < key ? 1u : 0u) + (k1 < key ? 1u : 0u);
+  }
+  if (j < n) r += keys[j] < key ? 1u : 0u;
+  return r;
 }
 
 // Block-wide bitonic sort (ascending) of n (power of two) keys in LDS.
@@ -348,6 +372,232 @@ __device__ void TopLFinish(int qi, int L, uint32_t m, const uint64_t* sel, int32
   }
 }
 
+// The LUT of query qi by ONE wave (lanes 0..63; no workgroup barrier), the
+// same arithmetic as BuildLut.
+__device__ void BuildLutWave(int qi, const LutParams& p) {
+  const int lane = threadIdx.x & 63;
+  const float* q = p.queries + size_t(qi) * p.dim;
+  const int nb = p.nb, dpb = p.dpb;
+  const int nent = nb * 16;
+  const int last = p.dim - dpb * (nb - 1);
+  constexpr int kPer = (kMaxBlocks * 16) / 64;   // entries per lane
+  float raw[kPer];
+  float local_max = 0.0f;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int e = lane + 64 * u;
+    float v = 0.0f;
+    if (e < nent) {
+      const int b = e >> 4, c = e & 15;
+      const int nd = (b == nb - 1) ? last : dpb;
+      const float* qb = q + size_t(b) * dpb;
+      const float* cb = p.codebook + (size_t(b) * 16 + c) * dpb;
+      if (p.metric == 0) {
+        float s = __fmul_rn(qb[0], cb[0]);
+        for (int i = 1; i < nd; ++i) s = __fadd_rn(s, __fmul_rn(qb[i], cb[i]));
+        v = -s;
+      } else {
+        float t = __fsub_rn(qb[0], cb[0]);
+        float s = __fmul_rn(t, t);
+        for (int i = 1; i < nd; ++i) {
+          const float w = __fsub_rn(qb[i], cb[i]);
+          s = __fadd_rn(s, __fmul_rn(w, w));
+        }
+        v = s;
+      }
+    }
+    raw[u] = v;
+    local_max = fmaxf(local_max, fabsf(v));
+  }
+  for (int off = 32; off > 0; off >>= 1) local_max = fmaxf(local_max, __shfl_xor(local_max, off));
+  const float m = __fdiv_rn(127.0f, fmaxf(SqrtFltEps(), local_max));
+  const int tot = p.padded_blocks * 16;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int e = lane + 64 * u;
+    if (e < tot) {
+      int8_t v8 = 0;
+      if (e < nent) {
+        const float r = roundf(__fmul_rn(raw[u], m));
+        v8 = int8_t(int(r));
+        if (p.lut_u8) p.lut_u8[size_t(qi) * nent + e] = uint8_t(int(r) + 128);
+      }
+      p.lut[size_t(qi) * tot + e] = v8;
+    }
+  }
+  if (lane == 0) {
+    p.mult[qi] = m;
+    p.inv[qi] = p.residual ? float(1.0 / double(m)) : __fdiv_rn(1.0f, m);
+  }
+}
+
+// Exact top-L by (score, center index) with ONE wave per query (4 queries
+// per 256-thread block, no workgroup barriers), the row in registers (VPL
+// scores per lane, nl <= 64 * VPL).  Linear 256-bin histograms of the
+// ordered score bits between the row's current [lo, hi] (radix digits of
+// nearby floats would all hit one bin) narrow down to the bin holding the
+// L-th score; every key below that bin and the keys inside it are compacted
+// in LDS (ballot prefix) and ordered by a counting rank over (score, leaf)
+// (keys are unique), of which the first L are kept.  Then the pairs' ranks
+// in their leaves' lists and the query's LUT (the front end's tail, as
+// TopLFinish).
+constexpr int kWaveTopL = 256;   // L limit of the wave kernel
+constexpr int kWaveTopCand = 512;   // compacted keys one wave can order
+
+template <int VPL>
+__global__ void __launch_bounds__(256) topl_wave_kernel(const float* __restrict__ scores, int nq,
+                                                        int nl, int L, int32_t* __restrict__ out_leaf,
+                                                        float* __restrict__ out_dist, TopLTail tail) {
+  __shared__ uint32_t hist[4][256];
+  __shared__ uint64_t sel[4][kWaveTopCand];
+  __shared__ uint64_t srt[4][kWaveTopL];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int qi = blockIdx.x * 4 + wv;
+  if (qi >= nq) return;
+  const float* row = scores + size_t(qi) * nl;
+  uint32_t* hs = hist[wv];
+  // per score: its ordered bits and its state: 0 = taken (below the
+  // boundary bin), 1 = boundary candidate, 2 = out
+  uint32_t v[VPL];
+  uint8_t st[VPL];
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    const int cix = lane + 64 * u;
+    v[u] = cix < nl ? OrderedBits(row[cix]) : 0xFFFFFFFFu;
+    st[u] = cix < nl ? 1 : 2;
+  }
+  const uint32_t m = min(uint32_t(L), uint32_t(nl));
+  uint32_t below = 0, incnt = uint32_t(nl);
+  for (int round = 0; round < 6 && below + incnt > uint32_t(kWaveTopCand); ++round) {
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+#pragma unroll
+    for (int u = 0; u < VPL; ++u)
+      if (st[u] == 1) {
+        lo = min(lo, v[u]);
+        hi = max(hi, v[u]);
+      }
+    for (int off = 32; off > 0; off >>= 1) {
+      lo = min(lo, uint32_t(__shfl_xor(int(lo), off)));
+      hi = max(hi, uint32_t(__shfl_xor(int(hi), off)));
+    }
+    if (lo == hi) break;   // one value left in the boundary set
+    // bin = floor((v - lo) * scale / 2^32), scale = floor(255.99 * 2^32 / span):
+    // monotone in v, 0 at lo, <= 255 at hi (no division per value)
+    const uint64_t scale = ((uint64_t(255) << 32) + 0xFFFFFFFFull) / (uint64_t(hi - lo));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) hs[lane + 64 * u] = 0;
+    WaveLdsSync();
+#pragma unroll
+    for (int u = 0; u < VPL; ++u)
+      if (st[u] == 1) atomicAdd(&hs[uint32_t((uint64_t(v[u] - lo) * scale) >> 32)], 1u);
+    WaveLdsSync();
+    const uint32_t h0 = hs[4 * lane], h1 = hs[4 * lane + 1], h2 = hs[4 * lane + 2],
+                   h3 = hs[4 * lane + 3];
+    uint32_t incl = h0 + h1 + h2 + h3;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t t = __shfl_up(incl, off);
+      if (lane >= off) incl += t;
+    }
+    const uint32_t excl = incl - (h0 + h1 + h2 + h3);
+    const uint32_t need = m - below;
+    const bool mine = excl < need && incl >= need;
+    uint32_t bsel = 0, cum = excl, hb = 0;
+    if (mine) {
+      const uint32_t hv[4] = {h0, h1, h2, h3};
+      int u = 0;
+      while (cum + hv[u] < need) { cum += hv[u]; ++u; }
+      bsel = 4 * lane + u;
+      hb = hv[u];
+    }
+    const int src = __ffsll((unsigned long long)__ballot(mine)) - 1;
+    bsel = __shfl(bsel, src);
+    cum = __shfl(cum, src);
+    hb = __shfl(hb, src);
+#pragma unroll
+    for (int u = 0; u < VPL; ++u)
+      if (st[u] == 1) {
+        const uint32_t bn = uint32_t((uint64_t(v[u] - lo) * scale) >> 32);
+        st[u] = bn < bsel ? 0 : bn > bsel ? 2 : 1;
+      }
+    below += cum;
+    incnt = hb;
+    WaveLdsSync();
+  }
+  // the taken keys and the boundary candidates, in LDS
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    const bool in = st[u] <= 1;
+    const uint64_t bal = __ballot(in);
+    if (in) {
+      const uint32_t pos = cnt + uint32_t(__popcll(bal & ((1ull << lane) - 1ull)));
+      if (pos < uint32_t(kWaveTopCand)) sel[wv][pos] = (uint64_t(v[u]) << 32) | uint32_t(lane + 64 * u);
+    }
+    cnt += uint32_t(__popcll(bal));
+  }
+  WaveLdsSync();
+  if (cnt <= uint32_t(kWaveTopCand)) {
+    // counting rank over (score, leaf), keys unique; keep the first m
+    const uint64_t* sk = sel[wv];
+    for (uint32_t i = lane; i < cnt; i += 64) {
+      const uint64_t key = sk[i];
+      uint32_t r = 0;
+      uint32_t j = 0;
+#pragma unroll 8
+      for (; j + 1 < cnt; j += 2) {
+        const uint64_t k0 = sk[j], k1 = sk[j + 1];
+        r += (k0 < key ? 1u : 0u) + (k1 < key ? 1u : 0u);
+      }
+      if (j < cnt) r += sk[j] < key ? 1u : 0u;
+      if (r < m) srt[wv][r] = key;
+    }
+  } else {
+    // more than kWaveTopCand keys on one boundary value (all-equal rows):
+    // the keys below it by rank, then the lowest-index ties in index order
+    uint32_t T = 0;
+#pragma unroll
+    for (int u = 0; u < VPL; ++u)
+      if (st[u] == 1) T = v[u];
+    for (int off = 32; off > 0; off >>= 1) T = max(T, uint32_t(__shfl_xor(int(T), off)));
+    uint32_t c2 = 0;
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+      const bool in = st[u] == 0;
+      const uint64_t bal = __ballot(in);
+      if (in) sel[wv][c2 + uint32_t(__popcll(bal & ((1ull << lane) - 1ull)))] =
+          (uint64_t(v[u]) << 32) | uint32_t(lane + 64 * u);
+      c2 += uint32_t(__popcll(bal));
+    }
+    WaveLdsSync();
+    for (uint32_t i = lane; i < c2; i += 64) {
+      const uint64_t key = sel[wv][i];
+      uint32_t r = 0;
+      for (uint32_t j = 0; j < c2; ++j) r += sel[wv][j] < key ? 1u : 0u;
+      srt[wv][r] = key;
+    }
+    uint32_t t = 0;
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+      const bool te = st[u] == 1;
+      const uint64_t bal = __ballot(te);
+      if (te) {
+        const uint32_t pos = c2 + t + uint32_t(__popcll(bal & ((1ull << lane) - 1ull)));
+        if (pos < m) srt[wv][pos] = (uint64_t(T) << 32) | uint32_t(lane + 64 * u);
+      }
+      t += uint32_t(__popcll(bal));
+    }
+  }
+  WaveLdsSync();
+  for (int i = lane; i < L; i += 64) {
+    const bool has = uint32_t(i) < m;
+    const int32_t leaf = has ? int32_t(srt[wv][i] & 0xFFFFFFFFu) : -1;
+    out_leaf[size_t(qi) * L + i] = leaf;
+    out_dist[size_t(qi) * L + i] = has ? FromOrdered(uint32_t(srt[wv][i] >> 32)) : __int_as_float(0x7fc00000);
+    if (tail.leaf_count && has) tail.rank[size_t(qi) * L + i] = atomicAdd(&tail.leaf_count[leaf], 1u);
+  }
+  if (tail.lut.lut) BuildLutWave(qi, tail.lut);
+}
+
 __global__ void __launch_bounds__(256) topl_select_kernel(const float* __restrict__ scores, int nl,
                                                           int L, uint32_t kcap,
                                                           int32_t* __restrict__ out_leaf,
@@ -505,7 +755,7 @@ __global__ void __launch_bounds__(1024) worklist_kernel(
     const uint32_t* __restrict__ leaf_size, int nl, int nb, uint32_t chunk_tiles,
     uint32_t* __restrict__ leaf_item0, uint32_t* __restrict__ pos_unit0,
     uint32_t* __restrict__ gunits, uint32_t* __restrict__ totals,
-    unsigned long long* __restrict__ code_bytes) {
+    unsigned long long* __restrict__ code_bytes, int grid, uint4* __restrict__ wave_start) {
   __shared__ uint32_t s_items[1024], s_wt[1024], s_pairs[1024];
   __shared__ unsigned long long s_bytes[1024];
   const int tid = threadIdx.x;
@@ -588,6 +838,13 @@ __global__ void __launch_bounds__(1024) worklist_kernel(
     totals[1] = s_items[nt - 1];
     totals[2] = total_w;
   }
+  // the waves of groups without units get an empty share (the items kernel
+  // writes every other wave's share)
+  __syncthreads();
+  for (int i = tid; i < grid; i += nt) {
+    const int g = i & (kGroups - 1);
+    if (gunits[g + 1] == gunits[g]) wave_start[i] = make_uint4(0, 0, 0, 0);
+  }
 }
 
 // Phase 2 (one 64-thread block per leaf position): the leaf's work items,
@@ -656,15 +913,6 @@ __global__ void __launch_bounds__(64) items_kernel(
   }
 }
 
-// Waves of groups with no units at all (or of a grid too short for the
-// snake above) get an empty share.
-__global__ void wave_clear_kernel(const uint32_t* __restrict__ gunits, int grid,
-                                  uint4* __restrict__ wave_start) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= grid) return;
-  const int g = i & (kGroups - 1);
-  if (gunits[g + 1] == gunits[g]) wave_start[i] = make_uint4(0, 0, 0, 0);
-}
 
 // ---------------------------------------------------------------------------
 // LUT16 scan on MFMA.
@@ -993,15 +1241,6 @@ __device__ __forceinline__ v16i TileMfma(const uint32_t* codes, const v4i (&b)[K
 // result consumed at the next item's start, behind that item's loads).
 // ABL = 4: timing ablation without the epilogue (results invalid).
 // ---------------------------------------------------------------------------
-// LDS hand-off between the lanes of ONE wave (the scan's workgroups are a
-// single wave): a wave's DS instructions execute in issue order, so all that
-// is needed is that the compiler keeps them in program order and that the
-// wave's outstanding LDS operations are complete.  Unlike __syncthreads()
-// this does not wait for the wave's global loads (the code-tile and next-item
-// prefetches stay in flight).
-__device__ __forceinline__ void WaveLdsSync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
 
 constexpr int kHitsPerWave = 64;   // a tile adds at most one hit per lane
 constexpr int kItemKeys = 256;   // survivors one work item stages in LDS
@@ -1050,9 +1289,12 @@ __global__ void __launch_bounds__(64, (K <= 25 ? SMX_SCAN_WAVES_PER_SIMD : 2))
   constexpr int R = 3;   // one-hot reads in flight ahead of their MFMA
   __shared__ uint4 hsum[HW][2];     // 16 sums as int16 pairs
   __shared__ uint32_t hmeta[HW];    // tile << 6 | lane
-  __shared__ uint64_t kbuf[KB];        // the item's survivors (all its queries)
-  __shared__ uint8_t kslot[KB];        // their query slots
-  __shared__ uint32_t qcnt[Q], q_slot[Q], s_kn;
+  // survivors of an item (all its queries) and their query slots, double
+  // buffered: an item's are copied to the lists during the next item
+  __shared__ uint64_t kbuf[2][KB];
+  __shared__ uint8_t kslot[2][KB];
+  __shared__ uint32_t s_kn[2];
+  __shared__ uint32_t qcnt[Q], q_slot[Q], qrun[Q], prev_qid[Q];
   __shared__ QParam qp[Q];
   __shared__ v4i oh_tab[16];
   const int lane = threadIdx.x;
@@ -1075,8 +1317,27 @@ __global__ void __launch_bounds__(64, (K <= 25 ? SMX_SCAN_WAVES_PER_SIMD : 2))
   ItemLane cl = a.lanes[size_t(w) * Q + c];
   bool pending = false;   // the previous item's survivors await their copy
   uint32_t slot = 0;      // that copy's first list slot (lanes < 32)
-  while (units > 0 || pending) {
-    const bool has = units > 0;
+  uint32_t par = 0;       // this item's survivor buffer
+  // the previous item's survivors to their queries' lists: each key's place =
+  // its query's reserved first slot (the returned value of the item-end
+  // atomic, waited for only here) + a running count
+  auto copy_prev = [&]() {
+    const uint32_t pp = par ^ 1u;
+    if (lane < Q) {
+      q_slot[lane] = slot;
+      qrun[lane] = 0;
+    }
+    WaveLdsSync();
+    const uint32_t kn = min(s_kn[pp], uint32_t(KB));
+    for (uint32_t e = uint32_t(lane); e < kn; e += 64) {
+      const uint32_t qs = kslot[pp][e];
+      const uint32_t sl = q_slot[qs] + atomicAdd(&qrun[qs], 1u);
+      if (sl < a.cap) a.cand[size_t(prev_qid[qs]) * a.cap + sl] = kbuf[pp][e];
+    }
+    WaveLdsSync();
+    pending = false;
+  };
+  while (units > 0) {
     if (ABL & 8) {
       st_rt = __builtin_amdgcn_s_memrealtime();
       st_t0 = __builtin_amdgcn_s_memtime();
@@ -1091,30 +1352,12 @@ __global__ void __launch_bounds__(64, (K <= 25 ? SMX_SCAN_WAVES_PER_SIMD : 2))
     v4i b[K];
     uint32_t codes[NW] = {};
     const uint8_t* tb = a.tiles + cur.tile_off * 64ull * W + size_t(lane) * W;
-    if (has) {
+    {
       const v4i* src = reinterpret_cast<const v4i*>(a.lut) + size_t(cl.qid) * 2 * K + h;
 #pragma unroll
       for (int s = 0; s < K; ++s) b[s] = src[2 * s];
       if (j0 < jend) LoadCodes<K>(tb + size_t(j0) * 64 * W, codes);   // (empty leaf: no tile)
     }
-    if (pending) {
-      // the previous item's staged survivors to their queries' lists: each
-      // key's place = its query's reserved first slot + a running count
-      if (lane < Q) {
-        q_slot[lane] = slot;
-        qcnt[lane] = 0;
-      }
-      WaveLdsSync();
-      const uint32_t kn = min(s_kn, uint32_t(KB));
-      for (uint32_t e = uint32_t(lane); e < kn; e += 64) {
-        const uint32_t qs = kslot[e];
-        const uint32_t sl = q_slot[qs] + atomicAdd(&qcnt[qs], 1u);
-        if (sl < a.cap) a.cand[size_t(qp[qs].qid) * a.cap + sl] = kbuf[e];
-      }
-      WaveLdsSync();
-      pending = false;
-    }
-    if (!has) break;
     // the next item's descriptor and record, in flight during this item
     const uint32_t wn = min(w + 1, a.num_items - 1);
     const WorkItem nxt = work[wn];
@@ -1132,7 +1375,7 @@ __global__ void __launch_bounds__(64, (K <= 25 ? SMX_SCAN_WAVES_PER_SIMD : 2))
       qp[lane] = v;
       qcnt[lane] = 0;
     }
-    if (lane == 0) s_kn = 0;
+    if (lane == 0) s_kn[par] = 0;
     units -= jend - j0;
     jfirst = 0;
     WaveLdsSync();
@@ -1162,10 +1405,10 @@ __global__ void __launch_bounds__(64, (K <= 25 ? SMX_SCAN_WAVES_PER_SIMD : 2))
                                              : a.members[moff + dp];
             const uint64_t key = (uint64_t(OrderedBits(d)) << 32) | tie;
             if (key <= TT) {
-              const uint32_t p = atomicAdd(&s_kn, 1u);
+              const uint32_t p = atomicAdd(&s_kn[par], 1u);
               if (p < uint32_t(KB)) {
-                kbuf[p] = key;
-                kslot[p] = uint8_t(cc);
+                kbuf[par][p] = key;
+                kslot[par][p] = uint8_t(cc);
                 atomicAdd(&qcnt[cc], 1u);
               } else {  // item buffer full (rare): straight to the global list
                 const uint32_t gs = atomicAdd(&a.cand_count[qq], 1u);
@@ -1240,12 +1483,14 @@ __global__ void __launch_bounds__(64, (K <= 25 ? SMX_SCAN_WAVES_PER_SIMD : 2))
       for (uint32_t j = j0;; j += 2) {
         LoadCodes<K>(tb + size_t(min(j + 1, jl)) * 64 * W, cb);
         tile(codes, j);
+        if (pending) copy_prev();   // after the item's first tile: the atomic has returned
         if (j + 1 >= jend) break;
         LoadCodes<K>(tb + size_t(min(j + 2, jl)) * 64 * W, codes);
         tile(cb, j + 1);
         if (j + 2 >= jend) break;
       }
     }
+    if (pending) copy_prev();   // (an item without tiles)
     if (ABL & 8) st_t2 = __builtin_amdgcn_s_memtime();
     if (ABL & 8) {
       uint32_t sv = lane < Q ? qcnt[lane] : 0u;
@@ -1257,8 +1502,10 @@ __global__ void __launch_bounds__(64, (K <= 25 ? SMX_SCAN_WAVES_PER_SIMD : 2))
     if (lane < Q) {
       const uint32_t m = qcnt[lane];
       slot = m ? atomicAdd(&a.cand_count[cl.qid], m) : 0u;
+      prev_qid[lane] = cl.qid;
     }
     pending = true;
+    par ^= 1u;
     if ((ABL & 8) && lane == 0)
       StampItem(a, w, st_rt, st_t0, st_t1, st_t2, __builtin_amdgcn_s_memtime(),
                 uint64_t(jend - j0) | (uint64_t(st_hits) << 16) | (uint64_t(st_surv) << 40));
@@ -1266,6 +1513,7 @@ __global__ void __launch_bounds__(64, (K <= 25 ? SMX_SCAN_WAVES_PER_SIMD : 2))
     cl = nrec;
     ++w;
   }
+  if (pending) copy_prev();
 }
 
 // One-query variant for the stage entry point: raw sums of one leaf.
@@ -1374,6 +1622,10 @@ __global__ void __launch_bounds__(256) final_select_kernel(SelectArgs a) {
   extern __shared__ uint64_t lds[];
   const int qi = a.qlist ? int(a.qlist[blockIdx.x]) : int(blockIdx.x);
   const uint32_t raw_n = a.cand_count[qi];
+  if (threadIdx.x == 0 && raw_n > a.cap && !a.qlist) {   // overflow: the host tightens and rescans
+    a.overflow[0] = 1u;
+    atomicMax(&a.overflow[1], raw_n);
+  }
 
   const uint32_t n = min(raw_n, a.cap);
   // LDS: keys[kcap] | sel[selcap] | aux[kkp2] | q[dim] | gid[kk] | dist[kk] | hist | scan
@@ -1563,6 +1815,10 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int qi = blockIdx.x;
   const uint32_t raw_n = a.cand_count[qi];
+  if (threadIdx.x == 0 && raw_n > a.cap && !a.qlist) {   // overflow: the host tightens and rescans
+    a.overflow[0] = 1u;
+    atomicMax(&a.overflow[1], raw_n);
+  }
   if (tid == 0) s_c = 0;
   const uint32_t n = min(raw_n, a.cap);
   const uint32_t k = uint32_t(a.kk);
@@ -1634,7 +1890,7 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
   if (uint32_t(tid) < c) {
     const uint64_t key = sel[tid];
     uint32_t r = 0;
-    for (uint32_t j = 0; j < c; ++j) r += sel[j] < key ? 1u : 0u;
+    r = CountLess(sel, c, key);
     out[r] = key;
   }
   __syncthreads();
@@ -1717,10 +1973,15 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
   if (a.reorder && !a.pre_only) ExactDistances8(a, rows, rowid, m, dist, qi);
   // final (distance, global id) rank; keep the output width
   const uint32_t keep = min(m, uint32_t(a.out_width));
+  uint64_t fkey = 0;
   if (uint32_t(tid) < m) {
-    const uint64_t key = (uint64_t(OrderedBits(dist[tid])) << 32) | gid[tid];
-    uint32_t r = 0;
-    for (uint32_t j = 0; j < m; ++j) r += ((uint64_t(OrderedBits(dist[j])) << 32) | gid[j]) < key;
+    fkey = (uint64_t(OrderedBits(dist[tid])) << 32) | gid[tid];
+    sel[tid] = fkey;
+  }
+  __syncthreads();
+  if (uint32_t(tid) < m) {
+    const uint64_t key = fkey;
+    const uint32_t r = CountLess(sel, m, key);
     if (r < keep) {
       a.out_idx[size_t(qi) * a.out_width + r] = uint32_t(key & 0xFFFFFFFFu);
       a.out_dist[size_t(qi) * a.out_width + r] = FromOrdered(uint32_t(key >> 32));
@@ -1885,8 +2146,8 @@ __global__ void __launch_bounds__(1024) cand_stats_kernel(const uint32_t* __rest
       mx = max(mx, s_max[w]);
       sum += s_sum[w];
     }
-    stats[0] = over ? 1u : 0u;
-    stats[1] = over;
+    if (over) stats[0] = 1u;
+    stats[1] = max(stats[1], over);
     stats[2] = mx;
     stats[8] = sum;
   }
@@ -1925,10 +2186,11 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   const FrontArgs none{};
   const FrontArgs& f = front ? *front : none;
   TopLTail tail{};
-  tail.leaf_count = f.leaf_count;
+  static const int dbg = [] { const char* e = std::getenv("SMX_DBG_FRONT"); return e ? std::atoi(e) : 0; }();
+  tail.leaf_count = (dbg & 1) ? nullptr : f.leaf_count;
   tail.rank = f.rank;
   tail.lut = LutParams{queries, ix.dim, ix.codebook, ix.nb, ix.dpb, 2 * ix.ksteps, ix.metric,
-                       ix.residual, f.lut, f.mult, f.inv, nullptr};
+                       ix.residual, (dbg & 2) ? nullptr : f.lut, f.mult, f.inv, nullptr};
   hipLaunchKernelGGL(partition_scores_kernel,
                      dim3((nq + kPartTile - 1) / kPartTile, (ix.nl + kPartTile - 1) / kPartTile),
                      dim3(256), 0, s, queries, nq, ix.dim, ix.centers, ix.cnorm, ix.nl, ix.metric,
@@ -1936,7 +2198,13 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   // static LDS of the kernel besides the dynamic key buffers: the LUT build's
   // raw table and reduction (~5 KB) and the selection's words
   constexpr size_t kStaticLds = 6 * 1024;
-  if (ix.nl <= kLdsSelectLeaves && lds + kStaticLds <= 160 * 1024) {
+  if (L <= kWaveTopL && ix.nl <= 64 * 16) {
+    hipLaunchKernelGGL(topl_wave_kernel<16>, dim3((nq + 3) / 4), dim3(256), 0, s, scores, nq, ix.nl,
+                       L, out_leaf, out_dist, tail);
+  } else if (L <= kWaveTopL && ix.nl <= 64 * 32) {
+    hipLaunchKernelGGL(topl_wave_kernel<32>, dim3((nq + 3) / 4), dim3(256), 0, s, scores, nq, ix.nl,
+                       L, out_leaf, out_dist, tail);
+  } else if (ix.nl <= kLdsSelectLeaves && lds + kStaticLds <= 160 * 1024) {
     hipLaunchKernelGGL(topl_select_kernel, dim3(nq), dim3(256), lds, s, scores, ix.nl, L, kcap,
                        out_leaf, out_dist, tail);
   } else {
@@ -1964,9 +2232,7 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
                           unsigned long long* code_bytes, uint32_t chunk_tiles, hipStream_t s) {
   hipLaunchKernelGGL(worklist_kernel, dim3(1), dim3(1024), 0, s, leaf_count, ix.leaf_order,
                      ix.leaf_size, ix.nl, ix.nb, chunk_tiles, leaf_item0, pos_unit0, gunits, totals,
-                     code_bytes);
-  hipLaunchKernelGGL(wave_clear_kernel, dim3((grid + 255) / 256), dim3(256), 0, s, gunits, grid,
-                     wave_start);
+                     code_bytes, grid, wave_start);
   hipLaunchKernelGGL(items_kernel, dim3(ix.nl), dim3(64), 0, s, leaf_count, ix.leaf_order,
                      ix.leaf_size, ix.tile_off, ix.member_off, chunk_tiles, grid, leaf_item0,
                      pos_unit0, gunits, work, lanes, wave_start);
@@ -2110,7 +2376,9 @@ hipError_t LaunchMergeShards(const MergeArgs& a, hipStream_t s) {
 
 hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s) {
   if (nq == 0) return hipSuccess;
-  if (!a.qlist)
+  // the overflow flag is raised by the select kernels themselves; the
+  // candidate-count statistics only for profiled calls
+  if (!a.qlist && a.stats)
     hipLaunchKernelGGL(cand_stats_kernel, dim3(1), dim3(1024), 0, s, a.cand_count, nq, a.cap,
                        a.overflow);
   uint32_t kkp2 = 1;

@@ -468,6 +468,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sel.out_count = out_count;
   sel.out_width = width;
   sel.overflow = stats;
+  sel.stats = h->profiling ? 1 : 0;
   sel.fallback = w.fallback;
   sel.qlist = nullptr;
   sel.shard_out = shard_out;
