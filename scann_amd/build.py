@@ -31,18 +31,22 @@ def needs_build() -> bool:
     return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, defines=(), out: str = OUT) -> str:
+    """The product library; `defines` + `out` make a diagnostic variant
+    (e.g. ("SMX_PHASE_STAMPS",) -> lib/libscann_mi355x_ps.so, loaded through
+    $SMX_LIB by the tools only)."""
+    if not force and out == OUT and not needs_build():
         return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    tmp = OUT + f".tmp{os.getpid()}"
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = out + f".tmp{os.getpid()}"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-Wall", "-o", tmp] + [os.path.join(CSRC, f) for f in SOURCES]
+           "-ffp-contract=off", "-Wall", "-o", tmp] + [f"-D{d}" for d in defines] + \
+        [os.path.join(CSRC, f) for f in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

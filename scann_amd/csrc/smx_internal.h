@@ -15,6 +15,11 @@ constexpr int kDpPerTile = 32;
 constexpr int kMaxBlocks = 64;           // LUT16 blocks supported (K <= 32)
 constexpr uint64_t kNoThreshold = ~0ull;
 constexpr int kWorkGroups = 8;        // XCD groups of the scan's work list
+// Per-leaf list counters and per-query candidate counters take a 128-byte
+// line each: device-scope atomics on one line serialize, and 100k returning
+// atomics over 1000 packed counters (32 lines) cost ~12 us where one line per
+// counter costs ~1 us.  counter(i) = base[i * kCounterStride].
+constexpr uint32_t kCounterStride = 32;
 
 // Bytes of code data one lane holds per 32-datapoint tile: lane (r, h) keeps
 // the nibbles of datapoint r for blocks h, h+2, h+4, ... (K = ceil(B/2)).
@@ -90,7 +95,7 @@ struct ScanArgs {
   uint32_t num_items;
   const uint64_t* tau_key;    // [nq] emission threshold keys
   uint64_t* cand;             // [nq][cap]
-  uint32_t* cand_count;       // [nq]
+  uint32_t* cand_count;       // [nq] strided (kCounterStride)
   unsigned long long* stamps; // diagnostic variant 8 only: [cap][8] per-item stamps
   uint32_t* stamp_count;
   uint32_t stamp_cap;
@@ -169,9 +174,11 @@ struct MergeArgs {
 // Per-call state the partition kernel resets on its way (no memset nodes):
 // counters to 0, candidate counts to 0, thresholds to "open".
 struct StateInit {
-  uint32_t* counters = nullptr;
+  uint32_t* counters = nullptr;     // n_counters strided leaf counters
   uint32_t n_counters = 0;
-  uint32_t* cand_count = nullptr;
+  uint32_t* stats = nullptr;        // n_stats packed words
+  uint32_t n_stats = 0;
+  uint32_t* cand_count = nullptr;   // n_cand strided counters
   uint32_t n_cand = 0;
   uint64_t* tau = nullptr;
   uint32_t n_tau = 0;
@@ -181,7 +188,7 @@ struct StateInit {
 // the partition / top-L launches.  NULL members are skipped.
 struct FrontArgs {
   StateInit init;
-  uint32_t* leaf_count = nullptr;   // [nl], zeroed by init
+  uint32_t* leaf_count = nullptr;   // [nl] strided (kCounterStride), zeroed by init
   uint32_t* rank = nullptr;         // [nq][L]
   int8_t* lut = nullptr;            // [nq][2K][16]
   float* mult = nullptr;            // [nq]
@@ -224,6 +231,10 @@ hipError_t LaunchExactDistances(const DeviceIndex& ix, const float* queries, int
                                 const uint32_t* ids, int k, float* out, hipStream_t s);
 hipError_t LaunchLeafScores(const DeviceIndex& ix, int leaf, const int8_t* lut,
                             int32_t* out, hipStream_t s);
+// Diagnostic build only (-DSMX_PHASE_STAMPS): where the phase stamps go
+// ([3 kernels][kPhaseQueries][8] u64, or NULL).
+constexpr int kPhaseQueries = 4096;
+hipError_t SetPhaseStamps(unsigned long long* p);
 hipError_t LaunchFill64(uint64_t* p, uint64_t v, size_t n, hipStream_t s);
 
 }  // namespace smx

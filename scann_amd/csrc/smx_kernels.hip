@@ -55,6 +55,22 @@ __device__ __forceinline__ float FromOrdered(uint32_t o) {
   return __uint_as_float(u);
 }
 
+// Diagnostic build only (-DSMX_PHASE_STAMPS, tools/phase_stamps.py): the
+// 100 MHz clock at phase boundaries of the front-end and select kernels,
+// [kernel][query][8].  Compiled out of the product library.
+#ifdef SMX_PHASE_STAMPS
+__device__ unsigned long long* g_phase_stamps;
+#define SMX_PHASE(kid, qi, ph)                                                             \
+  do {                                                                                     \
+    if (g_phase_stamps && (threadIdx.x & 63) == 0)                                         \
+      g_phase_stamps[((size_t(kid) * kPhaseQueries) + (qi)) * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define SMX_PHASE(kid, qi, ph) \
+  do {                         \
+  } while (0)
+#endif
+
 __device__ __forceinline__ uint32_t NextPow2(uint32_t x) {
   return x <= 1 ? 1u : 1u << (32 - __clz(x - 1));
 }
@@ -67,6 +83,19 @@ __device__ __forceinline__ uint32_t NextPow2(uint32_t x) {
 // prefetches stay in flight).
 __device__ __forceinline__ void WaveLdsSync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// Inclusive block scan of one value per thread (256 threads).
+__device__ __forceinline__ uint32_t BlockInclusiveScan256(uint32_t v, uint32_t* wsum) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = uint32_t(__shfl_up(int(v), off));
+    if (lane >= off) v += t;
+  }
+  if (lane == 63) wsum[wid] = v;
+  __syncthreads();
+  for (int w = 0; w < wid; ++w) v += wsum[w];
+  return v;
 }
 
 // Number of keys[0..n) below key (LDS, all lanes read the same words:
@@ -213,8 +242,9 @@ __global__ void __launch_bounds__(256) partition_scores_kernel(
     // launch reads it, the top-L launch that follows does
     const uint32_t gt = (blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
     const uint32_t gs = gridDim.x * gridDim.y * blockDim.x;
-    for (uint32_t i = gt; i < init.n_counters; i += gs) init.counters[i] = 0u;
-    for (uint32_t i = gt; i < init.n_cand; i += gs) init.cand_count[i] = 0u;
+    for (uint32_t i = gt; i < init.n_counters; i += gs) init.counters[size_t(i) * kCounterStride] = 0u;
+    for (uint32_t i = gt; i < init.n_stats; i += gs) init.stats[i] = 0u;
+    for (uint32_t i = gt; i < init.n_cand; i += gs) init.cand_count[size_t(i) * kCounterStride] = 0u;
     for (uint32_t i = gt; i < init.n_tau; i += gs) init.tau[i] = kNoThreshold;
   }
   __shared__ float qs[kPartTile][kPartChunk + 1];
@@ -248,14 +278,23 @@ __global__ void __launch_bounds__(256) partition_scores_kernel(
   const float cscale = metric == 1 ? 2.0f : 1.0f;
   for (int d0 = 0; d0 < dim; d0 += kPartChunk) {
     __syncthreads();
+    // all loads of the chunk in flight together: clamped indices, the
+    // padding applied after (a guarded load waits on its own)
+    constexpr int kPer = (kPartTile * kPartChunk) / 256;
+    float qv[kPer], cv[kPer];
 #pragma unroll
-    for (int i = 0; i < (kPartTile * kPartChunk) / 256; ++i) {
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + i * 256;
+      const int row = e / kPartChunk, col = e % kPartChunk, d = min(d0 + col, dim - 1);
+      qv[i] = queries[size_t(min(qt + row, nq - 1)) * dim + d];
+      cv[i] = centers[size_t(min(ct + row, nl - 1)) * dim + d];
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
       const int e = tid + i * 256;
       const int row = e / kPartChunk, col = e % kPartChunk, d = d0 + col;
-      const float* qrow = queries + size_t(min(qt + row, nq - 1)) * dim;
-      const float* crow = centers + size_t(min(ct + row, nl - 1)) * dim;
-      qs[row][col] = d < dim ? -qrow[d] : -0.0f;
-      cs[row][col] = d < dim ? __fmul_rn(crow[d], cscale) : 0.0f;
+      qs[row][col] = d < dim ? -qv[i] : -0.0f;
+      cs[row][col] = d < dim ? __fmul_rn(cv[i], cscale) : 0.0f;
     }
     __syncthreads();
     const int steps = min(kPartChunk, ((dim - d0) + 1) & ~1);
@@ -292,55 +331,72 @@ struct LutParams {
   uint8_t* lut_u8;   // optional biased uint8 copy (stage entry point)
 };
 
-// The LUT of query qi by one 256-thread block (all threads must call).
+// The LUT of query qi by one 256-thread block (all threads must call), four
+// entries per thread.  Dimension i of a thread's entries is loaded for all of
+// them at once (clamped indices, no guarded loads: a guarded load waits on its
+// own), then accumulated in the reference's order.
 __device__ void BuildLut(int qi, const LutParams& p) {
-  __shared__ float raw[kMaxBlocks * 16];
-  __shared__ float red[256];
+  __shared__ float red[4];
+  constexpr int kPer = (kMaxBlocks * 16) / 256;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const float* q = p.queries + size_t(qi) * p.dim;
   const int nb = p.nb, dpb = p.dpb;
   const int nent = nb * 16;
   const int last = p.dim - dpb * (nb - 1);
-  float local_max = 0.0f;
-  for (int e = threadIdx.x; e < nent; e += blockDim.x) {
-    const int b = e >> 4, c = e & 15;
-    const int nd = (b == nb - 1) ? last : dpb;
-    const float* qb = q + size_t(b) * dpb;
-    const float* cb = p.codebook + (size_t(b) * 16 + c) * dpb;
-    float v;
-    if (p.metric == 0) {
-      float s = __fmul_rn(qb[0], cb[0]);
-      for (int i = 1; i < nd; ++i) s = __fadd_rn(s, __fmul_rn(qb[i], cb[i]));
-      v = -s;
-    } else {
-      float t = __fsub_rn(qb[0], cb[0]);
-      float s = __fmul_rn(t, t);
-      for (int i = 1; i < nd; ++i) {
-        const float u = __fsub_rn(qb[i], cb[i]);
-        s = __fadd_rn(s, __fmul_rn(u, u));
-      }
-      v = s;
+  float raw[kPer];
+  for (int i = 0; i < dpb; ++i) {
+    float qv[kPer], cv[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int e = min(t + 256 * u, nent - 1);
+      const int b = e >> 4, c = e & 15;
+      qv[u] = q[min(b * dpb + i, p.dim - 1)];
+      cv[u] = p.codebook[(size_t(b) * 16 + c) * dpb + i];
     }
-    raw[e] = v;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int b = min(t + 256 * u, nent - 1) >> 4;
+      const int nd = (b == nb - 1) ? last : dpb;
+      float v;
+      if (p.metric == 0) {
+        v = __fmul_rn(qv[u], cv[u]);
+      } else {
+        const float w = __fsub_rn(qv[u], cv[u]);
+        v = __fmul_rn(w, w);
+      }
+      if (i == 0) raw[u] = v;
+      else if (i < nd) raw[u] = __fadd_rn(raw[u], v);
+    }
+  }
+  float local_max = 0.0f;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int e = t + 256 * u;
+    float v = 0.0f;
+    if (e < nent) v = p.metric == 0 ? -raw[u] : raw[u];
+    raw[u] = v;
     local_max = fmaxf(local_max, fabsf(v));
   }
-  red[threadIdx.x] = local_max;
+  for (int off = 32; off > 0; off >>= 1) local_max = fmaxf(local_max, __shfl_xor(local_max, off));
+  if (lane == 0) red[wid] = local_max;
   __syncthreads();
-  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
-    __syncthreads();
-  }
-  const float m = __fdiv_rn(127.0f, fmaxf(SqrtFltEps(), red[0]));
+  local_max = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float m = __fdiv_rn(127.0f, fmaxf(SqrtFltEps(), local_max));
   const int tot = p.padded_blocks * 16;
-  for (int e = threadIdx.x; e < tot; e += blockDim.x) {
-    int8_t v8 = 0;
-    if (e < nent) {
-      const float r = roundf(__fmul_rn(raw[e], m));
-      v8 = int8_t(int(r));
-      if (p.lut_u8) p.lut_u8[size_t(qi) * nent + e] = uint8_t(int(r) + 128);
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int e = t + 256 * u;
+    if (e < tot) {
+      int8_t v8 = 0;
+      if (e < nent) {
+        const float r = roundf(__fmul_rn(raw[u], m));
+        v8 = int8_t(int(r));
+        if (p.lut_u8) p.lut_u8[size_t(qi) * nent + e] = uint8_t(int(r) + 128);
+      }
+      p.lut[size_t(qi) * tot + e] = v8;
     }
-    p.lut[size_t(qi) * tot + e] = v8;
   }
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     p.mult[qi] = m;
     p.inv[qi] = p.residual ? float(1.0 / double(m)) : __fdiv_rn(1.0f, m);
   }
@@ -364,7 +420,7 @@ __device__ void TopLFinish(int qi, int L, uint32_t m, const uint64_t* sel, int32
     const int32_t leaf = has ? int32_t(sel[i] & 0xFFFFFFFFu) : -1;
     out_leaf[size_t(qi) * L + i] = leaf;
     out_dist[size_t(qi) * L + i] = has ? FromOrdered(uint32_t(sel[i] >> 32)) : __int_as_float(0x7fc00000);
-    if (tail.leaf_count && has) tail.rank[size_t(qi) * L + i] = atomicAdd(&tail.leaf_count[leaf], 1u);
+    if (tail.leaf_count && has) tail.rank[size_t(qi) * L + i] = atomicAdd(&tail.leaf_count[size_t(leaf) * kCounterStride], 1u);
   }
   if (tail.lut.lut) {
     __syncthreads();
@@ -372,106 +428,58 @@ __device__ void TopLFinish(int qi, int L, uint32_t m, const uint64_t* sel, int32
   }
 }
 
-// The LUT of query qi by ONE wave (lanes 0..63; no workgroup barrier), the
-// same arithmetic as BuildLut.
-__device__ void BuildLutWave(int qi, const LutParams& p) {
-  const int lane = threadIdx.x & 63;
-  const float* q = p.queries + size_t(qi) * p.dim;
-  const int nb = p.nb, dpb = p.dpb;
-  const int nent = nb * 16;
-  const int last = p.dim - dpb * (nb - 1);
-  constexpr int kPer = (kMaxBlocks * 16) / 64;   // entries per lane
-  float raw[kPer];
-  float local_max = 0.0f;
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int e = lane + 64 * u;
-    float v = 0.0f;
-    if (e < nent) {
-      const int b = e >> 4, c = e & 15;
-      const int nd = (b == nb - 1) ? last : dpb;
-      const float* qb = q + size_t(b) * dpb;
-      const float* cb = p.codebook + (size_t(b) * 16 + c) * dpb;
-      if (p.metric == 0) {
-        float s = __fmul_rn(qb[0], cb[0]);
-        for (int i = 1; i < nd; ++i) s = __fadd_rn(s, __fmul_rn(qb[i], cb[i]));
-        v = -s;
-      } else {
-        float t = __fsub_rn(qb[0], cb[0]);
-        float s = __fmul_rn(t, t);
-        for (int i = 1; i < nd; ++i) {
-          const float w = __fsub_rn(qb[i], cb[i]);
-          s = __fadd_rn(s, __fmul_rn(w, w));
-        }
-        v = s;
-      }
-    }
-    raw[u] = v;
-    local_max = fmaxf(local_max, fabsf(v));
-  }
-  for (int off = 32; off > 0; off >>= 1) local_max = fmaxf(local_max, __shfl_xor(local_max, off));
-  const float m = __fdiv_rn(127.0f, fmaxf(SqrtFltEps(), local_max));
-  const int tot = p.padded_blocks * 16;
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int e = lane + 64 * u;
-    if (e < tot) {
-      int8_t v8 = 0;
-      if (e < nent) {
-        const float r = roundf(__fmul_rn(raw[u], m));
-        v8 = int8_t(int(r));
-        if (p.lut_u8) p.lut_u8[size_t(qi) * nent + e] = uint8_t(int(r) + 128);
-      }
-      p.lut[size_t(qi) * tot + e] = v8;
-    }
-  }
-  if (lane == 0) {
-    p.mult[qi] = m;
-    p.inv[qi] = p.residual ? float(1.0 / double(m)) : __fdiv_rn(1.0f, m);
-  }
-}
+// Exact top-L by (score, center index) with one 256-thread block per query,
+// the row in registers (VPT scores per thread, nl <= 256 * VPT; a block per
+// query, not a wave: 1000 queries must fill 1024 SIMDs several waves deep).
+// Linear 256-bin histograms of the ordered score bits between the row's
+// current [lo, hi] (radix digits of nearby floats would all hit one bin)
+// narrow down to the bin holding the L-th score until at most 256 keys are
+// left; every key below that bin and the keys inside it are compacted in LDS
+// and ordered by a counting rank over (score, leaf) (keys are unique), of
+// which the first L are kept.  Then the pairs' ranks in their leaves' lists
+// and the query's LUT (the front end's tail, as TopLFinish).
+constexpr int kWaveTopL = 256;         // L limit of the register top-L kernel
+constexpr int kBlockTopCand = 1024;    // compacted keys one block orders
+constexpr uint32_t kTopNarrow = 256;   // histogram rounds until this many keys
 
-// Exact top-L by (score, center index) with ONE wave per query (4 queries
-// per 256-thread block, no workgroup barriers), the row in registers (VPL
-// scores per lane, nl <= 64 * VPL).  Linear 256-bin histograms of the
-// ordered score bits between the row's current [lo, hi] (radix digits of
-// nearby floats would all hit one bin) narrow down to the bin holding the
-// L-th score; every key below that bin and the keys inside it are compacted
-// in LDS (ballot prefix) and ordered by a counting rank over (score, leaf)
-// (keys are unique), of which the first L are kept.  Then the pairs' ranks
-// in their leaves' lists and the query's LUT (the front end's tail, as
-// TopLFinish).
-constexpr int kWaveTopL = 256;   // L limit of the wave kernel
-constexpr int kWaveTopCand = 512;   // compacted keys one wave can order
-
-template <int VPL>
-__global__ void __launch_bounds__(256) topl_wave_kernel(const float* __restrict__ scores, int nq,
-                                                        int nl, int L, int32_t* __restrict__ out_leaf,
-                                                        float* __restrict__ out_dist, TopLTail tail) {
-  __shared__ uint32_t hist[4][256];
-  __shared__ uint64_t sel[4][kWaveTopCand];
-  __shared__ uint64_t srt[4][kWaveTopL];
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int qi = blockIdx.x * 4 + wv;
-  if (qi >= nq) return;
+template <int VPT>
+__global__ void __launch_bounds__(256) topl_block_kernel(const float* __restrict__ scores, int nl,
+                                                         int L, int32_t* __restrict__ out_leaf,
+                                                         float* __restrict__ out_dist, TopLTail tail) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint64_t sel[kBlockTopCand];
+  __shared__ uint64_t srt[kWaveTopL];
+  __shared__ uint32_t wsum[4], s_lo[4], s_hi[4], s_wave[4], s_bin, s_cum, s_hb, s_cnt, s_cnt2;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int qi = blockIdx.x;
+  SMX_PHASE(0, qi, 0);
   const float* row = scores + size_t(qi) * nl;
-  uint32_t* hs = hist[wv];
+  const uint64_t lanes_below = (1ull << lane) - 1ull;
+  // every load issued before the first use (clamped index, no guarded load)
+  float f[VPT];
+#pragma unroll
+  for (int u = 0; u < VPT; ++u) f[u] = row[min(tid + 256 * u, nl - 1)];
   // per score: its ordered bits and its state: 0 = taken (below the
   // boundary bin), 1 = boundary candidate, 2 = out
-  uint32_t v[VPL];
-  uint8_t st[VPL];
+  uint32_t v[VPT];
+  uint8_t st[VPT];
 #pragma unroll
-  for (int u = 0; u < VPL; ++u) {
-    const int cix = lane + 64 * u;
-    v[u] = cix < nl ? OrderedBits(row[cix]) : 0xFFFFFFFFu;
+  for (int u = 0; u < VPT; ++u) {
+    const int cix = tid + 256 * u;
+    v[u] = cix < nl ? OrderedBits(f[u]) : 0xFFFFFFFFu;
     st[u] = cix < nl ? 1 : 2;
   }
+  if (tid == 0) { s_cnt = 0; s_cnt2 = 0; }
+  __syncthreads();   // the counters are zero before any wave's compaction
+  SMX_PHASE(0, qi, 1);
   const uint32_t m = min(uint32_t(L), uint32_t(nl));
   uint32_t below = 0, incnt = uint32_t(nl);
-  for (int round = 0; round < 6 && below + incnt > uint32_t(kWaveTopCand); ++round) {
-    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+  uint32_t lo = 0, hi = 0;
+  for (int round = 0; round < 8 && m > 0 && below + incnt > kTopNarrow; ++round) {
+    lo = 0xFFFFFFFFu;
+    hi = 0;
 #pragma unroll
-    for (int u = 0; u < VPL; ++u)
+    for (int u = 0; u < VPT; ++u)
       if (st[u] == 1) {
         lo = min(lo, v[u]);
         hi = max(hi, v[u]);
@@ -480,122 +488,105 @@ __global__ void __launch_bounds__(256) topl_wave_kernel(const float* __restrict_
       lo = min(lo, uint32_t(__shfl_xor(int(lo), off)));
       hi = max(hi, uint32_t(__shfl_xor(int(hi), off)));
     }
-    if (lo == hi) break;   // one value left in the boundary set
+    if (lane == 0) { s_lo[wid] = lo; s_hi[wid] = hi; }
+    hist[tid] = 0;
+    __syncthreads();
+    lo = min(min(s_lo[0], s_lo[1]), min(s_lo[2], s_lo[3]));
+    hi = max(max(s_hi[0], s_hi[1]), max(s_hi[2], s_hi[3]));
+    if (lo == hi) break;   // block-uniform: one value left in the boundary set
     // bin = floor((v - lo) * scale / 2^32), scale = floor(255.99 * 2^32 / span):
     // monotone in v, 0 at lo, <= 255 at hi (no division per value)
     const uint64_t scale = ((uint64_t(255) << 32) + 0xFFFFFFFFull) / (uint64_t(hi - lo));
 #pragma unroll
-    for (int u = 0; u < 4; ++u) hs[lane + 64 * u] = 0;
-    WaveLdsSync();
-#pragma unroll
-    for (int u = 0; u < VPL; ++u)
-      if (st[u] == 1) atomicAdd(&hs[uint32_t((uint64_t(v[u] - lo) * scale) >> 32)], 1u);
-    WaveLdsSync();
-    const uint32_t h0 = hs[4 * lane], h1 = hs[4 * lane + 1], h2 = hs[4 * lane + 2],
-                   h3 = hs[4 * lane + 3];
-    uint32_t incl = h0 + h1 + h2 + h3;
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t t = __shfl_up(incl, off);
-      if (lane >= off) incl += t;
-    }
-    const uint32_t excl = incl - (h0 + h1 + h2 + h3);
+    for (int u = 0; u < VPT; ++u)
+      if (st[u] == 1) atomicAdd(&hist[uint32_t((uint64_t(v[u] - lo) * scale) >> 32)], 1u);
+    __syncthreads();
+    const uint32_t hv = hist[tid];
+    const uint32_t inc = BlockInclusiveScan256(hv, wsum);
     const uint32_t need = m - below;
-    const bool mine = excl < need && incl >= need;
-    uint32_t bsel = 0, cum = excl, hb = 0;
-    if (mine) {
-      const uint32_t hv[4] = {h0, h1, h2, h3};
-      int u = 0;
-      while (cum + hv[u] < need) { cum += hv[u]; ++u; }
-      bsel = 4 * lane + u;
-      hb = hv[u];
-    }
-    const int src = __ffsll((unsigned long long)__ballot(mine)) - 1;
-    bsel = __shfl(bsel, src);
-    cum = __shfl(cum, src);
-    hb = __shfl(hb, src);
+    if (inc - hv < need && inc >= need) { s_bin = uint32_t(tid); s_cum = inc - hv; s_hb = hv; }
+    __syncthreads();
+    const uint32_t bsel = s_bin;
+    below += s_cum;
+    incnt = s_hb;
 #pragma unroll
-    for (int u = 0; u < VPL; ++u)
+    for (int u = 0; u < VPT; ++u)
       if (st[u] == 1) {
         const uint32_t bn = uint32_t((uint64_t(v[u] - lo) * scale) >> 32);
         st[u] = bn < bsel ? 0 : bn > bsel ? 2 : 1;
       }
-    below += cum;
-    incnt = hb;
-    WaveLdsSync();
+    __syncthreads();   // hist, wsum, s_lo and s_bin are rewritten by the next round
   }
-  // the taken keys and the boundary candidates, in LDS
-  uint32_t cnt = 0;
+  SMX_PHASE(0, qi, 2);
+  // the taken keys and the boundary candidates, in LDS (one LDS atomic per wave)
 #pragma unroll
-  for (int u = 0; u < VPL; ++u) {
+  for (int u = 0; u < VPT; ++u) {
     const bool in = st[u] <= 1;
     const uint64_t bal = __ballot(in);
+    uint32_t base = 0;
+    if (lane == 0 && bal) base = atomicAdd(&s_cnt, uint32_t(__popcll(bal)));
+    base = uint32_t(__shfl(int(base), 0));
     if (in) {
-      const uint32_t pos = cnt + uint32_t(__popcll(bal & ((1ull << lane) - 1ull)));
-      if (pos < uint32_t(kWaveTopCand)) sel[wv][pos] = (uint64_t(v[u]) << 32) | uint32_t(lane + 64 * u);
+      const uint32_t pos = base + uint32_t(__popcll(bal & lanes_below));
+      if (pos < uint32_t(kBlockTopCand)) sel[pos] = (uint64_t(v[u]) << 32) | uint32_t(tid + 256 * u);
     }
-    cnt += uint32_t(__popcll(bal));
   }
-  WaveLdsSync();
-  if (cnt <= uint32_t(kWaveTopCand)) {
+  __syncthreads();
+  const uint32_t cnt = s_cnt;
+  if (cnt <= uint32_t(kBlockTopCand)) {
     // counting rank over (score, leaf), keys unique; keep the first m
-    const uint64_t* sk = sel[wv];
-    for (uint32_t i = lane; i < cnt; i += 64) {
-      const uint64_t key = sk[i];
-      uint32_t r = 0;
-      uint32_t j = 0;
-#pragma unroll 8
-      for (; j + 1 < cnt; j += 2) {
-        const uint64_t k0 = sk[j], k1 = sk[j + 1];
-        r += (k0 < key ? 1u : 0u) + (k1 < key ? 1u : 0u);
-      }
-      if (j < cnt) r += sk[j] < key ? 1u : 0u;
-      if (r < m) srt[wv][r] = key;
+    for (uint32_t i = tid; i < cnt; i += 256) {
+      const uint64_t key = sel[i];
+      const uint32_t r = CountLess(sel, cnt, key);
+      if (r < m) srt[r] = key;
     }
   } else {
-    // more than kWaveTopCand keys on one boundary value (all-equal rows):
-    // the keys below it by rank, then the lowest-index ties in index order
-    uint32_t T = 0;
+    // more than kBlockTopCand keys on one boundary value (lo == hi, e.g. an
+    // all-equal row): the keys below it by rank, then the lowest-index ties
+    // in index order (index c = tid + 256 u: u-major, then thread order)
+    const uint32_t T = lo;
+    __syncthreads();   // every thread has read s_cnt; sel is rewritten
 #pragma unroll
-    for (int u = 0; u < VPL; ++u)
-      if (st[u] == 1) T = v[u];
-    for (int off = 32; off > 0; off >>= 1) T = max(T, uint32_t(__shfl_xor(int(T), off)));
-    uint32_t c2 = 0;
-#pragma unroll
-    for (int u = 0; u < VPL; ++u) {
+    for (int u = 0; u < VPT; ++u) {
       const bool in = st[u] == 0;
       const uint64_t bal = __ballot(in);
-      if (in) sel[wv][c2 + uint32_t(__popcll(bal & ((1ull << lane) - 1ull)))] =
-          (uint64_t(v[u]) << 32) | uint32_t(lane + 64 * u);
-      c2 += uint32_t(__popcll(bal));
+      uint32_t base = 0;
+      if (lane == 0 && bal) base = atomicAdd(&s_cnt2, uint32_t(__popcll(bal)));
+      base = uint32_t(__shfl(int(base), 0));
+      if (in) sel[base + uint32_t(__popcll(bal & lanes_below))] = (uint64_t(v[u]) << 32) | uint32_t(tid + 256 * u);
     }
-    WaveLdsSync();
-    for (uint32_t i = lane; i < c2; i += 64) {
-      const uint64_t key = sel[wv][i];
-      uint32_t r = 0;
-      for (uint32_t j = 0; j < c2; ++j) r += sel[wv][j] < key ? 1u : 0u;
-      srt[wv][r] = key;
+    __syncthreads();
+    const uint32_t c2 = s_cnt2;   // == below < m
+    for (uint32_t i = tid; i < c2; i += 256) {
+      const uint64_t key = sel[i];
+      srt[CountLess(sel, c2, key)] = key;
     }
-    uint32_t t = 0;
+    uint32_t ties = 0;
 #pragma unroll
-    for (int u = 0; u < VPL; ++u) {
+    for (int u = 0; u < VPT; ++u) {
       const bool te = st[u] == 1;
       const uint64_t bal = __ballot(te);
-      if (te) {
-        const uint32_t pos = c2 + t + uint32_t(__popcll(bal & ((1ull << lane) - 1ull)));
-        if (pos < m) srt[wv][pos] = (uint64_t(T) << 32) | uint32_t(lane + 64 * u);
-      }
-      t += uint32_t(__popcll(bal));
+      if (lane == 0) s_wave[wid] = uint32_t(__popcll(bal));
+      __syncthreads();
+      uint32_t before = ties + uint32_t(__popcll(bal & lanes_below));
+      for (int w = 0; w < wid; ++w) before += s_wave[w];
+      if (te && c2 + before < m) srt[c2 + before] = (uint64_t(T) << 32) | uint32_t(tid + 256 * u);
+      ties += s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+      __syncthreads();   // s_wave is rewritten by the next u
     }
   }
-  WaveLdsSync();
-  for (int i = lane; i < L; i += 64) {
+  __syncthreads();
+  SMX_PHASE(0, qi, 3);
+  for (int i = tid; i < L; i += 256) {
     const bool has = uint32_t(i) < m;
-    const int32_t leaf = has ? int32_t(srt[wv][i] & 0xFFFFFFFFu) : -1;
+    const int32_t leaf = has ? int32_t(srt[i] & 0xFFFFFFFFu) : -1;
     out_leaf[size_t(qi) * L + i] = leaf;
-    out_dist[size_t(qi) * L + i] = has ? FromOrdered(uint32_t(srt[wv][i] >> 32)) : __int_as_float(0x7fc00000);
-    if (tail.leaf_count && has) tail.rank[size_t(qi) * L + i] = atomicAdd(&tail.leaf_count[leaf], 1u);
+    out_dist[size_t(qi) * L + i] = has ? FromOrdered(uint32_t(srt[i] >> 32)) : __int_as_float(0x7fc00000);
+    if (tail.leaf_count && has) tail.rank[size_t(qi) * L + i] = atomicAdd(&tail.leaf_count[size_t(leaf) * kCounterStride], 1u);
   }
-  if (tail.lut.lut) BuildLutWave(qi, tail.lut);
+  SMX_PHASE(0, qi, 4);
+  if (tail.lut.lut) BuildLut(qi, tail.lut);
+  SMX_PHASE(0, qi, 5);
 }
 
 __global__ void __launch_bounds__(256) topl_select_kernel(const float* __restrict__ scores, int nl,
@@ -767,7 +758,7 @@ __global__ void __launch_bounds__(1024) worklist_kernel(
   unsigned long long sb = 0;
   for (int p = beg; p < end; ++p) {
     const uint32_t leaf = order[p];
-    const uint32_t c = cnt[leaf], n = leaf_size[leaf];
+    const uint32_t c = cnt[size_t(leaf) * kCounterStride], n = leaf_size[leaf];
     uint32_t items;
     sw += LeafUnits(c, n, chunk_tiles, items);
     st += items;
@@ -817,7 +808,7 @@ __global__ void __launch_bounds__(1024) worklist_kernel(
     const int pp = beg - 1;
     const uint32_t leaf = order[pp];
     uint32_t items;
-    prev = group_of(rw - LeafUnits(cnt[leaf], leaf_size[leaf], chunk_tiles, items));
+    prev = group_of(rw - LeafUnits(cnt[size_t(leaf) * kCounterStride], leaf_size[leaf], chunk_tiles, items));
   }
   for (int p = beg; p < end; ++p) {
     const uint32_t leaf = order[p];
@@ -827,7 +818,7 @@ __global__ void __launch_bounds__(1024) worklist_kernel(
     leaf_item0[leaf] = rt;
     pos_unit0[p] = rw;
     uint32_t items;
-    rw += LeafUnits(cnt[leaf], leaf_size[leaf], chunk_tiles, items);
+    rw += LeafUnits(cnt[size_t(leaf) * kCounterStride], leaf_size[leaf], chunk_tiles, items);
     rt += items;
   }
   if (beg < end && end == nl) {
@@ -861,7 +852,7 @@ __global__ void __launch_bounds__(64) items_kernel(
     ItemLane* __restrict__ lanes, uint4* __restrict__ wave_start) {
   const int p = blockIdx.x, lane = threadIdx.x;
   const uint32_t leaf = order[p];
-  const uint32_t c = cnt[leaf], n = leaf_size[leaf];
+  const uint32_t c = cnt[size_t(leaf) * kCounterStride], n = leaf_size[leaf];
   const uint32_t chunks = LeafChunks(n, chunk_tiles);
   const uint32_t qt = (c + kQueriesPerTile - 1) / kQueriesPerTile;
   const uint32_t item0 = leaf_item0[leaf];
@@ -1006,27 +997,14 @@ constexpr int kSeedPerThread = 32;
 constexpr uint32_t kSeedCap = 256u * kSeedPerThread;
 constexpr int kSeedMaxLeaves = 64;   // one wave of leaf slots
 
-// Inclusive block scan of one value per thread (256 threads).
-__device__ __forceinline__ uint32_t BlockInclusiveScan256(uint32_t v, uint32_t* wsum) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t t = uint32_t(__shfl_up(int(v), off));
-    if (lane >= off) v += t;
-  }
-  if (lane == 63) wsum[wid] = v;
-  __syncthreads();
-  for (int w = 0; w < wid; ++w) v += wsum[w];
-  return v;
-}
-
 // The threshold key of query qi from its seed leaves, or kNoThreshold (no
 // bound); block-wide (256 threads, all call; the value is returned to all).
 template <int K>
 __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
   constexpr int W = 4 * NW;
-  constexpr int U = 4;   // datapoints whose code loads are in flight together
-  __shared__ int8_t lut[2 * K * 16];
+  constexpr int U = 8;   // datapoints whose code loads are in flight together
+  __shared__ __align__(16) int8_t lut[2 * K * 16];
   __shared__ uint32_t hist[256];
   __shared__ uint32_t s_start[kSeedMaxLeaves + 1];
   __shared__ uint64_t s_tile0[kSeedMaxLeaves];
@@ -1034,8 +1012,12 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
   __shared__ uint32_t wsum[4], s_lo[4], s_hi[4], s_bin, s_below;
   __shared__ uint64_t s_T;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  SMX_PHASE(1, qi, 0);
   if (a.seed <= 0) return kNoThreshold;
-  for (int e = tid; e < 2 * K * 16; e += 256) lut[e] = a.lut[size_t(qi) * 2 * K * 16 + e];
+  static_assert(2 * K * 16 / 4 <= 256, "one LUT word per thread");
+  if (tid < 2 * K * 16 / 4)
+    reinterpret_cast<uint32_t*>(lut)[tid] =
+        reinterpret_cast<const uint32_t*>(a.lut + size_t(qi) * 2 * K * 16)[tid];
   const float inv = a.inv[qi];
   const int nseed = min(a.seed, min(a.L, kSeedMaxLeaves));
   if (wid == 0) {
@@ -1053,6 +1035,7 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
     if (lane == 63) s_start[kSeedMaxLeaves] = inc;
   }
   __syncthreads();
+  SMX_PHASE(1, qi, 1);
   const uint32_t total = min(s_start[kSeedMaxLeaves], kSeedCap);
   const uint32_t kk = uint32_t(a.kk);
   if (kk == 0 || total < kk) return kNoThreshold;   // no bound: the threshold stays open
@@ -1091,6 +1074,7 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
       for (int u = 0; u < U; ++u) vals[i0 + u] = 0xFFFFFFFFu;   // no datapoint
     }
   }
+  SMX_PHASE(1, qi, 2);
   // range of the values, then histogram rounds down to the kk-th value
   uint32_t lo = 0xFFFFFFFFu, hi = 0;
 #pragma unroll
@@ -1108,14 +1092,16 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
   lo = min(min(s_lo[0], s_lo[1]), min(s_lo[2], s_lo[3]));
   hi = max(max(s_hi[0], s_hi[1]), max(s_hi[2], s_hi[3]));
   uint32_t below = 0;   // values smaller than lo
-  while (lo < hi) {     // block-uniform; each round shrinks [lo, hi] 256-fold
-    const uint64_t span = uint64_t(hi - lo) + 1;
+  while (lo < hi) {     // block-uniform; each round shrinks [lo, hi] ~256-fold
+    // bin = floor((v - lo) * scale / 2^32), scale = floor(255.99 * 2^32 / span):
+    // monotone, 0 at lo, <= 255 at hi, no division per value
+    const uint64_t scale = ((uint64_t(255) << 32) + 0xFFFFFFFFull) / uint64_t(hi - lo);
     hist[tid] = 0;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kSeedPerThread; ++i) {
       const uint32_t v = vals[i];
-      if (v >= lo && v <= hi) atomicAdd(&hist[uint32_t((uint64_t(v - lo) * 256u) / span)], 1u);
+      if (v >= lo && v <= hi) atomicAdd(&hist[uint32_t((uint64_t(v - lo) * scale) >> 32)], 1u);
     }
     __syncthreads();
     const uint32_t hv = hist[tid];
@@ -1127,15 +1113,16 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
     __syncthreads();
     const uint32_t b = s_bin;
     below = s_below;
-    // values of bin b: [lo + ceil(b*span/256), lo + ceil((b+1)*span/256) - 1]
-    const uint32_t blo = lo + uint32_t((uint64_t(b) * span + 255u) / 256u);
-    const uint32_t bhi = lo + uint32_t((uint64_t(b + 1) * span + 255u) / 256u) - 1u;
+    // values of bin b: v - lo in [ceil(b 2^32 / scale), ceil((b+1) 2^32 / scale) - 1]
+    const uint32_t blo = lo + uint32_t(((uint64_t(b) << 32) + scale - 1) / scale);
+    const uint32_t bhi = lo + uint32_t(((uint64_t(b + 1) << 32) + scale - 1) / scale) - 1u;
     lo = blo;
-    hi = bhi;
+    hi = min(bhi, hi);
     __syncthreads();   // hist, wsum and s_bin are rewritten by the next round
   }
   if (tid == 0) s_T = (uint64_t(hi) << 32) | 0xFFFFFFFFull;
   __syncthreads();
+  SMX_PHASE(1, qi, 3);
   return s_T;
 }
 
@@ -1167,6 +1154,7 @@ __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
     const uint32_t w0 = a.leaf_item0[leaf] + (r / kQueriesPerTile) * chunks;
     for (uint32_t ch = 0; ch < chunks; ++ch) a.lanes[size_t(w0 + ch) * kQueriesPerTile + (r % kQueriesPerTile)] = v;
   }
+  SMX_PHASE(1, qi, 4);
 }
 
 
@@ -1411,7 +1399,7 @@ __global__ void __launch_bounds__(64, (K <= 25 ? SMX_SCAN_WAVES_PER_SIMD : 2))
                 kslot[par][p] = uint8_t(cc);
                 atomicAdd(&qcnt[cc], 1u);
               } else {  // item buffer full (rare): straight to the global list
-                const uint32_t gs = atomicAdd(&a.cand_count[qq], 1u);
+                const uint32_t gs = atomicAdd(&a.cand_count[size_t(qq) * kCounterStride], 1u);
                 if (gs < a.cap) a.cand[size_t(qq) * a.cap + gs] = key;
               }
             }
@@ -1501,7 +1489,7 @@ __global__ void __launch_bounds__(64, (K <= 25 ? SMX_SCAN_WAVES_PER_SIMD : 2))
     // it at the next item's start (after that item's loads are issued)
     if (lane < Q) {
       const uint32_t m = qcnt[lane];
-      slot = m ? atomicAdd(&a.cand_count[cl.qid], m) : 0u;
+      slot = m ? atomicAdd(&a.cand_count[size_t(cl.qid) * kCounterStride], m) : 0u;
       prev_qid[lane] = cl.qid;
     }
     pending = true;
@@ -1569,7 +1557,7 @@ __global__ void __launch_bounds__(256) tighten_kernel(const uint64_t* __restrict
                                                       uint64_t* __restrict__ tau_key) {
   extern __shared__ uint64_t keys[];
   const int qi = blockIdx.x;
-  if (cand_count[qi] <= cap || kk <= 0) return;
+  if (cand_count[size_t(qi) * kCounterStride] <= cap || kk <= 0) return;
   const uint32_t np2 = NextPow2(cap);
   for (uint32_t i = threadIdx.x; i < np2; i += blockDim.x)
     keys[i] = i < cap ? cand[size_t(qi) * cap + i] : ~0ull;
@@ -1621,7 +1609,7 @@ __device__ float ExactDistance(const float* __restrict__ q, const float* __restr
 __global__ void __launch_bounds__(256) final_select_kernel(SelectArgs a) {
   extern __shared__ uint64_t lds[];
   const int qi = a.qlist ? int(a.qlist[blockIdx.x]) : int(blockIdx.x);
-  const uint32_t raw_n = a.cand_count[qi];
+  const uint32_t raw_n = a.cand_count[size_t(qi) * kCounterStride];
   if (threadIdx.x == 0 && raw_n > a.cap && !a.qlist) {   // overflow: the host tightens and rescans
     a.overflow[0] = 1u;
     atomicMax(&a.overflow[1], raw_n);
@@ -1769,6 +1757,9 @@ constexpr int kFsBins = 256;
 // lanes per candidate: lane l of a group owns accumulator l of the A.8 layout
 // (dims l, l+8, ...) and the folds follow ExactDistance exactly.  256
 // threads; ends with a barrier.
+constexpr int kXMax = 16;   // dims per lane held in registers (dim <= 128)
+constexpr int kXPass = 2;   // 32-candidate passes whose rows are in flight together
+
 __device__ void ExactDistances8(const SelectArgs& a, const float* rows, const uint32_t* rowid,
                                 uint32_t m, float* dist, int qi) {
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1781,28 +1772,76 @@ __device__ void ExactDistances8(const SelectArgs& a, const float* rows, const ui
     const float t = __fsub_rn(x, y);
     return __fmaf_rn(t, t, acc);
   };
-  for (uint32_t base = 0; base < m; base += 32) {
-    const uint32_t i = base + uint32_t(tid >> 3);
-    const bool act = i < m;
-    const float* x = rows + size_t(rowid[act ? i : 0]) * dim;
-    float acc = 0.0f;
-    for (int j = 0; j < j8; j += 8) acc = term(acc, q[j + l], x[j + l]);
+  // the tails of ExactDistance: 4-wide at j8 (lanes 0..3), 2-wide at j2
+  // (lanes 2, 3), scalar at j1
+  int j = j8;
+  const bool has4 = j + 4 <= dim;
+  if (has4) j += 4;
+  const int j2 = j;
+  const bool has2 = j + 2 <= dim;
+  if (has2) j += 2;
+  const int j1 = j;
+  const bool has1 = j < dim;
+  // folds of one candidate's 8 accumulators (lane l holds accumulator l)
+  auto finish = [&](float acc, float q4, float x4, float q2, float x2, float q1, float x1) {
     const float hi4 = __shfl(acc, gb + ((l + 4) & 7));
     float sv = __fadd_rn(hi4, acc);   // lanes l < 4: s[l]
-    int j = j8;
-    if (j + 4 <= dim) {
-      if (l < 4) sv = term(sv, q[j + l], x[j + l]);
-      j += 4;
-    }
-    if (j + 2 <= dim) {
-      if (l == 2 || l == 3) sv = term(sv, q[j + l - 2], x[j + l - 2]);
-      j += 2;
-    }
+    if (has4 && l < 4) sv = term(sv, q4, x4);
+    if (has2 && (l == 2 || l == 3)) sv = term(sv, q2, x2);
     const float s1 = __shfl(sv, gb + 1), s2 = __shfl(sv, gb + 2), s3 = __shfl(sv, gb + 3);
     float r = __fadd_rn(__fadd_rn(sv, s2), __fadd_rn(s1, s3));
-    if (j < dim) r = term(r, q[j], x[j]);
-    __syncthreads();   // every read of rowid/dist for this pass is done
-    if (l == 0 && act) dist[i] = r;
+    if (has1) r = term(r, q1, x1);
+    return r;
+  };
+  const int c4 = min(j8 + (l & 3), dim - 1), c2 = min(j2 + (l & 1), dim - 1), c1 = min(j1, dim - 1);
+  if (dim <= 8 * kXMax) {
+    // every load of kXPass passes is issued before the first use (clamped
+    // indices; the accumulation below stops at j8)
+    float qv[kXMax];
+#pragma unroll
+    for (int k = 0; k < kXMax; ++k) qv[k] = q[min(l + 8 * k, dim - 1)];
+    const float q4 = q[c4], q2 = q[c2], q1 = q[c1];
+    const int nj = j8 >> 3;
+    for (uint32_t base = 0; base < m; base += 32 * kXPass) {
+      float xv[kXPass][kXMax], x4[kXPass], x2[kXPass], x1[kXPass];
+#pragma unroll
+      for (int p = 0; p < kXPass; ++p) {
+        const uint32_t i = min(base + 32 * p + uint32_t(tid >> 3), m - 1);
+        const float* x = rows + size_t(rowid[i]) * dim;
+#pragma unroll
+        for (int k = 0; k < kXMax; ++k) xv[p][k] = x[min(l + 8 * k, dim - 1)];
+        x4[p] = x[c4];
+        x2[p] = x[c2];
+        x1[p] = x[c1];
+      }
+      float r[kXPass];
+#pragma unroll
+      for (int p = 0; p < kXPass; ++p) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kXMax; ++k)
+          if (k < nj) acc = term(acc, qv[k], xv[p][k]);
+        r[p] = finish(acc, q4, x4[p], q2, x2[p], q1, x1[p]);
+      }
+      __syncthreads();   // every read of rowid/dist for these passes is done
+#pragma unroll
+      for (int p = 0; p < kXPass; ++p) {
+        const uint32_t i = base + 32 * p + uint32_t(tid >> 3);
+        if (l == 0 && i < m) dist[i] = r[p];
+      }
+    }
+  } else {
+    for (uint32_t base = 0; base < m; base += 32) {
+      const uint32_t i = base + uint32_t(tid >> 3);
+      const bool act = i < m;
+      const float* x = rows + size_t(rowid[act ? i : 0]) * dim;
+      float acc = 0.0f;
+#pragma unroll 8
+      for (int jj = 0; jj < j8; jj += 8) acc = term(acc, q[jj + l], x[jj + l]);
+      const float r = finish(acc, q[c4], x[c4], q[c2], x[c2], q[c1], x[c1]);
+      __syncthreads();   // every read of rowid/dist for this pass is done
+      if (l == 0 && act) dist[i] = r;
+    }
   }
   __syncthreads();
 }
@@ -1814,7 +1853,8 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
   __shared__ uint32_t s_lo[4], s_hi[4], s_b, s_cle, s_cbef, s_c;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int qi = blockIdx.x;
-  const uint32_t raw_n = a.cand_count[qi];
+  SMX_PHASE(2, qi, 0);
+  const uint32_t raw_n = a.cand_count[size_t(qi) * kCounterStride];
   if (threadIdx.x == 0 && raw_n > a.cap && !a.qlist) {   // overflow: the host tightens and rescans
     a.overflow[0] = 1u;
     atomicMax(&a.overflow[1], raw_n);
@@ -1885,6 +1925,7 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
     }
     __syncthreads();
   }
+  SMX_PHASE(2, qi, 1);
   const uint32_t c = n <= uint32_t(kSelMax) ? n : s_c;
   // counting rank: keys are unique, so rank = number of smaller keys
   if (uint32_t(tid) < c) {
@@ -1894,6 +1935,7 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
     out[r] = key;
   }
   __syncthreads();
+  SMX_PHASE(2, qi, 2);
   uint32_t m = min(c, k);
   // exact-reorder rows: dataset[global id], or in a shard with its own rows,
   // member_rows[member slot]
@@ -1917,6 +1959,7 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
     dist[tid] = FromOrdered(uint32_t(key >> 32));
   }
   __syncthreads();
+  SMX_PHASE(2, qi, 3);
   if (a.shard_out) {
     // local top-k' with exact distances of this shard's rows; de-duplication
     // and the final order happen in the merge
@@ -1970,7 +2013,9 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
     __syncthreads();
     m = min(s_c, uint32_t(a.pre_nn));
   }
+  SMX_PHASE(2, qi, 4);
   if (a.reorder && !a.pre_only) ExactDistances8(a, rows, rowid, m, dist, qi);
+  SMX_PHASE(2, qi, 5);
   // final (distance, global id) rank; keep the output width
   const uint32_t keep = min(m, uint32_t(a.out_width));
   uint64_t fkey = 0;
@@ -1992,6 +2037,7 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
     a.out_dist[size_t(qi) * a.out_width + i] = __int_as_float(0x7fc00000);
   }
   if (tid == 0 && a.out_count) a.out_count[qi] = int32_t(keep);
+  SMX_PHASE(2, qi, 6);
 }
 
 // ---------------------------------------------------------------------------
@@ -2127,7 +2173,7 @@ __global__ void __launch_bounds__(1024) cand_stats_kernel(const uint32_t* __rest
   __shared__ uint32_t s_over[16], s_max[16], s_sum[16];
   uint32_t over = 0, mx = 0, sum = 0;
   for (int i = threadIdx.x; i < nq; i += blockDim.x) {
-    const uint32_t v = cand_count[i];
+    const uint32_t v = cand_count[size_t(i) * kCounterStride];
     if (v > cap) over = max(over, v);
     mx = max(mx, v);
     sum += v;
@@ -2198,12 +2244,12 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   // static LDS of the kernel besides the dynamic key buffers: the LUT build's
   // raw table and reduction (~5 KB) and the selection's words
   constexpr size_t kStaticLds = 6 * 1024;
-  if (L <= kWaveTopL && ix.nl <= 64 * 16) {
-    hipLaunchKernelGGL(topl_wave_kernel<16>, dim3((nq + 3) / 4), dim3(256), 0, s, scores, nq, ix.nl,
-                       L, out_leaf, out_dist, tail);
-  } else if (L <= kWaveTopL && ix.nl <= 64 * 32) {
-    hipLaunchKernelGGL(topl_wave_kernel<32>, dim3((nq + 3) / 4), dim3(256), 0, s, scores, nq, ix.nl,
-                       L, out_leaf, out_dist, tail);
+  if (L <= kWaveTopL && ix.nl <= 256 * 4) {
+    hipLaunchKernelGGL(topl_block_kernel<4>, dim3(nq), dim3(256), 0, s, scores, ix.nl, L, out_leaf,
+                       out_dist, tail);
+  } else if (L <= kWaveTopL && ix.nl <= 256 * 8) {
+    hipLaunchKernelGGL(topl_block_kernel<8>, dim3(nq), dim3(256), 0, s, scores, ix.nl, L, out_leaf,
+                       out_dist, tail);
   } else if (ix.nl <= kLdsSelectLeaves && lds + kStaticLds <= 160 * 1024) {
     hipLaunchKernelGGL(topl_select_kernel, dim3(nq), dim3(256), lds, s, scores, ix.nl, L, kcap,
                        out_leaf, out_dist, tail);
@@ -2403,6 +2449,15 @@ hipError_t LaunchExactDistances(const DeviceIndex& ix, const float* queries, int
   hipLaunchKernelGGL(exact_distances_kernel, dim3(nq), dim3(128), 0, s, queries, ix.dataset,
                      ix.dim, ix.metric, ids, k, out);
   return hipGetLastError();
+}
+
+hipError_t SetPhaseStamps(unsigned long long* p) {
+#ifdef SMX_PHASE_STAMPS
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_phase_stamps), &p, sizeof(p));
+#else
+  (void)p;
+  return hipSuccess;
+#endif
 }
 
 hipError_t LaunchFill64(uint64_t* p, uint64_t v, size_t n, hipStream_t s) {

@@ -79,7 +79,7 @@ int EffectiveKSteps(int nb) {
 struct CounterLayout {
   uint32_t stats, words;
   explicit CounterLayout(int nl) {
-    stats = (uint32_t(nl) + 31u) & ~31u;
+    stats = uint32_t(nl) * smx::kCounterStride;   // nl strided leaf counters first
     words = stats + 32u;
   }
 };
@@ -105,7 +105,7 @@ struct Workspace {
   uint32_t* gunits = nullptr;       // [16] the XCD groups' unit boundaries
   uint64_t* tau = nullptr;          // [nq]
   uint64_t* cand = nullptr;         // [nq][cap]
-  uint32_t* cand_count = nullptr;   // [nq]
+  uint32_t* cand_count = nullptr;   // [nq] strided (kCounterStride)
   uint32_t* fallback = nullptr;     // [nq] queries the wave final select hands back
   uint32_t* out_idx = nullptr;
   float* out_dist = nullptr;
@@ -346,7 +346,7 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
       (rc = DAlloc(&w.wave_start, size_t(std::max(h->grid, 1)))) ||
       (rc = DAlloc(&w.pos_unit0, size_t(nl + 1))) || (rc = DAlloc(&w.gunits, 16)) ||
       (rc = DAlloc(&w.work, max_items)) || (rc = DAlloc(&w.tau, nq)) ||
-      (rc = DAlloc(&w.cand, size_t(nq) * cap)) || (rc = DAlloc(&w.cand_count, nq)) ||
+      (rc = DAlloc(&w.cand, size_t(nq) * cap)) || (rc = DAlloc(&w.cand_count, size_t(nq) * smx::kCounterStride)) ||
       (rc = DAlloc(&w.fallback, nq)) ||
       (rc = DAlloc(&w.out_idx, size_t(nq) * width)) ||
       (rc = DAlloc(&w.out_dist, size_t(nq) * width)) || (rc = DAlloc(&w.out_count, nq))) {
@@ -483,7 +483,9 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     // front end: state reset, partition scores, top-L + ranks + LUTs
     smx::FrontArgs f;
     f.init.counters = w.counters;
-    f.init.n_counters = lay.words;
+    f.init.n_counters = uint32_t(nl);
+    f.init.stats = stats;
+    f.init.n_stats = 32u;
     f.init.cand_count = w.cand_count;
     f.init.n_cand = uint32_t(nq);
     f.init.tau = w.tau;
@@ -560,7 +562,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     if (++retries > 64) return Fail(SMX_INTERNAL, "candidate tightening did not converge");
     SMX_HIP(smx::LaunchTighten(w.cand, w.cand_count, w.cap, nq, kk, w.tau, s));
     SMX_HIP(smx::LaunchRefreshLanes(w.lanes, w.max_items, stats + 3, w.tau, ix.nb, s));
-    SMX_HIP(hipMemsetAsync(w.cand_count, 0, sizeof(uint32_t) * nq, s));
+    SMX_HIP(hipMemsetAsync(w.cand_count, 0, sizeof(uint32_t) * nq * smx::kCounterStride, s));
     SMX_HIP(hipMemsetAsync(stats, 0, sizeof(uint32_t) * 3, s));
     SMX_HIP(hipMemsetAsync(stats + 8, 0, 2 * sizeof(uint32_t), s));
     SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s));
@@ -587,6 +589,26 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
       }
     }
   }
+#ifdef SMX_PHASE_STAMPS
+  {
+    // diagnostic build: the phase stamps of this call to $SMX_PHASE_FILE
+    static unsigned long long* ps = nullptr;
+    const size_t words = size_t(3) * smx::kPhaseQueries * 8;
+    if (!ps) {
+      SMX_HIP(hipMalloc(&ps, words * 8));
+      SMX_HIP(smx::SetPhaseStamps(ps));
+    }
+    if (const char* path = std::getenv("SMX_PHASE_FILE")) {
+      SMX_HIP(hipDeviceSynchronize());
+      std::vector<unsigned long long> buf(words);
+      SMX_HIP(hipMemcpy(buf.data(), ps, words * 8, hipMemcpyDeviceToHost));
+      if (FILE* f = std::fopen(path, "wb")) {
+        std::fwrite(buf.data(), 8, buf.size(), f);
+        std::fclose(f);
+      }
+    }
+  }
+#endif
   smx_timings& t = h->timings;
   if (h->profiling) {
     // The stream is idle here, so reading the events costs no extra sync.

@@ -1,0 +1,68 @@
+"""Phase timeline of the front-end and select kernels (diagnostic build).
+
+    python tools/phase_stamps.py build     (here: compiles lib/libscann_mi355x_ps.so)
+    python tools/phase_stamps.py [seed]    (on the GPU box)
+
+The -DSMX_PHASE_STAMPS library writes the 100 MHz clock at phase boundaries
+of topl_wave_kernel (0), seed_tau_kernel (1) and final_select_rank_kernel (2)
+per query; this prints each phase's duration and where the kernels' spans go.
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+LIB = os.path.join(ROOT, "scann_amd", "lib", "libscann_mi355x_ps.so")
+NAMES = {0: ("topl_wave", ["load", "rounds", "compact+rank", "out+rank atomics", "lut"]),
+         1: ("seed_tau", ["lut+prefix", "score loop", "histogram", "lanes scatter"]),
+         2: ("final_select", ["load+narrow", "rank", "gid gather", "dedupe", "exact", "out"])}
+
+
+def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "build":
+        from scann_amd import build
+        print(build.build(force=True, defines=("SMX_PHASE_STAMPS",), out=LIB))
+        return
+    seed = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    os.environ["SMX_LIB"] = LIB
+    path = "/tmp/smx_phase.bin"
+    os.environ["SMX_PHASE_FILE"] = path
+    import torch
+    from bench import LEAVES_TO_SEARCH, NQ, PRE_NN, FINAL_NN, build_index
+    from scann_amd import _native
+    db, q, ix = build_index(1_183_514, seed=2)
+    nat = _native.NativeIndex(ix)
+    qd = torch.from_numpy(q).cuda()
+    oi = torch.zeros((NQ, FINAL_NN), dtype=torch.int32, device="cuda")
+    od = torch.zeros((NQ, FINAL_NN), dtype=torch.float32, device="cuda")
+    nat.set_tuning(4096, seed, 0, 32)
+    for _ in range(4):
+        nat.search_batched_device(qd.data_ptr(), NQ, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True,
+                                  oi.data_ptr(), od.data_ptr(), None)
+    torch.cuda.synchronize()
+    r = np.fromfile(path, dtype=np.uint64).reshape(3, 4096, 8)[:, :NQ].astype(np.int64)
+    for kid, (name, phases) in NAMES.items():
+        t = r[kid]
+        n = len(phases) + 1
+        ok = (t[:, :n] > 0).all(1)
+        t = t[ok][:, :n]
+        if not len(t):
+            print(f"{name}: no stamps")
+            continue
+        t0 = t[:, 0].min()
+        span = (t[:, n - 1].max() - t0) / 100.0
+        st = (t[:, 0] - t0) / 100.0
+        en = (t[:, n - 1] - t0) / 100.0
+        print(f"{name}: {len(t)} queries, span {span:.1f} us; start p50 {np.median(st):.1f} "
+              f"max {st.max():.1f}; end p10 {np.percentile(en, 10):.1f} p50 {np.median(en):.1f} "
+              f"max {en.max():.1f}")
+        for i, ph in enumerate(phases):
+            d = (t[:, i + 1] - t[:, i]) / 100.0
+            print(f"    {ph:18s} p50 {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} "
+                  f"max {d.max():6.2f} us")
+
+
+if __name__ == "__main__":
+    main()
