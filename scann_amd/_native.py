@@ -8,6 +8,7 @@ raises, and every search runs the HIP kernels.
 from __future__ import annotations
 
 import ctypes
+import sys
 import os
 
 import numpy as np
@@ -100,6 +101,19 @@ def _c(a, dt):
     return np.ascontiguousarray(a, dtype=dt)
 
 
+def _current_stream(stream):
+    """The HIP stream a device entry point runs on: the caller's, else torch's
+    current stream when torch is in use (the device entry points return with
+    the work enqueued, so results are ordered with the caller's own reads and
+    writes of those buffers), else the library's own stream (None)."""
+    if stream is not None:
+        return stream
+    torch = sys.modules.get("torch")
+    if torch is not None and torch.cuda.is_available() and torch.cuda.is_initialized():
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    return None
+
+
 class NativeIndex:
     """Owns one smx_index handle (device-resident index)."""
 
@@ -150,7 +164,8 @@ class NativeIndex:
                               out_idx_ptr, out_dist_ptr, out_count_ptr=None, stream=None):
         p = SearchParams(int(leaves), int(pre_nn), int(final_nn), int(bool(reorder)))
         check(self.lib.smx_search_batched_device(self.h, q_ptr, nq, self.dim, ctypes.byref(p),
-                                                 out_idx_ptr, out_dist_ptr, out_count_ptr, stream),
+                                                 out_idx_ptr, out_dist_ptr, out_count_ptr,
+                                                 _current_stream(stream)),
               "Error during search")
 
     # -- range-split shards; device pointers ----------------
@@ -166,14 +181,16 @@ class NativeIndex:
                             stream=None):
         p = SearchParams(int(leaves), int(pre_nn), int(final_nn), int(bool(reorder)))
         check(self.lib.smx_search_shard_device(self.h, q_ptr, nq, self.dim, ctypes.byref(p),
-                                               entries_ptr, stream), "Error during search")
+                                               entries_ptr, _current_stream(stream)),
+              "Error during search")
 
     def merge_shards_device(self, world, nq, leaves, pre_nn, final_nn, reorder, entries_ptr,
                             out_idx_ptr, out_dist_ptr, out_count_ptr=None, stream=None):
         p = SearchParams(int(leaves), int(pre_nn), int(final_nn), int(bool(reorder)))
         check(self.lib.smx_merge_shards_device(self.h, int(world), int(nq), ctypes.byref(p),
                                                entries_ptr, out_idx_ptr, out_dist_ptr,
-                                               out_count_ptr, stream), "smx_merge_shards")
+                                               out_count_ptr, _current_stream(stream)),
+              "smx_merge_shards")
 
     def search_pre_reorder(self, queries, leaves, pre_nn):
         q = _c(queries, np.float32)

@@ -126,9 +126,33 @@ struct SeedArgs {
   int nb;
 };
 
+// An overflowed query's rescan (RescanQuery, inside the select kernels):
+// the query's leaves, LUT and lists, and the code layout of the index.
+struct RescanArgs {
+  const int32_t* topl_leaf;   // [nq][L]
+  const float* topl_dist;
+  int L;
+  int residual;
+  int ksteps;
+  const int8_t* lut;          // [nq][2K][16]
+  const float* inv;
+  const uint8_t* tiles;
+  const uint64_t* tile_off;
+  const uint32_t* leaf_size;
+  const uint32_t* members;
+  const uint64_t* member_off;
+  int shift;
+  uint64_t* cand;
+  uint32_t* cand_count;       // strided
+  uint64_t* tau_key;
+  uint32_t cap;
+  int kk;
+  uint32_t* stats;            // [10] queries rescanned [11] rescan rounds
+};
+
 struct SelectArgs {
   const uint64_t* cand;
-  const uint32_t* cand_count;
+  uint32_t* cand_count;       // (rewritten by an overflow rescan)
   uint32_t cap;
   int kk;                     // k' kept before dedupe
   int pre_nn;                 // kept after SOAR dedupe
@@ -147,10 +171,9 @@ struct SelectArgs {
   float* out_dist;
   int32_t* out_count;
   int out_width;
-  uint32_t* overflow;         // stats: [0] flag [1] max overflow [2] max count [8] sum [9] fallbacks
+  uint32_t* overflow;         // stats: [0] flag [1] max overflow [2] max count [8] sum
   int stats;                  // also compute [2] and [8] (profiled calls)
-  uint32_t* fallback;         // [nq] queries the wave kernel hands to the block kernel (or NULL)
-  const uint32_t* qlist;      // block kernel over these queries only (or NULL: all)
+  RescanArgs rescan;          // overflowed lists are rescanned in the select kernels
   ShardEntry* shard_out;      // shard mode: [nq][kk] local top-k' entries (or NULL)
   const uint32_t* row_base;   // shard: whole-leaf row of each leaf's first shard row
   const float* member_rows;   // shard: [members][dim] rows for the exact distances
@@ -218,13 +241,8 @@ hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int va
 // Resident scan workgroups per CU (occupancy of the index's instantiation).
 hipError_t ScanBlocksPerCU(const DeviceIndex& ix, int* blocks);
 hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s);
-// After LaunchTighten: the items' lane records take the new thresholds.
-hipError_t LaunchRefreshLanes(ItemLane* lanes, uint32_t max_items, const uint32_t* totals,
-                              const uint64_t* tau_key, int nb, hipStream_t s);
-hipError_t LaunchTighten(const uint64_t* cand, const uint32_t* cand_count, uint32_t cap,
-                         int nq, int kk, uint64_t* tau_key, hipStream_t s);
-// One wave per query when a.fallback is set and the buffers fit; the block
-// kernel otherwise, or over a.qlist (the wave kernel's fallback queries).
+// The rank kernel (one block per query, <= kSelMax keys in LDS) for k' <=
+// kSelMax, the block kernel otherwise; both rescan overflowed lists first.
 hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s);
 hipError_t LaunchMergeShards(const MergeArgs& a, hipStream_t s);
 hipError_t LaunchExactDistances(const DeviceIndex& ix, const float* queries, int nq,

@@ -996,6 +996,7 @@ __device__ __forceinline__ void LoadCodes(const uint8_t* p, uint32_t* codes) {
 constexpr int kSeedPerThread = 32;
 constexpr uint32_t kSeedCap = 256u * kSeedPerThread;
 constexpr int kSeedMaxLeaves = 64;   // one wave of leaf slots
+constexpr int kSeedSel = 1024;       // values under the minima bound ranked exactly
 
 // The threshold key of query qi from its seed leaves, or kNoThreshold (no
 // bound); block-wide (256 threads, all call; the value is returned to all).
@@ -1004,12 +1005,18 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
   constexpr int W = 4 * NW;
   constexpr int U = 8;   // datapoints whose code loads are in flight together
+  constexpr int NB = (K + 1) / 2;   // code bytes per half holding steps < K
   __shared__ __align__(16) int8_t lut[2 * K * 16];
+  // pair tables: ptab[h][j][byte] = the LUT sum of the two nibbles of code
+  // byte j of half h (blocks 4j + h and 4j + 2 + h): one LDS lookup per code
+  // byte instead of one per nibble
+  __shared__ int16_t ptab[2 * NB * 256];
+  __shared__ uint64_t skey[kSeedSel];
   __shared__ uint32_t hist[256];
   __shared__ uint32_t s_start[kSeedMaxLeaves + 1];
   __shared__ uint64_t s_tile0[kSeedMaxLeaves];
   __shared__ float s_bias[kSeedMaxLeaves];
-  __shared__ uint32_t wsum[4], s_lo[4], s_hi[4], s_bin, s_below;
+  __shared__ uint32_t wsum[4], s_lo[4], s_hi[4], s_bin, s_below, s_thi, s_cnt;
   __shared__ uint64_t s_T;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   SMX_PHASE(1, qi, 0);
@@ -1039,6 +1046,15 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
   const uint32_t total = min(s_start[kSeedMaxLeaves], kSeedCap);
   const uint32_t kk = uint32_t(a.kk);
   if (kk == 0 || total < kk) return kNoThreshold;   // no bound: the threshold stays open
+#pragma unroll
+  for (int i = 0; i < 2 * NB; ++i) {
+    const int h = i / NB, j = i % NB, s0 = 2 * j, s1 = 2 * j + 1;
+    int v = lut[(2 * s0 + h) * 16 + (tid & 15)];
+    if (s1 < K) v += lut[(2 * s1 + h) * 16 + (tid >> 4)];
+    ptab[i * 256 + tid] = int16_t(v);
+  }
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
 
   uint32_t vals[kSeedPerThread];
   int r = 0;   // seed leaf of this thread's current number (numbers only grow)
@@ -1061,10 +1077,10 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
       for (int u = 0; u < U; ++u) {
         int acc = 0;
 #pragma unroll
-        for (int s = 0; s < K; ++s) {
-          const uint32_t n0 = (c0[u][s >> 3] >> ((s & 7) * 4)) & 15u;
-          const uint32_t n1 = (c1[u][s >> 3] >> ((s & 7) * 4)) & 15u;
-          acc += int(lut[(2 * s) * 16 + n0]) + int(lut[(2 * s + 1) * 16 + n1]);
+        for (int j = 0; j < NB; ++j) {
+          const uint32_t b0 = (c0[u][j >> 2] >> (8 * (j & 3))) & 0xFFu;
+          const uint32_t b1 = (c1[u][j >> 2] >> (8 * (j & 3))) & 0xFFu;
+          acc += int(ptab[j * 256 + b0]) + int(ptab[(NB + j) * 256 + b1]);
         }
         const uint32_t g = uint32_t(tid) + 256u * uint32_t(i0 + u);
         vals[i0 + u] = g < total ? OrderedBits(DistOf(acc, inv, s_bias[ru[u]])) : 0xFFFFFFFFu;
@@ -1075,6 +1091,38 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
     }
   }
   SMX_PHASE(1, qi, 2);
+  if (kk <= 256u) {
+    // The kk-th smallest of the 256 per-thread minima bounds the kk-th value
+    // from above (a subset's kk-th is never smaller); the few values under it
+    // (~1.3 kk) are compacted and the exact kk-th found by a counting rank
+    // over (value, number) keys.  Histogram rounds only when they overflow.
+    uint32_t vmin = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i < kSeedPerThread; ++i) vmin = min(vmin, vals[i]);
+    const uint64_t mk = (uint64_t(vmin) << 32) | uint32_t(tid);
+    skey[tid] = mk;
+    __syncthreads();
+    if (CountLess(skey, 256u, mk) == kk - 1u) s_thi = vmin;
+    __syncthreads();
+    const uint32_t thi = s_thi;
+#pragma unroll
+    for (int i = 0; i < kSeedPerThread; ++i)
+      if (vals[i] <= thi) {
+        const uint32_t pos = atomicAdd(&s_cnt, 1u);
+        if (pos < uint32_t(kSeedSel)) skey[pos] = (uint64_t(vals[i]) << 32) | (uint32_t(tid) + 256u * i);
+      }
+    __syncthreads();
+    const uint32_t c = s_cnt;
+    if (c <= uint32_t(kSeedSel)) {
+      for (uint32_t i = tid; i < c; i += 256) {
+        const uint64_t key = skey[i];
+        if (CountLess(skey, c, key) == kk - 1u) s_T = (key & 0xFFFFFFFF00000000ull) | 0xFFFFFFFFull;
+      }
+      __syncthreads();
+      SMX_PHASE(1, qi, 3);
+      return s_T;
+    }
+  }
   // range of the values, then histogram rounds down to the kk-th value
   uint32_t lo = 0xFFFFFFFFu, hi = 0;
 #pragma unroll
@@ -1534,36 +1582,115 @@ __global__ void __launch_bounds__(64) leaf_scores_kernel(const uint8_t* __restri
   }
 }
 
-// Overflow recovery, part 2: the items' lane records take the tightened
-// thresholds (the scan's sum limits and key tests read them there).
-__global__ void refresh_lanes_kernel(ItemLane* __restrict__ lanes, const uint32_t* __restrict__ totals,
-                                     const uint64_t* __restrict__ tau_key, int nb) {
-  const size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= size_t(totals[1]) * kQueriesPerTile) return;
-  ItemLane v = lanes[i];
-  if (v.amax == kNoSum) return;
-  const uint64_t T = tau_key[v.qid];
-  const int smin = -128 * nb, smax = 128 * nb;
-  v.tau = T;
-  v.amax = T == kNoThreshold ? smax : SumLimit(FromOrdered(uint32_t(T >> 32)), v.inv, v.bias, smin, smax);
-  lanes[i] = v;
+// ---------------------------------------------------------------------------
+// Overflow recovery on the device (no host round trip).  A query whose list
+// overflowed (more candidates under its threshold than the list holds) keeps
+// the first `cap` arrivals, every one a genuine candidate; their k'-th
+// smallest key is then a valid, tighter threshold.  The block rescans the
+// query's L leaves with the same sums, distances and keys as the scan
+// (VALU, pair tables as SeedTau) and keeps the keys under it; cap >= 2 k'
+// makes each further pass drop at least cap - k' keys, so this converges.
+// Rare path: grid-stride over the queries, most blocks only read counts.
+// ---------------------------------------------------------------------------
+// k-th smallest (1-based) of n u64 keys in global memory, block-wide: eight
+// 8-bit radix passes over the keys that share the prefix found so far.
+__device__ uint64_t KthSmallestKey(const uint64_t* keys, uint32_t n, uint32_t k, uint32_t* hist,
+                                   uint32_t* wsum) {
+  __shared__ uint64_t s_prefix;
+  __shared__ uint32_t s_need;
+  const int tid = threadIdx.x;
+  if (tid == 0) { s_prefix = 0; s_need = k; }
+  for (int pass = 0; pass < 8; ++pass) {
+    const int shift = 56 - 8 * pass;
+    hist[tid] = 0;
+    __syncthreads();
+    const uint64_t prefix = s_prefix;
+    const uint32_t need = s_need;
+    for (uint32_t i = tid; i < n; i += 256) {
+      const uint64_t key = keys[i];
+      if (pass == 0 || (key >> (shift + 8)) == (prefix >> (shift + 8)))
+        atomicAdd(&hist[uint32_t(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    const uint32_t hv = hist[tid];
+    const uint32_t inc = BlockInclusiveScan256(hv, wsum);
+    __syncthreads();   // every thread has read s_prefix / s_need
+    if (inc - hv < need && inc >= need) {
+      s_prefix = prefix | (uint64_t(tid) << shift);
+      s_need = need - (inc - hv);
+    }
+    __syncthreads();
+  }
+  return s_prefix;
 }
 
-// Overflow recovery: the k'-th smallest stored key is a valid (tighter)
-// threshold because every stored key is a genuine candidate.
-__global__ void __launch_bounds__(256) tighten_kernel(const uint64_t* __restrict__ cand,
-                                                      const uint32_t* __restrict__ cand_count,
-                                                      uint32_t cap, int kk,
-                                                      uint64_t* __restrict__ tau_key) {
-  extern __shared__ uint64_t keys[];
-  const int qi = blockIdx.x;
-  if (cand_count[size_t(qi) * kCounterStride] <= cap || kk <= 0) return;
-  const uint32_t np2 = NextPow2(cap);
-  for (uint32_t i = threadIdx.x; i < np2; i += blockDim.x)
-    keys[i] = i < cap ? cand[size_t(qi) * cap + i] : ~0ull;
+// Query qi's list after a rescan under the k'-th smallest of its first cap
+// stored keys (repeated while it still overflows); returns the new count.
+// Block-wide (256 threads); runtime K (a rare path: one VALU pass over the
+// query's L leaves per round, pair tables as SeedTau).
+__device__ __forceinline__ uint32_t RescanQuery(const RescanArgs& a, int qi, uint32_t n) {
+  __shared__ __align__(16) int8_t lut[2 * kMaxBlocks * 16];
+  __shared__ int16_t ptab[2 * (kMaxBlocks / 4) * 256];   // NB <= 16
+  __shared__ uint32_t hist[256], wsum[4], s_n;
+  const int tid = threadIdx.x;
+  const int K = a.ksteps, NB = (K + 1) / 2, NW = (NB + 3) / 4, W = 4 * NW;
+  if (tid == 0) atomicAdd(&a.stats[10], 1u);
+  for (int e = tid; e < 2 * K * 16 / 4; e += 256)
+    reinterpret_cast<uint32_t*>(lut)[e] = reinterpret_cast<const uint32_t*>(a.lut + size_t(qi) * 2 * K * 16)[e];
   __syncthreads();
-  BitonicSort(keys, np2);
-  if (threadIdx.x == 0 && keys[kk - 1] < tau_key[qi]) tau_key[qi] = keys[kk - 1];
+  for (int i = 0; i < 2 * NB; ++i) {
+    const int h = i / NB, j = i % NB, s0 = 2 * j, s1 = 2 * j + 1;
+    int v = lut[(2 * s0 + h) * 16 + (tid & 15)];
+    if (s1 < K) v += lut[(2 * s1 + h) * 16 + (tid >> 4)];
+    ptab[i * 256 + tid] = int16_t(v);
+  }
+  const float inv = a.inv[qi];
+  uint64_t* row = a.cand + size_t(qi) * a.cap;
+  while (n > a.cap) {   // block-uniform
+    const uint64_t T = KthSmallestKey(row, a.cap, uint32_t(a.kk), hist, wsum);
+    if (tid == 0) {
+      s_n = 0;
+      atomicAdd(&a.stats[11], 1u);
+      a.tau_key[qi] = T;
+    }
+    __syncthreads();
+    for (int i = 0; i < a.L; ++i) {
+      const int32_t leaf = a.topl_leaf[size_t(qi) * a.L + i];
+      if (leaf < 0) continue;
+      const uint32_t ln = a.leaf_size[leaf];
+      const uint64_t t0 = a.tile_off[leaf];
+      const uint64_t moff = a.member_off[leaf];
+      const float bias = a.residual ? a.topl_dist[size_t(qi) * a.L + i] : 0.0f;
+      for (uint32_t dp = tid; dp < ln; dp += 256) {
+        const uint32_t* tp = reinterpret_cast<const uint32_t*>(
+            a.tiles + ((t0 + (dp >> 5)) * 64 + (dp & 31)) * W);
+        uint32_t c0[4] = {0, 0, 0, 0}, c1[4] = {0, 0, 0, 0};
+        for (int w = 0; w < NW; ++w) {
+          c0[w] = tp[w];
+          c1[w] = tp[8 * W + w];   // + 32 lanes * W bytes
+        }
+        int acc = 0;
+        for (int j = 0; j < NB; ++j) {
+          const uint32_t b0 = (c0[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+          const uint32_t b1 = (c1[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+          acc += int(ptab[j * 256 + b0]) + int(ptab[(NB + j) * 256 + b1]);
+        }
+        const float d = DistOf(acc, inv, bias);
+        const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp) : a.members[moff + dp];
+        const uint64_t key = (uint64_t(OrderedBits(d)) << 32) | tie;
+        if (key <= T) {
+          const uint32_t p = atomicAdd(&s_n, 1u);
+          if (p < a.cap) row[p] = key;
+        }
+      }
+    }
+    __syncthreads();
+    n = s_n;
+    __syncthreads();   // every thread has read s_n before the next round resets it
+  }
+  if (tid == 0) a.cand_count[size_t(qi) * kCounterStride] = n;
+  __syncthreads();
+  return n;
 }
 
 // Exact reorder distance (A.8): 8 fused accumulators over dims 0..8m-1,
@@ -1606,13 +1733,15 @@ __device__ float ExactDistance(const float* __restrict__ q, const float* __restr
 // (distance, id) sort of SortAndDropResults.
 // LDS: keys[cap_pow2] u64 | q[dim] f32 | gid/dist scratch.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) final_select_kernel(SelectArgs a) {
+__device__ void FinalSelectQuery(const SelectArgs& a, int qi) {
   extern __shared__ uint64_t lds[];
-  const int qi = a.qlist ? int(a.qlist[blockIdx.x]) : int(blockIdx.x);
-  const uint32_t raw_n = a.cand_count[size_t(qi) * kCounterStride];
-  if (threadIdx.x == 0 && raw_n > a.cap && !a.qlist) {   // overflow: the host tightens and rescans
-    a.overflow[0] = 1u;
-    atomicMax(&a.overflow[1], raw_n);
+  uint32_t raw_n = a.cand_count[size_t(qi) * kCounterStride];
+  if (raw_n > a.cap) {   // block-uniform: the list overflowed, rescan on the device
+    if (threadIdx.x == 0) {
+      a.overflow[0] = 1u;
+      atomicMax(&a.overflow[1], raw_n);
+    }
+    raw_n = RescanQuery(a.rescan, qi, raw_n);
   }
 
   const uint32_t n = min(raw_n, a.cap);
@@ -1738,6 +1867,10 @@ __global__ void __launch_bounds__(256) final_select_kernel(SelectArgs a) {
   if (threadIdx.x == 0 && a.out_count) a.out_count[qi] = int32_t(keep);
 }
 
+__global__ void __launch_bounds__(256) final_select_kernel(SelectArgs a) {
+  FinalSelectQuery(a, int(blockIdx.x));
+}
+
 // ---------------------------------------------------------------------------
 // Final selection, default path: one 256-thread block per query and at most
 // kSelMax keys ever held in LDS.  A linear histogram of the distance word
@@ -1854,10 +1987,13 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int qi = blockIdx.x;
   SMX_PHASE(2, qi, 0);
-  const uint32_t raw_n = a.cand_count[size_t(qi) * kCounterStride];
-  if (threadIdx.x == 0 && raw_n > a.cap && !a.qlist) {   // overflow: the host tightens and rescans
-    a.overflow[0] = 1u;
-    atomicMax(&a.overflow[1], raw_n);
+  uint32_t raw_n = a.cand_count[size_t(qi) * kCounterStride];
+  if (raw_n > a.cap) {   // block-uniform: the list overflowed, rescan on the device
+    if (threadIdx.x == 0) {
+      a.overflow[0] = 1u;
+      atomicMax(&a.overflow[1], raw_n);
+    }
+    raw_n = RescanQuery(a.rescan, qi, raw_n);
   }
   if (tid == 0) s_c = 0;
   const uint32_t n = min(raw_n, a.cap);
@@ -1915,13 +2051,19 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
       lo = blo;
       hi = bhi;
     }
-    if (!ok) {   // block-uniform
-      if (tid == 0) a.fallback[atomicAdd(&a.overflow[9], 1u)] = uint32_t(qi);
-      return;
-    }
-    for (uint32_t i = tid; i < n; i += 256) {
-      const uint64_t key = ck[i];
-      if (uint32_t(key >> 32) <= lim) sel[atomicAdd(&s_c, 1u)] = key;
+    if (ok) {
+      for (uint32_t i = tid; i < n; i += 256) {
+        const uint64_t key = ck[i];
+        if (uint32_t(key >> 32) <= lim) sel[atomicAdd(&s_c, 1u)] = key;
+      }
+    } else {   // block-uniform: > kSelMax keys on one distance value (ties):
+      // the k-th key itself by a radix select over the whole keys (unique),
+      // then exactly the k keys up to it
+      const uint64_t kth = KthSmallestKey(ck, n, k, hist, wsum);
+      for (uint32_t i = tid; i < n; i += 256) {
+        const uint64_t key = ck[i];
+        if (key <= kth) sel[atomicAdd(&s_c, 1u)] = key;
+      }
     }
     __syncthreads();
   }
@@ -2391,27 +2533,6 @@ hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStrea
   return hipGetLastError();
 }
 
-hipError_t LaunchTighten(const uint64_t* cand, const uint32_t* cand_count, uint32_t cap, int nq,
-                         int kk, uint64_t* tau_key, hipStream_t s) {
-  if (nq == 0) return hipSuccess;
-  uint32_t np2 = 1;
-  while (np2 < cap) np2 <<= 1;
-  const size_t lds = size_t(np2) * 8;
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(tighten_kernel, dim3(nq), dim3(256), lds, s, cand, cand_count, cap, kk,
-                     tau_key);
-  return hipGetLastError();
-}
-
-hipError_t LaunchRefreshLanes(ItemLane* lanes, uint32_t max_items, const uint32_t* totals,
-                              const uint64_t* tau_key, int nb, hipStream_t s) {
-  const size_t n = size_t(max_items) * kQueriesPerTile;
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(refresh_lanes_kernel, dim3((n + 255) / 256), dim3(256), 0, s, lanes, totals,
-                     tau_key, nb);
-  return hipGetLastError();
-}
-
 hipError_t LaunchMergeShards(const MergeArgs& a, hipStream_t s) {
   if (a.nq == 0) return hipSuccess;
   if (a.world < 1 || a.world > 64 || a.kk > kSelMax || a.world * a.kk > kMergeMaxEntries)
@@ -2424,21 +2545,21 @@ hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s) {
   if (nq == 0) return hipSuccess;
   // the overflow flag is raised by the select kernels themselves; the
   // candidate-count statistics only for profiled calls
-  if (!a.qlist && a.stats)
+  if (a.stats)
     hipLaunchKernelGGL(cand_stats_kernel, dim3(1), dim3(1024), 0, s, a.cand_count, nq, a.cap,
                        a.overflow);
   uint32_t kkp2 = 1;
   while (kkp2 < uint32_t(a.kk)) kkp2 <<= 1;
-  if (!a.qlist && a.fallback && a.kk <= kSelMax) {   // (shard mode too)
-    hipLaunchKernelGGL(final_select_rank_kernel, dim3(nq), dim3(256), 0, s, a);
-    return hipGetLastError();
-  }
   uint32_t kcap = 1;
   while (kcap < a.cap) kcap <<= 1;
   const uint32_t selcap = std::max<uint32_t>(2048u, 2 * kkp2);
   const size_t lds = size_t(kcap) * 8 + size_t(selcap) * 8 + size_t(kkp2) * 8 +
                      size_t(a.dim) * 4 + size_t(a.kk) * 8 + (kSelBins + 256) * 4;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (a.kk <= kSelMax) {   // (shard mode too)
+    hipLaunchKernelGGL(final_select_rank_kernel, dim3(nq), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(final_select_kernel, dim3(nq), dim3(256), lds, s, a);
   return hipGetLastError();
 }

@@ -106,7 +106,6 @@ struct Workspace {
   uint64_t* tau = nullptr;          // [nq]
   uint64_t* cand = nullptr;         // [nq][cap]
   uint32_t* cand_count = nullptr;   // [nq] strided (kCounterStride)
-  uint32_t* fallback = nullptr;     // [nq] queries the wave final select hands back
   uint32_t* out_idx = nullptr;
   float* out_dist = nullptr;
   int32_t* out_count = nullptr;
@@ -116,7 +115,7 @@ struct Workspace {
     DFree(inv);
     DFree(counters); DFree(rank); DFree(leaf_item0); DFree(lanes); DFree(wave_start);
     DFree(pos_unit0); DFree(gunits);
-    DFree(work); DFree(tau); DFree(cand); DFree(cand_count); DFree(fallback); DFree(out_idx);
+    DFree(work); DFree(tau); DFree(cand); DFree(cand_count); DFree(out_idx);
     DFree(out_dist);
     DFree(out_count);
     nq = L = kk = dim = width = 0;
@@ -145,6 +144,8 @@ struct smx_index {
   uint32_t* host_stats = nullptr;  // pinned copy of the stats words
   smx_timings timings{};
   hipEvent_t ev[16] = {};
+  hipEvent_t done_ev = nullptr;      // the last call's end (cross-stream ordering)
+  hipStream_t last_stream = nullptr;
   // scan variant 8 (diagnostics): per-item stamps, dumped to $SMX_STAMPS
   unsigned long long* stamps = nullptr;
   uint32_t* stamp_count = nullptr;
@@ -347,7 +348,6 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
       (rc = DAlloc(&w.pos_unit0, size_t(nl + 1))) || (rc = DAlloc(&w.gunits, 16)) ||
       (rc = DAlloc(&w.work, max_items)) || (rc = DAlloc(&w.tau, nq)) ||
       (rc = DAlloc(&w.cand, size_t(nq) * cap)) || (rc = DAlloc(&w.cand_count, size_t(nq) * smx::kCounterStride)) ||
-      (rc = DAlloc(&w.fallback, nq)) ||
       (rc = DAlloc(&w.out_idx, size_t(nq) * width)) ||
       (rc = DAlloc(&w.out_dist, size_t(nq) * width)) || (rc = DAlloc(&w.out_count, nq))) {
     w.Release();
@@ -469,8 +469,26 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sel.out_width = width;
   sel.overflow = stats;
   sel.stats = h->profiling ? 1 : 0;
-  sel.fallback = w.fallback;
-  sel.qlist = nullptr;
+  smx::RescanArgs& ra = sel.rescan;
+  ra.topl_leaf = w.topl_leaf;
+  ra.topl_dist = w.topl_dist;
+  ra.L = L;
+  ra.residual = ix.residual;
+  ra.ksteps = ix.ksteps;
+  ra.lut = w.lut;
+  ra.inv = w.inv;
+  ra.tiles = ix.tiles;
+  ra.tile_off = ix.tile_off;
+  ra.leaf_size = ix.leaf_size;
+  ra.members = ix.members;
+  ra.member_off = ix.member_off;
+  ra.shift = ix.shift;
+  ra.cand = w.cand;
+  ra.cand_count = w.cand_count;
+  ra.tau_key = w.tau;
+  ra.cap = w.cap;
+  ra.kk = kk;
+  ra.stats = stats;
   sel.shard_out = shard_out;
   sel.row_base = ix.row_base;
   sel.member_rows = ix.member_rows;
@@ -508,9 +526,14 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     Mark(h, 6, s);
     SMX_HIP(smx::LaunchFinalSelect(sel, nq, s));
     Mark(h, 7, s);
-    SMX_HIP(hipMemcpyAsync(h->host_stats, stats, 10 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     return SMX_OK;
   };
+  // The workspace is shared by every stream: a call on another stream than
+  // the last one waits for that one's work (stream-ordered, no host sync).
+  if (h->last_stream != s) {
+    SMX_HIP(hipStreamWaitEvent(s, h->done_ev, 0));
+    h->last_stream = s;
+  }
   bool ran = false;
   // (profiled calls run eagerly: HIP events recorded inside a captured graph
   // carry no timestamps)
@@ -544,31 +567,13 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     }
   }
   if (!ran && (rc = first_pass())) return rc;
-  SMX_HIP(hipStreamSynchronize(s));
-  int retries = 0;
-  uint32_t st[10];
-  std::memcpy(st, h->host_stats, sizeof(st));
-  for (;;) {
-    if (!st[0]) {
-      if (st[9]) {  // queries the wave final select could not narrow
-        smx::SelectArgs fb = sel;
-        fb.qlist = w.fallback;
-        SMX_HIP(smx::LaunchFinalSelect(fb, int(st[9]), s));
-        SMX_HIP(hipStreamSynchronize(s));
-      }
-      break;
-    }
-    // a candidate list overflowed: tighten the thresholds and rescan
-    if (++retries > 64) return Fail(SMX_INTERNAL, "candidate tightening did not converge");
-    SMX_HIP(smx::LaunchTighten(w.cand, w.cand_count, w.cap, nq, kk, w.tau, s));
-    SMX_HIP(smx::LaunchRefreshLanes(w.lanes, w.max_items, stats + 3, w.tau, ix.nb, s));
-    SMX_HIP(hipMemsetAsync(w.cand_count, 0, sizeof(uint32_t) * nq * smx::kCounterStride, s));
-    SMX_HIP(hipMemsetAsync(stats, 0, sizeof(uint32_t) * 3, s));
-    SMX_HIP(hipMemsetAsync(stats + 8, 0, 2 * sizeof(uint32_t), s));
-    SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s));
-    Mark(h, 6, s);
-    SMX_HIP(smx::LaunchFinalSelect(sel, nq, s));
-    Mark(h, 7, s);
+  SMX_HIP(hipEventRecord(h->done_ev, s));
+  // No host round trip: overflow and the select's fallback queries are
+  // handled on the device, so the call returns with the work enqueued
+  // (search_batched_device is stream-ordered; the host-buffer entry points
+  // synchronise on their result copies).  Profiled calls read the stats.
+  uint32_t st[12] = {};
+  if (h->profiling || variant == 8) {
     SMX_HIP(hipMemcpyAsync(h->host_stats, stats, sizeof(st), hipMemcpyDeviceToHost, s));
     SMX_HIP(hipStreamSynchronize(s));
     std::memcpy(st, h->host_stats, sizeof(st));
@@ -627,7 +632,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   t.scan_code_bytes = double(cb);
   t.seed_pairs = int32_t(std::min(seed, L)) * nq;
   t.scan_pairs = int32_t(st[3]);
-  t.overflow_retries = retries;
+  t.overflow_retries = int32_t(st[11]);   // rescan passes (queries: st[10])
   t.max_candidates = int32_t(st[2]);
   t.scan_item_tiles = double(st[5]);
   t.mean_candidates = float(st[8]) / float(nq);
@@ -698,6 +703,12 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
     return Fail(SMX_DEVICE_ERROR, "hipStreamCreate failed");
   }
   for (auto& e : h->ev) (void)hipEventCreate(&e);
+  if (hipEventCreateWithFlags(&h->done_ev, hipEventDisableTiming) != hipSuccess) {
+    smx_index_destroy(h);
+    return Fail(SMX_DEVICE_ERROR, "hipEventCreate failed");
+  }
+  SMX_HIP(hipEventRecord(h->done_ev, h->stream));
+  h->last_stream = h->stream;
   hipDeviceProp_t prop;
   SMX_HIP(hipGetDeviceProperties(&prop, device));
   {
@@ -705,7 +716,7 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
     SMX_HIP(smx::ScanBlocksPerCU(h->ix, &per_cu));
     h->grid = prop.multiProcessorCount * std::max(1, per_cu);
   }
-  if (hipHostMalloc(reinterpret_cast<void**>(&h->host_stats), 16 * sizeof(uint32_t)) != hipSuccess) {
+  if (hipHostMalloc(reinterpret_cast<void**>(&h->host_stats), 32 * sizeof(uint32_t)) != hipSuccess) {
     smx_index_destroy(h);
     return Fail(SMX_OUT_OF_MEMORY, "hipHostMalloc failed");
   }
@@ -728,6 +739,7 @@ int smx_index_destroy(smx_index* h) {
   FreeIndex(h->ix);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
+  if (h->done_ev) (void)hipEventDestroy(h->done_ev);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return SMX_OK;

@@ -38,6 +38,15 @@ def test_library_exports_every_declared_symbol(lib):
     assert not missing
 
 
+def test_library_resolves_every_internal_symbol(lib):
+    """A lazily bound load hides a missing definition until the first call:
+    every symbol of the library's own namespace must be defined in it."""
+    from scann_amd import build
+    out = os.popen(f"nm -D --undefined-only {build.OUT}").read()
+    assert "_ZN3smx" not in out, [l for l in out.splitlines() if "_ZN3smx" in l]
+    ctypes.CDLL(build.OUT, mode=os.RTLD_NOW | os.RTLD_LOCAL)
+
+
 def test_binding_covers_every_declared_symbol():
     from scann_amd import _native
     assert sorted(_native.SIGNATURES) == declared_functions()

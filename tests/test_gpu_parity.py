@@ -112,7 +112,8 @@ def test_exact_distances_bit_exact(native, oracle, small_dot):
 
 @pytest.mark.parametrize("chunk", [16, 32])
 def test_overflow_tightening_is_exact(native, oracle, small_dot, chunk):
-    """A tiny candidate capacity forces the tightening loop; results unchanged."""
+    """A tiny candidate capacity overflows every list: the device-side rescan
+    (k'-th stored key as the new threshold) leaves the results unchanged."""
     ix, db, q = small_dot
     n = _nat(native, ix)
     n.set_tuning(128, 0, 0, chunk)   # no seed pass: every candidate is emitted -> overflow
@@ -206,10 +207,10 @@ def test_scan_chunks_match_oracle(native, oracle, small_l2, chunk):
 
 def test_final_select_refinement_and_fallback(native, oracle):
     """No seed threshold, so every scanned datapoint is a candidate (n well
-    above the wave select's 512-key buffer): its histogram refinement runs for
+    above the rank select's 256-key buffer): its histogram refinement runs for
     every query, and for queries next to a block of 1200 identical datapoints
-    one distance value holds > 512 keys, which sends them to the block-kernel
-    fallback.  Both must equal the ideal oracle."""
+    one distance value holds > 256 keys, which sends them to the exact radix
+    select over whole keys.  Both must equal the ideal oracle."""
     from scann_amd import index_builder, synthetic
     db = synthetic.mixture(3000, 16, 8, 0.9, 7)
     db[:1200] = db[0]
@@ -231,3 +232,55 @@ def test_final_select_refinement_and_fallback(native, oracle):
     oi, od, oc = oracle.search(ix, q, 6, 100, 10, True, oracle.MODE_IDEAL)
     np.testing.assert_array_equal(gi, oi)
     np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+
+
+@pytest.mark.parametrize("pre_nn", [300, 2000])
+def test_large_kprime_block_select(native, oracle, small_dot, pre_nn):
+    """k' above the rank kernel's 256 keys (the block select kernel), up to
+    the supported maximum 2048 (ADVICE: a case near k' max)."""
+    ix, db, q = small_dot
+    n = _nat(native, ix)
+    gi, gd, gc = n.search_pre_reorder(q, 24, pre_nn)
+    oi, od, oc = oracle.search_pre_reorder(ix, q, 24, pre_nn, oracle.MODE_IDEAL)
+    np.testing.assert_array_equal(gc, oc)
+    np.testing.assert_array_equal(gi, oi)
+    np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+    gi, gd, gc = n.search_batched(q, 24, pre_nn, 10, True)
+    oi, od, oc = oracle.search(ix, q, 24, pre_nn, 10, True, oracle.MODE_IDEAL)
+    np.testing.assert_array_equal(gi, oi)
+    np.testing.assert_allclose(gd, od, rtol=RTOL)
+
+
+def test_overflow_rescan_in_block_select(native, oracle, small_dot):
+    """k' = 300 with a 600-key list and no seed threshold: every list
+    overflows and the block select kernel rescans it on the device."""
+    ix, db, q = small_dot
+    n = _nat(native, ix)
+    n.set_tuning(600, 0, 0, 32)
+    n.set_profiling(True)
+    gi, gd, gc = n.search_pre_reorder(q, 48, 300)
+    assert n.timings()["overflow_retries"] >= 1
+    oi, od, oc = oracle.search_pre_reorder(ix, q, 48, 300, oracle.MODE_IDEAL)
+    np.testing.assert_array_equal(gi, oi)
+    np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+
+
+def test_device_entry_point_is_stream_ordered(native, oracle, small_dot):
+    """search_batched_device returns with the work enqueued on torch's
+    current stream (no host synchronisation inside): back-to-back calls into
+    different output buffers, read after the stream, equal the oracle."""
+    import torch
+    ix, db, q = small_dot
+    n = _nat(native, ix)
+    qd = torch.from_numpy(q).cuda()
+    outs = []
+    for _ in range(3):
+        oi_ = torch.full((q.shape[0], 10), -1, dtype=torch.int32, device="cuda")
+        od_ = torch.zeros((q.shape[0], 10), dtype=torch.float32, device="cuda")
+        n.search_batched_device(qd.data_ptr(), q.shape[0], 12, 100, 10, True, oi_.data_ptr(),
+                                od_.data_ptr())
+        outs.append((oi_, od_))
+    oi, od, oc = oracle.search(ix, q, 12, 100, 10, True, oracle.MODE_IDEAL)
+    for oi_, od_ in outs:
+        np.testing.assert_array_equal(oi_.cpu().numpy().view(np.uint32), oi)
+        np.testing.assert_allclose(od_.cpu().numpy(), od, rtol=RTOL)
