@@ -1246,54 +1246,68 @@ __device__ __forceinline__ v16i TileMfma(const uint32_t* codes, const v4i (&b)[K
 }
 
 // ---------------------------------------------------------------------------
-// The scan kernel: one wave per workgroup, every wave an independent
-// persistent worker with a static share of the work (no dequeue atomics --
-// a returning device-scope atomic costs microseconds under this load -- no
-// workgroup barriers, no LUT staging).
+// The scan kernel: one workgroup of kScanWaves waves per CU (3 per SIMD), the
+// CU's waves sharing a static share of the work and balancing it among
+// themselves through LDS atomics (a returning device-scope atomic costs
+// microseconds under this load; an LDS atomic ~100 cycles).
 //
-// Work items (leaf, 32-query tile of that leaf, chunk of <= chunk_tiles
-// 32-datapoint tiles) are listed in 8 groups of consecutive leaves with equal
-// MFMA work, one per XCD group (blockIdx % 8 share an XCD under the observed
-// round-robin placement; speed only, never correctness), so a leaf's query
-// tiles run on one XCD and re-read the leaf's codes from that XCD's L2.  The
-// worklist kernel cuts each group's tiles into equal contiguous shares, one
-// per wave of the group (wave_start): a share may begin and end inside an
-// item.  Each item's descriptor and lane record are loaded one item ahead.
+// Work items (leaf, 32-query tile of that leaf, chunk of tiles) are listed in
+// 8 groups of consecutive leaves with equal MFMA work, one per XCD group
+// (blockIdx % 8 share an XCD under the observed round-robin placement; speed
+// only, never correctness), so a leaf's query tiles run on one XCD and re-read
+// the leaf's codes from that XCD's L2.  The worklist kernel cuts each group's
+// tiles into equal contiguous shares, one per workgroup (wave_start); a share
+// may begin and end inside an item.  Wave 0 lists the share's segments (item,
+// tile range) in LDS; each wave claims a segment, loads its B fragments once
+// and takes the segment's tiles two at a time from the segment's LDS counter
+// (one pair claimed ahead); a wave with no unclaimed segment left joins the
+// segment with the most tiles left.  Every wave therefore works until the
+// CU's share is done, whatever its tiles' hit rates and setup costs.
 //
-// Per item: lane (c, h) takes its query slot's record (query, sum limit,
+// Per segment: lane (c, h) takes its query slot's record (query, sum limit,
 // bias; written by the seed kernel), loads the int8 LUT rows 2s+h, s < K, of
-// query c into K registers (the MFMA B fragments for the whole item); then
-// for each tile K x MFMA i32_32x32x32_i8 with A = one-hot codes (row =
-// datapoint, 16 bytes per lane-half = one block's 16 centers) gives
-// S[dp][q] = sum_b LUT_q[b][code(dp, b)] exactly (|S| <= 127*B).  A datapoint
-// can only pass when S <= amax_q (the largest sum whose distance can pass the
-// query's threshold; d is monotone in S); a lane whose 16-sum minimum passes
-// appends its sums (packed int16) and a tag to the wave's LDS hit list;
-// drain() runs the per-element test, the distance
+// query c into K registers (the MFMA B fragments); then for each tile K x MFMA
+// i32_32x32x32_i8 with A = one-hot codes (row = datapoint, 16 bytes per
+// lane-half = one block's 16 centers) gives S[dp][q] = sum_b LUT_q[b][code(dp,
+// b)] exactly (|S| <= 127*B).  A datapoint can only pass when S <= amax_q (the
+// largest sum whose distance can pass the query's threshold; d is monotone in
+// S); a lane whose 16-sum minimum passes appends its sums (packed int16) and a
+// tag to the wave's LDS hit list; drain() runs the per-element test, the
+// distance
 //     d = fl(fl(float(S) * inv_q) + bias_{q,leaf})
 // and the key test (ordered(d) << 32 | tie) <= threshold key lane-parallel
-// over the hits, and stages the item's survivors in LDS: one global atomic per
-// query per item reserves their list slots (issued at the item's end, its
-// result consumed at the next item's start, behind that item's loads).
+// over the hits, and stages the segment's survivors in LDS: one global atomic
+// per query per segment reserves their list slots (issued at the segment's
+// end, its result consumed after the next segment's first tile).
 // ABL = 4: timing ablation without the epilogue (results invalid).
 // ---------------------------------------------------------------------------
 
 constexpr int kHitsPerWave = 64;   // a tile adds at most one hit per lane
-constexpr int kItemKeys = 256;   // survivors one work item stages in LDS
+constexpr int kItemKeys = 256;     // survivors one segment stages in LDS
+constexpr int kMaxSegs = 1024;     // share segments listed per round
+constexpr uint32_t kStealMin = 3;  // tiles left for a second wave to join a segment
+
+// Waves per scan workgroup: 3 per SIMD (168 VGPRs) up to K = 25; 2 per SIMD
+// above (the K B-fragment registers).
+#ifndef SMX_SCAN_WAVES
+#define SMX_SCAN_WAVES 12
+#endif
+template <int K>
+constexpr int ScanWaves() { return K <= 25 ? SMX_SCAN_WAVES : 8; }
 
 // Diagnostic stamps (ABL & 8; a separate buffer that nothing else reads):
-// per item {hw_id, xcc_id << 32 | item, realtime, memtime at the item's
-// start, after its setup, after its tiles, after its flush,
-// tiles | hit lanes << 16 | survivors << 40}.
-__device__ __forceinline__ void StampItem(const ScanArgs& a, uint32_t item, uint64_t rt,
-                                          uint64_t t0, uint64_t t1, uint64_t t2, uint64_t t3,
-                                          uint64_t tiles) {
+// per segment {hw_id | worker << 32, xcc_id << 32 | item, realtime, memtime at
+// the segment's start, after its setup, after its tiles, after its flush,
+// tiles | hit lanes << 16 | survivors << 40}; worker = block * waves + wave.
+__device__ __forceinline__ void StampItem(const ScanArgs& a, uint32_t worker, uint32_t item,
+                                          uint64_t rt, uint64_t t0, uint64_t t1, uint64_t t2,
+                                          uint64_t t3, uint64_t tiles) {
   const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID
   const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (15 << 11));  // HW_REG_XCC_ID
   const uint32_t slot = atomicAdd(a.stamp_count, 1u);
   if (slot < a.stamp_cap) {
     unsigned long long* p = a.stamps + size_t(slot) * 8;
-    p[0] = hw | (uint64_t(blockIdx.x) << 32);
+    p[0] = hw | (uint64_t(worker) << 32);
     p[1] = (uint64_t(xcc) << 32) | item;
     p[2] = rt;
     p[3] = t0;
@@ -1304,7 +1318,7 @@ __device__ __forceinline__ void StampItem(const ScanArgs& a, uint32_t item, uint
   }
 }
 
-// The query parameters of an item's 32 slots, in LDS for the drain.
+// The query parameters of a segment's 32 slots, in LDS for the drain.
 struct QParam {
   uint32_t qid;
   int32_t amax;
@@ -1313,243 +1327,388 @@ struct QParam {
   uint64_t tau;
 };
 
-#ifndef SMX_SCAN_WAVES_PER_SIMD
-#define SMX_SCAN_WAVES_PER_SIMD 3
-#endif
+// A wave's own LDS: hit list, survivor stage (double buffered: a segment's
+// survivors are copied to the lists during the next segment), per-slot counts.
+struct ScanWaveLds {
+  uint4 hsum[2 * kHitsPerWave][2];   // 16 sums as int16 pairs
+  uint32_t hmeta[2 * kHitsPerWave];  // tile << 6 | lane
+  uint64_t kbuf[2][kItemKeys];
+  uint8_t kslot[2][kItemKeys];
+  uint32_t s_kn[2];
+  uint32_t qcnt[32], q_slot[32], qrun[32], prev_qid[32];
+  QParam qp[32];
+};
+
+// Wave 0 of a scan workgroup: the next segments of the share (item, first
+// tile, end tile) into the LDS table, 64 items per step (a prefix of their
+// tiles), at most kMaxSegs; the share's remainder stays in s_sw / s_su.  Out
+// of line: it runs once per round, and inlined its shuffle addresses would
+// stay live (and spill) through the tile loop.
+__device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32_t& sj,
+                                          uint32_t* s_item, uint32_t* s_end, uint32_t* s_next,
+                                          uint32_t& s_sw, uint32_t& s_su, uint32_t& s_nseg,
+                                          uint32_t& s_claim) {
+  uint32_t sw = s_sw, su = s_su, nseg = 0;
+  while (su > 0 && nseg + 64 <= uint32_t(kMaxSegs)) {
+    const uint32_t idx = sw + uint32_t(lane);
+    const WorkItem it = a.work[min(idx, a.num_items - 1)];
+    const uint32_t j0 = (lane == 0 && sj) ? sj : it.j0;
+    const uint32_t t = it.jend > j0 ? min(it.jend - j0, su) : 0u;
+    uint32_t incl = t;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = uint32_t(__shfl_up(int(incl), off));
+      if (lane >= off) incl += y;
+    }
+    const uint32_t excl = incl - t;
+    const bool used = excl < su;   // a prefix of the lanes
+    const bool take = used && t > 0;
+    const uint64_t bt = __ballot(take);
+    if (take) {
+      const uint32_t pos = nseg + uint32_t(__popcll(bt & ((1ull << lane) - 1ull)));
+      s_item[pos] = idx;
+      s_next[pos] = j0;
+      s_end[pos] = j0 + min(t, su - excl);
+    }
+    const uint32_t nused = uint32_t(__popcll(__ballot(used)));
+    const uint32_t last_incl = uint32_t(__shfl(int(incl), int(nused) - 1));
+    sw += nused;
+    su -= min(su, last_incl);
+    nseg += uint32_t(__popcll(bt));
+    sj = 0;
+  }
+  if (lane == 0) {
+    s_sw = sw;
+    s_su = su;
+    s_nseg = nseg;
+    s_claim = 0;
+  }
+}
+
 template <int K, int ABL = 0>
-__global__ void __launch_bounds__(64, (K <= 25 ? SMX_SCAN_WAVES_PER_SIMD : 2))
-    lut16_scan_kernel(ScanArgs a) {
+__global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(ScanArgs a) {
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
   constexpr int W = 4 * NW;
-  constexpr int Q = 32, HW = 2 * kHitsPerWave, KB = kItemKeys;
+  constexpr int Q = 32, KB = kItemKeys, NWAVES = ScanWaves<K>();
   constexpr int R = 3;   // one-hot reads in flight ahead of their MFMA
-  __shared__ uint4 hsum[HW][2];     // 16 sums as int16 pairs
-  __shared__ uint32_t hmeta[HW];    // tile << 6 | lane
-  // survivors of an item (all its queries) and their query slots, double
-  // buffered: an item's are copied to the lists during the next item
-  __shared__ uint64_t kbuf[2][KB];
-  __shared__ uint8_t kslot[2][KB];
-  __shared__ uint32_t s_kn[2];
-  __shared__ uint32_t qcnt[Q], q_slot[Q], qrun[Q], prev_qid[Q];
-  __shared__ QParam qp[Q];
+  __shared__ ScanWaveLds wl_[NWAVES];
   __shared__ v4i oh_tab[16];
-  const int lane = threadIdx.x;
+  __shared__ uint32_t s_item[kMaxSegs], s_end[kMaxSegs], s_next[kMaxSegs];
+  __shared__ uint32_t s_nseg, s_claim, s_sw, s_su;
+  // wave-uniform values in scalar registers (the B fragments need the VGPRs)
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   const int c = lane & 31;
   const int h = lane >> 5;
-  if (lane < 16) {
+  ScanWaveLds& wl = wl_[wv];
+  if (threadIdx.x < 16) {
     v4i t = {0, 0, 0, 0};
-    t[lane >> 2] = int(1u << (8 * (lane & 3)));
-    oh_tab[lane] = t;
+    t[threadIdx.x >> 2] = int(1u << (8 * (threadIdx.x & 3)));
+    oh_tab[threadIdx.x] = t;
   }
-  uint64_t st_rt = 0, st_t0 = 0, st_t1 = 0, st_t2 = 0;
-  uint32_t st_hits = 0, st_surv = 0;
-  const WorkItem* work = a.work;
-  // this wave's static share: `units` tiles from tile j of item w on
+  const uint32_t worker = blockIdx.x * NWAVES + wv;
+  const WorkItem* __restrict__ work = a.work;
+  // this workgroup's share: `units` tiles from tile jfirst of item w on
   const uint4 ws = a.wave_start[blockIdx.x];
-  uint32_t w = __builtin_amdgcn_readfirstlane(ws.x);
-  uint32_t jfirst = __builtin_amdgcn_readfirstlane(ws.y);
-  uint32_t units = __builtin_amdgcn_readfirstlane(ws.z);
-  WorkItem cur = work[w];
-  ItemLane cl = a.lanes[size_t(w) * Q + c];
-  bool pending = false;   // the previous item's survivors await their copy
+  if (threadIdx.x == 0) {
+    s_sw = ws.x;
+    s_su = ws.z;
+  }
+  uint32_t sj = ws.y;   // the share's first tile inside its first item
+  bool pending = false;   // the previous segment's survivors await their copy
   uint32_t slot = 0;      // that copy's first list slot (lanes < 32)
-  uint32_t par = 0;       // this item's survivor buffer
-  // the previous item's survivors to their queries' lists: each key's place =
-  // its query's reserved first slot (the returned value of the item-end
-  // atomic, waited for only here) + a running count
+  uint32_t par = 0;       // this segment's survivor buffer
+  // the previous segment's survivors to their queries' lists: each key's
+  // place = its query's reserved first slot (the returned value of the
+  // segment-end atomic, waited for only here) + a running count
   auto copy_prev = [&]() {
     const uint32_t pp = par ^ 1u;
     if (lane < Q) {
-      q_slot[lane] = slot;
-      qrun[lane] = 0;
+      wl.q_slot[lane] = slot;
+      wl.qrun[lane] = 0;
     }
     WaveLdsSync();
-    const uint32_t kn = min(s_kn[pp], uint32_t(KB));
+    const uint32_t kn = min(wl.s_kn[pp], uint32_t(KB));
     for (uint32_t e = uint32_t(lane); e < kn; e += 64) {
-      const uint32_t qs = kslot[pp][e];
-      const uint32_t sl = q_slot[qs] + atomicAdd(&qrun[qs], 1u);
-      if (sl < a.cap) a.cand[size_t(prev_qid[qs]) * a.cap + sl] = kbuf[pp][e];
+      const uint32_t qs = wl.kslot[pp][e];
+      const uint32_t sl = wl.q_slot[qs] + atomicAdd(&wl.qrun[qs], 1u);
+      if (sl < a.cap) a.cand[size_t(wl.prev_qid[qs]) * a.cap + sl] = wl.kbuf[pp][e];
     }
     WaveLdsSync();
     pending = false;
   };
-  while (units > 0) {
-    if (ABL & 8) {
-      st_rt = __builtin_amdgcn_s_memrealtime();
-      st_t0 = __builtin_amdgcn_s_memtime();
-      st_hits = st_surv = 0;
-    }
-    // this item's B fragments (LUT rows 2s+h of query c) and first code tile
-    // go out first; the previous item's slot atomics (older) are waited for
-    // below without waiting for these
-    const uint32_t n = cur.n;
-    const uint32_t j0 = jfirst ? jfirst : cur.j0;
-    const uint32_t jend = min(cur.jend, j0 + units);
-    v4i b[K];
-    uint32_t codes[NW] = {};
-    const uint8_t* tb = a.tiles + cur.tile_off * 64ull * W + size_t(lane) * W;
-    {
-      const v4i* src = reinterpret_cast<const v4i*>(a.lut) + size_t(cl.qid) * 2 * K + h;
-#pragma unroll
-      for (int s = 0; s < K; ++s) b[s] = src[2 * s];
-      if (j0 < jend) LoadCodes<K>(tb + size_t(j0) * 64 * W, codes);   // (empty leaf: no tile)
-    }
-    // the next item's descriptor and record, in flight during this item
-    const uint32_t wn = min(w + 1, a.num_items - 1);
-    const WorkItem nxt = work[wn];
-    const ItemLane nrec = a.lanes[size_t(wn) * Q + c];
-    const int leaf = int(cur.leaf);
-    const uint64_t moff = cur.member_off;
-    const int amax = cl.amax;
-    if (lane < Q) {
-      QParam v;
-      v.qid = cl.qid;
-      v.amax = cl.amax;
-      v.bias = cl.bias;
-      v.inv = cl.inv;
-      v.tau = cl.tau;
-      qp[lane] = v;
-      qcnt[lane] = 0;
-    }
-    if (lane == 0) s_kn[par] = 0;
-    units -= jend - j0;
-    jfirst = 0;
-    WaveLdsSync();
-    uint32_t whits = 0;   // wave-uniform
+  // one LDS claim of two tiles of segment `sg` (lane 0; broadcast at use)
+  auto claim2 = [&](uint32_t sg) -> uint32_t {
+    uint32_t v = 0;
+    if (lane == 0) v = atomicAdd(&s_next[sg], 2u);
+    return v;
+  };
 
-    // lane k of the wave takes hits k, k+64: per-element test, key, exact
-    // threshold compare, append to the query's LDS stage
-    auto drain = [&]() {
-      for (uint32_t hidx = uint32_t(lane); hidx < whits; hidx += 64) {
-        const uint32_t meta = hmeta[hidx];
-        const uint32_t jj = meta >> 6;
-        const int cc = int(meta & 31u), hh = int((meta >> 5) & 1u);
-        const uint4 s0 = hsum[hidx][0], s1 = hsum[hidx][1];
-        const uint32_t sw[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-        const QParam pq = qp[cc];
-        const int am = pq.amax;
-        const float iv = pq.inv, bs = pq.bias;
-        const uint64_t TT = pq.tau;
-        const uint32_t qq = pq.qid;
+  for (;;) {   // rounds of at most kMaxSegs segments (block-uniform)
+    __syncthreads();   // s_sw / s_su / the segment table are free
+    if (wv == 0) ListSegments(a, lane, sj, s_item, s_end, s_next, s_sw, s_su, s_nseg, s_claim);
+    __syncthreads();
+    const uint32_t nseg = s_nseg;
+    if (nseg == 0) break;
+    // claim-ahead segment (a reservation: joiners may still take its tiles)
+    uint32_t sg_next = 0;
+    if (lane == 0) sg_next = atomicAdd(&s_claim, 1u);
+    // the claimed-ahead segment's item and query ids, loaded during the
+    // segment before it: the B-fragment addresses need the query id, so
+    // without this a segment's setup is two dependent global latencies
+    uint32_t pf_seg = ~0u, pf_item = 0, pf_qid = 0;
+    for (;;) {
+      uint32_t sg = __builtin_amdgcn_readfirstlane(sg_next);
+      if (sg >= nseg) {
+        // no unclaimed segment: join the last-claimed one (most tiles left,
+        // segments are claimed in order) with >= kStealMin tiles left
+        int found = -1;
+        for (int base = int(nseg) - 64; found < 0 && base > -64; base -= 64) {
+          const int i = base + lane;
+          bool ok = false;
+          if (i >= 0) {
+            const uint32_t e = s_end[i], nx = s_next[i];
+            ok = nx < e && e - nx >= kStealMin;
+          }
+          const uint64_t bal = __ballot(ok);
+          if (bal) found = base + 63 - int(__clzll(bal));
+        }
+        if (found < 0) break;
+        sg = uint32_t(__builtin_amdgcn_readfirstlane(found));
+      } else if (lane == 0) {
+        sg_next = atomicAdd(&s_claim, 1u);   // the next one, claimed ahead
+      }
+      const uint32_t end = __builtin_amdgcn_readfirstlane(s_end[sg]);
+      uint32_t j = __builtin_amdgcn_readfirstlane(claim2(sg));
+      if (j >= end) continue;   // (joined too late)
+      uint64_t st_rt = 0, st_t0 = 0, st_t1 = 0, st_t2 = 0;
+      uint32_t st_hits = 0, st_surv = 0;
+      if (ABL & 8) {
+        st_rt = __builtin_amdgcn_s_memrealtime();
+        st_t0 = __builtin_amdgcn_s_memtime();
+      }
+      uint32_t item, qid;
+      if (sg == pf_seg) {
+        item = pf_item;
+        qid = pf_qid;
+      } else {
+        item = __builtin_amdgcn_readfirstlane(s_item[sg]);
+        qid = a.lanes[size_t(item) * Q + c].qid;
+      }
+      const WorkItem cur = work[item];
+      {
+        const uint32_t sn = __builtin_amdgcn_readfirstlane(sg_next);
+        if (sn < nseg) {
+          pf_seg = sn;
+          pf_item = __builtin_amdgcn_readfirstlane(s_item[sn]);
+          pf_qid = a.lanes[size_t(pf_item) * Q + c].qid;
+        } else {
+          pf_seg = ~0u;
+        }
+      }
+      const ItemLane cl = a.lanes[size_t(item) * Q + c];
+      // this segment's B fragments (LUT rows 2s+h of query c) and first tile
+      const uint32_t n = cur.n;
+      v4i b[K];
+      uint32_t codes[NW] = {};
+      const uint8_t* tb = a.tiles + cur.tile_off * 64ull * W + size_t(lane) * W;
+      const v4i* bsrc = reinterpret_cast<const v4i*>(a.lut) + size_t(qid) * 2 * K + h;
+      auto load_b = [&]() {
+#pragma unroll
+        for (int s2 = 0; s2 < K; ++s2) b[s2] = bsrc[2 * s2];
+      };
+      load_b();
+      LoadCodes<K>(tb + size_t(j) * 64 * W, codes);
+      const int leaf = int(cur.leaf);
+      const uint64_t moff = cur.member_off;
+      const int amax = cl.amax;
+      if (lane < Q) {
+        QParam v;
+        v.qid = cl.qid;
+        v.amax = cl.amax;
+        v.bias = cl.bias;
+        v.inv = cl.inv;
+        v.tau = cl.tau;
+        wl.qp[lane] = v;
+        wl.qcnt[lane] = 0;
+      }
+      if (lane == 0) wl.s_kn[par] = 0;
+      WaveLdsSync();
+      uint32_t whits = 0;   // wave-uniform
+
+      // lane k of the wave takes hits k, k+64: per-element test, key, exact
+      // threshold compare, append to the query's LDS stage
+      auto drain = [&]() {
+        for (uint32_t hidx = uint32_t(lane); hidx < whits; hidx += 64) {
+          const uint32_t meta = wl.hmeta[hidx];
+          const uint32_t jj = meta >> 6;
+          const int cc = int(meta & 31u), hh = int((meta >> 5) & 1u);
+          const uint4 s0 = wl.hsum[hidx][0], s1 = wl.hsum[hidx][1];
+          const uint32_t sw8[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+          const QParam pq = wl.qp[cc];
+          const int am = pq.amax;
+          const float iv = pq.inv, bs = pq.bias;
+          const uint64_t TT = pq.tau;
+          const uint32_t qq = pq.qid;
 #pragma unroll 1
-        for (int i = 0; i < 16; ++i) {
-          const int sum = int(int16_t(uint16_t(sw[i >> 1] >> (16 * (i & 1)))));
-          if (sum <= am) {
-            const uint32_t dp = jj * kDpPerTile + (i & 3) + 8 * (i >> 2) + 4 * hh;
-            const float d = DistOf(sum, iv, bs);
-            const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp)
-                                             : a.members[moff + dp];
-            const uint64_t key = (uint64_t(OrderedBits(d)) << 32) | tie;
-            if (key <= TT) {
-              const uint32_t p = atomicAdd(&s_kn[par], 1u);
-              if (p < uint32_t(KB)) {
-                kbuf[par][p] = key;
-                kslot[par][p] = uint8_t(cc);
-                atomicAdd(&qcnt[cc], 1u);
-              } else {  // item buffer full (rare): straight to the global list
-                const uint32_t gs = atomicAdd(&a.cand_count[size_t(qq) * kCounterStride], 1u);
-                if (gs < a.cap) a.cand[size_t(qq) * a.cap + gs] = key;
+          for (int i = 0; i < 16; ++i) {
+            const int sum = int(int16_t(uint16_t(sw8[i >> 1] >> (16 * (i & 1)))));
+            if (sum <= am) {
+              const uint32_t dp = jj * kDpPerTile + (i & 3) + 8 * (i >> 2) + 4 * hh;
+              const float d = DistOf(sum, iv, bs);
+              const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp)
+                                               : a.members[moff + dp];
+              const uint64_t key = (uint64_t(OrderedBits(d)) << 32) | tie;
+              if (key <= TT) {
+                const uint32_t p = atomicAdd(&wl.s_kn[par], 1u);
+                if (p < uint32_t(KB)) {
+                  wl.kbuf[par][p] = key;
+                  wl.kslot[par][p] = uint8_t(cc);
+                  atomicAdd(&wl.qcnt[cc], 1u);
+                } else {  // stage full (rare): straight to the global list
+                  const uint32_t gs = atomicAdd(&a.cand_count[size_t(qq) * kCounterStride], 1u);
+                  if (gs < a.cap) a.cand[size_t(qq) * a.cap + gs] = key;
+                }
               }
             }
           }
         }
-      }
-      WaveLdsSync();   // the hit list is rewritten next
-    };
+        WaveLdsSync();   // the hit list is rewritten next
+      };
 
-    // one tile: K MFMAs, then the hit test (and the drain when the list is
-    // over half full or after the chunk's last tile)
-    auto tile = [&](const uint32_t (&cd)[NW], uint32_t j) {
-      v16i acc = TileMfma<K, R>(cd, b, oh_tab);
-      if (ABL & 4) {
-        int x = acc[0];
+      // one tile: K MFMAs, then the hit test
+      auto tile = [&](const uint32_t (&cd)[NW], uint32_t jt) {
+        v16i acc = TileMfma<K, R>(cd, b, oh_tab);
+        if (ABL & 4) {
+          int x = acc[0];
 #pragma unroll
-        for (int i = 1; i < 16; ++i) x ^= acc[i];
-        if (x == 0x7fffffff) a.cand_count[0] = x;
-        return;
-      }
-      const uint32_t rows_left = n - j * kDpPerTile;
-      if (rows_left < uint32_t(kDpPerTile)) {  // last tile of the leaf
+          for (int i = 1; i < 16; ++i) x ^= acc[i];
+          if (x == 0x7fffffff) a.cand_count[0] = x;
+          return;
+        }
+        const uint32_t rows_left = n - jt * kDpPerTile;
+        if (rows_left < uint32_t(kDpPerTile)) {  // last tile of the leaf
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const uint32_t row = (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (row >= rows_left) acc[i] = 0x7FFF;
+          for (int i = 0; i < 16; ++i) {
+            const uint32_t row = (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (row >= rows_left) acc[i] = 0x7FFF;
+          }
+        }
+        int m = min(min(acc[0], acc[1]), acc[2]);
+#pragma unroll
+        for (int i = 3; i < 15; i += 2) m = min(min(m, acc[i]), acc[i + 1]);
+        m = min(m, acc[15]);
+        const bool hit = m <= amax;
+        const uint64_t hb = __builtin_amdgcn_ballot_w64(hit);
+        if (hb) {
+          // whits <= 64 here and a tile adds at most 64: the list (128)
+          // always has room, so the sums are dead before any drain
+          const uint32_t nh = uint32_t(__popcll(hb));
+          if (hit) {
+            const uint32_t hs =
+                whits + __builtin_amdgcn_mbcnt_hi(uint32_t(hb >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo(uint32_t(hb), 0u));
+            uint32_t pk[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              pk[k] = (uint32_t(acc[2 * k]) & 0xFFFFu) | (uint32_t(acc[2 * k + 1]) << 16);
+            wl.hsum[hs][0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            wl.hsum[hs][1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+            wl.hmeta[hs] = (jt << 6) | uint32_t(lane);
+          }
+          whits += nh;
+          if (ABL & 8) st_hits += nh;
+          WaveLdsSync();
+        }
+      };
+      // a hit list over half full is drained between tiles with the B
+      // fragments dead (reloaded after, from L2): the drain's registers
+      // then never compete with them (rare: ~1 hit lane per tile)
+      auto drain_mid = [&]() {
+        if (whits > 64u) {
+          drain();
+          whits = 0;
+          load_b();
+        }
+      };
+
+      if (ABL & 8) st_t1 = __builtin_amdgcn_s_memtime();
+      // the tiles this wave takes, a claimed pair at a time with the next
+      // pair claimed ahead; two code buffers in turn (the load of the next
+      // tile is in flight while this one computes; a rotating copy would
+      // force a wait for it at the copy)
+      uint32_t pe = min(j + 2, end);        // the current pair [.., pe)
+      uint32_t na_raw = claim2(sg);          // the next pair (lane 0)
+      bool na_known = false;
+      uint32_t na = end;
+      auto next_tile = [&](uint32_t t, uint32_t& tn) -> bool {
+        if (t + 1 < pe) {
+          tn = t + 1;
+          return true;
+        }
+        if (!na_known) {
+          na = __builtin_amdgcn_readfirstlane(na_raw);
+          na_known = true;
+        }
+        if (na >= end) return false;
+        tn = na;
+        return true;
+      };
+      auto advance = [&](uint32_t t, uint32_t tn) {
+        if (!(t + 1 < pe)) {   // moved into the pair claimed ahead: claim another
+          pe = min(tn + 2, end);
+          na_raw = claim2(sg);
+          na_known = false;
+        }
+      };
+      uint32_t tiles_done = 0;
+      {
+        uint32_t cb[NW];
+        uint32_t t = j, tn = 0;
+        for (;;) {
+          bool more = next_tile(t, tn);
+          if (more) LoadCodes<K>(tb + size_t(tn) * 64 * W, cb);
+          tile(codes, t);
+          ++tiles_done;
+          if (pending) copy_prev();   // after the segment's first tile: the atomic has returned
+          if (!more) break;
+          drain_mid();
+          advance(t, tn);
+          t = tn;
+          more = next_tile(t, tn);
+          if (more) LoadCodes<K>(tb + size_t(tn) * 64 * W, codes);
+          tile(cb, t);
+          ++tiles_done;
+          if (!more) break;
+          drain_mid();
+          advance(t, tn);
+          t = tn;
         }
       }
-      int m = min(min(acc[0], acc[1]), acc[2]);
-#pragma unroll
-      for (int i = 3; i < 15; i += 2) m = min(min(m, acc[i]), acc[i + 1]);
-      m = min(m, acc[15]);
-      const bool hit = m <= amax;
-      const uint64_t hb = __builtin_amdgcn_ballot_w64(hit);
-      if (hb) {
-        // whits <= 64 here and a tile adds at most 64: the list (HW = 128)
-        // always has room, so the sums are dead before any drain
-        const uint32_t nh = uint32_t(__popcll(hb));
-        if (hit) {
-          const uint32_t hs =
-              whits + __builtin_amdgcn_mbcnt_hi(uint32_t(hb >> 32),
-                                                __builtin_amdgcn_mbcnt_lo(uint32_t(hb), 0u));
-          uint32_t pk[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k)
-            pk[k] = (uint32_t(acc[2 * k]) & 0xFFFFu) | (uint32_t(acc[2 * k + 1]) << 16);
-          hsum[hs][0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-          hsum[hs][1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
-          hmeta[hs] = (j << 6) | uint32_t(lane);
-        }
-        whits += nh;
-        if (ABL & 8) st_hits += nh;
-        WaveLdsSync();
-      }
-      if (whits > 64u || (j + 1 == jend && whits)) {
+      if (whits) {
         drain();
         whits = 0;
       }
-    };
-
-    if (ABL & 8) st_t1 = __builtin_amdgcn_s_memtime();
-    // tiles j0 .. jend-1, two code buffers in turn: the load of tile j+1 is
-    // in flight while tile j computes (a rotating copy would force a wait
-    // for it at the copy); prefetches are clamped to the chunk's last tile so
-    // no exec branch sits around a load
-    if (j0 < jend) {
-      const uint32_t jl = jend - 1;
-      uint32_t cb[NW];
-      for (uint32_t j = j0;; j += 2) {
-        LoadCodes<K>(tb + size_t(min(j + 1, jl)) * 64 * W, cb);
-        tile(codes, j);
-        if (pending) copy_prev();   // after the item's first tile: the atomic has returned
-        if (j + 1 >= jend) break;
-        LoadCodes<K>(tb + size_t(min(j + 2, jl)) * 64 * W, codes);
-        tile(cb, j + 1);
-        if (j + 2 >= jend) break;
+      if (ABL & 8) st_t2 = __builtin_amdgcn_s_memtime();
+      if (ABL & 8) {
+        uint32_t sv = lane < Q ? wl.qcnt[lane] : 0u;
+        for (int off = 32; off > 0; off >>= 1) sv += uint32_t(__shfl_xor(int(sv), off));
+        st_surv = sv;
       }
+      // one list-slot atomic per query slot with survivors; the copy waits
+      // for it after the next segment's first tile
+      if (lane < Q) {
+        const uint32_t m = wl.qcnt[lane];
+        slot = m ? atomicAdd(&a.cand_count[size_t(qid) * kCounterStride], m) : 0u;
+        wl.prev_qid[lane] = qid;
+      }
+      pending = true;
+      par ^= 1u;
+      if ((ABL & 8) && lane == 0)
+        StampItem(a, worker, item, st_rt, st_t0, st_t1, st_t2, __builtin_amdgcn_s_memtime(),
+                  uint64_t(tiles_done) | (uint64_t(st_hits) << 16) | (uint64_t(st_surv) << 40));
     }
-    if (pending) copy_prev();   // (an item without tiles)
-    if (ABL & 8) st_t2 = __builtin_amdgcn_s_memtime();
-    if (ABL & 8) {
-      uint32_t sv = lane < Q ? qcnt[lane] : 0u;
-      for (int off = 32; off > 0; off >>= 1) sv += uint32_t(__shfl_xor(int(sv), off));
-      st_surv = sv;
-    }
-    // one list-slot atomic per query slot with survivors; the copy waits for
-    // it at the next item's start (after that item's loads are issued)
-    if (lane < Q) {
-      const uint32_t m = qcnt[lane];
-      slot = m ? atomicAdd(&a.cand_count[size_t(cl.qid) * kCounterStride], m) : 0u;
-      prev_qid[lane] = cl.qid;
-    }
-    pending = true;
-    par ^= 1u;
-    if ((ABL & 8) && lane == 0)
-      StampItem(a, w, st_rt, st_t0, st_t1, st_t2, __builtin_amdgcn_s_memtime(),
-                uint64_t(jend - j0) | (uint64_t(st_hits) << 16) | (uint64_t(st_surv) << 40));
-    cur = nxt;
-    cl = nrec;
-    ++w;
+    if (pending) copy_prev();
   }
-  if (pending) copy_prev();
 }
 
 // One-query variant for the stage entry point: raw sums of one leaf.
@@ -2427,14 +2586,17 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
   return hipGetLastError();
 }
 
-#define SMX_SCAN_CASE(KV)                                                          \
-  case KV:                                                                         \
-    if (variant == 4)                                                              \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 4>), dim3(grid), dim3(64), 0, s, a); \
-    else if (variant == 8)                                                         \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 8>), dim3(grid), dim3(64), 0, s, a); \
-    else                                                                           \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64), 0, s, a); \
+#define SMX_SCAN_CASE(KV)                                                                  \
+  case KV:                                                                                 \
+    if (variant == 4)                                                                      \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 4>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
+                         0, s, a);                                                         \
+    else if (variant == 8)                                                                 \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 8>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
+                         0, s, a);                                                         \
+    else                                                                                   \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
+                         0, s, a);                                                         \
     break;
 
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,
@@ -2458,7 +2620,7 @@ hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int va
 #define SMX_OCC_CASE(KV)                                                                 \
   case KV:                                                                               \
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(                                 \
-        blocks, reinterpret_cast<const void*>(&lut16_scan_kernel<KV, 0>), 64, 0);
+        blocks, reinterpret_cast<const void*>(&lut16_scan_kernel<KV, 0>), 64 * ScanWaves<KV>(), 0);
 
 hipError_t ScanBlocksPerCU(const DeviceIndex& ix, int* blocks) {
   *blocks = 0;

@@ -273,11 +273,23 @@ int UploadIndex(const smx_index_desc* d, smx_index* h) {
   SMX_HIP(hipMemcpy(ix.leaf_size, size.data(), 4 * nl, hipMemcpyHostToDevice));
   SMX_HIP(hipMemcpy(ix.member_off, d->leaf_offsets, 8 * (nl + 1), hipMemcpyHostToDevice));
   if (M) SMX_HIP(hipMemcpy(ix.members, d->leaf_members, 4 * M, hipMemcpyHostToDevice));
-  // Work order: largest leaves first (their work items are the longest).
-  std::vector<uint32_t> order(nl);
-  for (int l = 0; l < nl; ++l) order[l] = uint32_t(l);
-  std::stable_sort(order.begin(), order.end(),
+  // Work order: the leaves by descending size dealt to the 8 XCD groups in a
+  // snake (0..7, 7..0, ...), each group's leaves contiguous and largest
+  // first.  The worklist cuts the order into 8 groups of equal MFMA work, so
+  // every group gets the same mix of large and small leaves (large leaves
+  // carry more queries near them and more threshold hits per tile: groups of
+  // consecutive sizes finished up to 20% apart).
+  std::vector<uint32_t> by_size(nl);
+  for (int l = 0; l < nl; ++l) by_size[l] = uint32_t(l);
+  std::stable_sort(by_size.begin(), by_size.end(),
                    [&](uint32_t a, uint32_t b) { return size[a] > size[b]; });
+  std::vector<uint32_t> order;
+  order.reserve(nl);
+  for (int g = 0; g < smx::kWorkGroups; ++g)
+    for (int p = 0; p < nl; ++p) {
+      const int r = p / smx::kWorkGroups, i = p % smx::kWorkGroups;
+      if ((r % 2 == 0 ? i : smx::kWorkGroups - 1 - i) == g) order.push_back(by_size[p]);
+    }
   SMX_HIP(hipMemcpy(ix.leaf_order, order.data(), 4 * nl, hipMemcpyHostToDevice));
   if (d->dataset)
     SMX_HIP(hipMemcpy(ix.dataset, d->dataset, sizeof(float) * size_t(d->num_datapoints) * dim,

@@ -1,4 +1,4 @@
-"""Per-item timeline of the LUT16 scan kernel (diagnostic variant 8).
+"""Per-segment timeline of the LUT16 scan kernel (diagnostic variant 8).
 
     python tools/scan_stamps.py [chunk_tiles]      (on the GPU box)
 
@@ -19,6 +19,8 @@ import torch  # noqa: E402
 
 from bench import LEAVES_TO_SEARCH, NQ, PRE_NN, FINAL_NN, build_index  # noqa: E402
 from scann_amd import _native  # noqa: E402
+
+WAVES = 12   # scan waves per workgroup (K <= 25)
 
 
 def main():
@@ -132,9 +134,10 @@ def main():
         ii = np.where(m)[0]
         j = ii[np.argmax(rt[ii])]
         wend[int(b)] = (rt[j] - rt0) / 100.0 + (t3[j] - t0[j]) / 2100.0
+    grp = (blk // WAVES) % 8   # worker = workgroup * WAVES + wave; workgroup % 8 = XCD group
     for gsel in range(8):
-        e = np.array([v for k, v in wend.items() if k % 8 == gsel])
-        hm = hits[(blk % 8 == gsel) & it].sum()
+        e = np.array([v for k, v in wend.items() if (k // WAVES) % 8 == gsel])
+        hm = hits[(grp == gsel) & it].sum()
         print(f"group {gsel}: wave end p10 {np.percentile(e, 10):.1f} p50 {np.median(e):.1f} max {e.max():.1f} us; hits {hm}")
     # per SIMD: end vs hits
     send, shits = {}, {}
@@ -146,9 +149,29 @@ def main():
     e = np.array([send[k] for k in ks]); hh = np.array([shits[k] for k in ks])
     print(f"SIMD end: p10 {np.percentile(e, 10):.1f} p50 {np.median(e):.1f} p90 {np.percentile(e, 90):.1f} max {e.max():.1f}; "
           f"corr(end, hits) {np.corrcoef(e, hh)[0, 1]:.2f}")
+    # per workgroup (CU share): end time vs its hits, segments (setups), tiles
+    wg = blk // WAVES
+    wgs = np.unique(wg[it])
+    wend_g, whits_g, wseg_g, wtil_g = [], [], [], []
+    for g_ in wgs:
+        m = (wg == g_) & it
+        ii = np.where(m)[0]
+        wend_g.append(max(wend[int(b)] for b in np.unique(blk[ii])))
+        whits_g.append(hits[ii].sum())
+        wseg_g.append(len(ii))
+        wtil_g.append(tiles[ii].sum())
+    wend_g, whits_g, wseg_g, wtil_g = map(np.array, (wend_g, whits_g, wseg_g, wtil_g))
+    print(f"workgroups {len(wgs)}: end p10 {np.percentile(wend_g, 10):.1f} p50 {np.median(wend_g):.1f} "
+          f"p90 {np.percentile(wend_g, 90):.1f} max {wend_g.max():.1f}; tiles min {wtil_g.min()} max {wtil_g.max()}; "
+          f"segments p50 {np.median(wseg_g):.0f} max {wseg_g.max()}")
+    for nm, v in (("hits", whits_g), ("segments", wseg_g), ("tiles", wtil_g)):
+        print(f"    corr(end, {nm}) {np.corrcoef(wend_g, v)[0, 1]:.2f}")
+    slow = np.argsort(wend_g)[-5:]
+    for i in slow:
+        print(f"    slow wg {wgs[i]}: end {wend_g[i]:.1f} hits {whits_g[i]} segments {wseg_g[i]} tiles {wtil_g[i]}")
     # XCC placement of the groups
     for gsel in range(8):
-        m = (blk % 8 == gsel) & it
+        m = (grp == gsel) & it
         if m.any():
             u, c = np.unique(xcc[m], return_counts=True)
             print(f"group {gsel}: xcc {dict(zip(u.tolist(), c.tolist()))}")
