@@ -1284,7 +1284,7 @@ __device__ __forceinline__ v16i TileMfma(const uint32_t* codes, const v4i (&b)[K
 
 constexpr int kHitsPerWave = 64;   // a tile adds at most one hit per lane
 constexpr int kItemKeys = 256;     // survivors one segment stages in LDS
-constexpr int kMaxSegs = 1024;     // share segments listed per round
+constexpr int kMaxSegs = 512;      // share segments listed per round
 constexpr uint32_t kStealMin = 3;  // tiles left for a second wave to join a segment
 
 // Waves per scan workgroup: 3 per SIMD (168 VGPRs) up to K = 25; 2 per SIMD
@@ -1339,15 +1339,23 @@ struct ScanWaveLds {
   QParam qp[32];
 };
 
+// A segment's item descriptor, kept in LDS: a segment's setup reads it from
+// there instead of waiting for a global load.
+struct SegDesc {
+  uint64_t tile_off;
+  uint64_t member_off;
+  uint32_t n;
+  uint32_t leaf;
+};
+
 // Wave 0 of a scan workgroup: the next segments of the share (item, first
-// tile, end tile) into the LDS table, 64 items per step (a prefix of their
-// tiles), at most kMaxSegs; the share's remainder stays in s_sw / s_su.  Out
-// of line: it runs once per round, and inlined its shuffle addresses would
-// stay live (and spill) through the tile loop.
+// tile, end tile, descriptor) into the LDS table, 64 items per step (a prefix
+// of their tiles), at most kMaxSegs; the share's remainder stays in s_sw /
+// s_su.
 __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32_t& sj,
-                                          uint32_t* s_item, uint32_t* s_end, uint32_t* s_next,
-                                          uint32_t& s_sw, uint32_t& s_su, uint32_t& s_nseg,
-                                          uint32_t& s_claim) {
+                                             uint32_t* s_item, uint32_t* s_end, uint32_t* s_next,
+                                             SegDesc* s_desc, uint32_t& s_sw, uint32_t& s_su,
+                                             uint32_t& s_nseg, uint32_t& s_claim) {
   uint32_t sw = s_sw, su = s_su, nseg = 0;
   while (su > 0 && nseg + 64 <= uint32_t(kMaxSegs)) {
     const uint32_t idx = sw + uint32_t(lane);
@@ -1368,6 +1376,12 @@ __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32
       s_item[pos] = idx;
       s_next[pos] = j0;
       s_end[pos] = j0 + min(t, su - excl);
+      SegDesc dsc;
+      dsc.tile_off = it.tile_off;
+      dsc.member_off = it.member_off;
+      dsc.n = it.n;
+      dsc.leaf = it.leaf;
+      s_desc[pos] = dsc;
     }
     const uint32_t nused = uint32_t(__popcll(__ballot(used)));
     const uint32_t last_incl = uint32_t(__shfl(int(incl), int(nused) - 1));
@@ -1393,6 +1407,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   __shared__ ScanWaveLds wl_[NWAVES];
   __shared__ v4i oh_tab[16];
   __shared__ uint32_t s_item[kMaxSegs], s_end[kMaxSegs], s_next[kMaxSegs];
+  __shared__ SegDesc s_desc[kMaxSegs];
   __shared__ uint32_t s_nseg, s_claim, s_sw, s_su;
   // wave-uniform values in scalar registers (the B fragments need the VGPRs)
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1415,6 +1430,8 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   }
   uint32_t sj = ws.y;   // the share's first tile inside its first item
   bool pending = false;   // the previous segment's survivors await their copy
+  bool flush = false;     // ... and, before that, their list-slot atomics
+  uint32_t fqid = 0;      // that segment's query ids (lanes < 32)
   uint32_t slot = 0;      // that copy's first list slot (lanes < 32)
   uint32_t par = 0;       // this segment's survivor buffer
   // the previous segment's survivors to their queries' lists: each key's
@@ -1436,6 +1453,19 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
     WaveLdsSync();
     pending = false;
   };
+  // one list-slot atomic per query slot with survivors of the last segment;
+  // issued behind the next segment's loads (vmcnt is in order: a wait for
+  // those loads would otherwise wait for these atomics too), consumed by
+  // copy_prev after that segment's first tile
+  auto flush_prev = [&]() {
+    if (lane < Q) {
+      const uint32_t m = wl.qcnt[lane];
+      slot = m ? atomicAdd(&a.cand_count[size_t(fqid) * kCounterStride], m) : 0u;
+      wl.prev_qid[lane] = fqid;
+    }
+    flush = false;
+    pending = true;
+  };
   // one LDS claim of two tiles of segment `sg` (lane 0; broadcast at use)
   auto claim2 = [&](uint32_t sg) -> uint32_t {
     uint32_t v = 0;
@@ -1445,7 +1475,8 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
 
   for (;;) {   // rounds of at most kMaxSegs segments (block-uniform)
     __syncthreads();   // s_sw / s_su / the segment table are free
-    if (wv == 0) ListSegments(a, lane, sj, s_item, s_end, s_next, s_sw, s_su, s_nseg, s_claim);
+    if (wv == 0) ListSegments(a, lane, sj, s_item, s_end, s_next, s_desc, s_sw, s_su, s_nseg,
+                                 s_claim);
     __syncthreads();
     const uint32_t nseg = s_nseg;
     if (nseg == 0) break;
@@ -1494,7 +1525,29 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         item = __builtin_amdgcn_readfirstlane(s_item[sg]);
         qid = a.lanes[size_t(item) * Q + c].qid;
       }
-      const WorkItem cur = work[item];
+      // the segment's lane records first (their wait then leaves the B loads
+      // in flight), then the B fragments and the first code tile
+      const ItemLane cl = a.lanes[size_t(item) * Q + c];
+      __builtin_amdgcn_sched_barrier(0);
+      const SegDesc& sd = s_desc[sg];
+      const uint64_t toff = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(sd.tile_off >> 32))) << 32) |
+                            __builtin_amdgcn_readfirstlane(uint32_t(sd.tile_off));
+      const uint64_t moff = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(sd.member_off >> 32))) << 32) |
+                            __builtin_amdgcn_readfirstlane(uint32_t(sd.member_off));
+      const uint32_t n = __builtin_amdgcn_readfirstlane(sd.n);
+      const int leaf = int(__builtin_amdgcn_readfirstlane(sd.leaf));
+      // this segment's B fragments (LUT rows 2s+h of query c) and first tile
+      v4i b[K];
+      uint32_t codes[NW] = {};
+      const uint8_t* tb = a.tiles + toff * 64ull * W + size_t(lane) * W;
+      const v4i* bsrc = reinterpret_cast<const v4i*>(a.lut) + size_t(qid) * 2 * K + h;
+      auto load_b = [&]() {
+#pragma unroll
+        for (int s2 = 0; s2 < K; ++s2) b[s2] = bsrc[2 * s2];
+      };
+      load_b();
+      LoadCodes<K>(tb + size_t(j) * 64 * W, codes);
+      // the claimed-ahead segment's item and query ids, for its setup
       {
         const uint32_t sn = __builtin_amdgcn_readfirstlane(sg_next);
         if (sn < nseg) {
@@ -1505,22 +1558,9 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
           pf_seg = ~0u;
         }
       }
-      const ItemLane cl = a.lanes[size_t(item) * Q + c];
-      // this segment's B fragments (LUT rows 2s+h of query c) and first tile
-      const uint32_t n = cur.n;
-      v4i b[K];
-      uint32_t codes[NW] = {};
-      const uint8_t* tb = a.tiles + cur.tile_off * 64ull * W + size_t(lane) * W;
-      const v4i* bsrc = reinterpret_cast<const v4i*>(a.lut) + size_t(qid) * 2 * K + h;
-      auto load_b = [&]() {
-#pragma unroll
-        for (int s2 = 0; s2 < K; ++s2) b[s2] = bsrc[2 * s2];
-      };
-      load_b();
-      LoadCodes<K>(tb + size_t(j) * 64 * W, codes);
-      const int leaf = int(cur.leaf);
-      const uint64_t moff = cur.member_off;
+
       const int amax = cl.amax;
+      if (flush) flush_prev();
       if (lane < Q) {
         QParam v;
         v.qid = cl.qid;
@@ -1587,11 +1627,12 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         }
         const uint32_t rows_left = n - jt * kDpPerTile;
         if (rows_left < uint32_t(kDpPerTile)) {  // last tile of the leaf
+          // row (i&3) + 8(i>>2) + 4h >= rows_left, against one per-tile value
+          // (16 hoisted row numbers would cost 16 registers for the loop)
+          const int lim = int(rows_left) - 4 * h;
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const uint32_t row = (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (row >= rows_left) acc[i] = 0x7FFF;
-          }
+          for (int i = 0; i < 16; ++i)
+            if ((i & 3) + 8 * (i >> 2) >= lim) acc[i] = 0x7FFF;
         }
         int m = min(min(acc[0], acc[1]), acc[2]);
 #pragma unroll
@@ -1694,19 +1735,14 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         for (int off = 32; off > 0; off >>= 1) sv += uint32_t(__shfl_xor(int(sv), off));
         st_surv = sv;
       }
-      // one list-slot atomic per query slot with survivors; the copy waits
-      // for it after the next segment's first tile
-      if (lane < Q) {
-        const uint32_t m = wl.qcnt[lane];
-        slot = m ? atomicAdd(&a.cand_count[size_t(qid) * kCounterStride], m) : 0u;
-        wl.prev_qid[lane] = qid;
-      }
-      pending = true;
+      flush = true;   // (its slot atomics: at the next segment's start)
+      fqid = qid;
       par ^= 1u;
       if ((ABL & 8) && lane == 0)
         StampItem(a, worker, item, st_rt, st_t0, st_t1, st_t2, __builtin_amdgcn_s_memtime(),
                   uint64_t(tiles_done) | (uint64_t(st_hits) << 16) | (uint64_t(st_surv) << 40));
     }
+    if (flush) flush_prev();
     if (pending) copy_prev();
   }
 }
