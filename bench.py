@@ -98,28 +98,97 @@ def build_index(n, seed):
     return db, q, ix
 
 
+def cpu_info():
+    """CPU model and SIMD ISA of the host (lscpu's fields, from /proc/cpuinfo)."""
+    model, flags = "unknown", set()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name") and model == "unknown":
+                    model = line.split(":", 1)[1].strip()
+                elif line.startswith("flags") and not flags:
+                    flags = set(line.split(":", 1)[1].split())
+    except OSError:
+        pass
+    isa = [x for x in ("sse4_2", "avx", "avx2", "fma", "avx512f", "avx512bw", "avx512_vnni",
+                       "avx512_vbmi") if x in flags]
+    return model, isa
+
+
+def host_threads():
+    """(cores this process can use, cores in its affinity mask): the affinity
+    mask capped by a cgroup CPU quota (a shared host grants a share of its
+    cores; threads beyond it only time-slice)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    cores = aff
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()[:2]),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            with open(path) as f:
+                text = f.read()
+            if parse is not None:
+                quota, period = parse(text)
+            else:
+                quota = text.strip()
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    period = f.read().strip()
+            if quota not in ("max", "-1"):
+                cores = max(1, min(aff, int(float(quota) / float(period))))
+            break
+        except (OSError, ValueError):
+            continue
+    return cores, aff
+
+
 def cpu_baseline(ix, q, gpu_idx, threads):
-    """The oracle's AVX2 port of the reference path on host cores (rank 0)."""
+    """The oracle's AVX2 port of the reference path on all host cores (rank 0):
+    median of 5 timed runs, each >= 2 s of repeated 1000-query batches, with the
+    leaf-scan phase (LUT16 + FastTopNeighbors) timed on its own."""
     from oracle import binding as oracle
     oracle.build()
     try:
         port = oracle.Avx2Port(ix)
     except ValueError:   # pipeline B (non-residual): the oracle's C restatement
         return cpu_baseline_restatement(ix, q, gpu_idx, threads)
-    port.search(q[:50], LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True, threads)  # warm-up
-    reps, t_total, out = 0, 0.0, None
-    while reps < 400 and (t_total < 10.0 or reps == 0):
-        t = time.perf_counter()
-        out = port.search(q, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True, threads)
-        t_total += time.perf_counter() - t
-        reps += 1
-    qps = reps * q.shape[0] / t_total
+    model, isa = cpu_info()
+    port.search(q, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True, threads)  # warm-up + calibration
+    t = time.perf_counter()
+    out = port.search(q, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True, threads)
+    per_batch = time.perf_counter() - t
+    reps = max(1, int(np.ceil(2.0 / max(per_batch, 1e-3))))
+    runs, scan_runs, front_runs = [], [], []
+    _, aff = host_threads()
+    for _ in range(5):
+        t_total, scan_s, front_s = 0.0, 0.0, 0.0
+        for _ in range(reps):
+            t = time.perf_counter()
+            out = port.search(q, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True, threads)
+            t_total += time.perf_counter() - t
+            scan_s += port.last_phase_s["scan"]
+            front_s += port.last_phase_s["front"]
+        nqs = reps * q.shape[0]
+        runs.append(nqs / t_total)
+        # a phase's CPU seconds spread over the cores
+        scan_runs.append(nqs * threads / max(scan_s, 1e-9))
+        front_runs.append(nqs * threads / max(front_s, 1e-9))
     mismatch = float((out[0] != gpu_idx).mean())
     port.close()
-    return dict(value=round(qps, 1), unit="queries/s", cores=threads, kind="port",
-                sample=f"{reps} x the same {q.shape[0]}-query batch through the AVX2 port of "
-                       f"the reference's batched tree-AH path (oracle/lut16_avx2_port.cc, "
-                       f"emulate-mode FastTopNeighbors), {threads} threads, {t_total:.1f}s",
+    return dict(value=round(float(np.median(runs)), 1), unit="queries/s", cores=threads,
+                affinity_cores=aff, kind="port", cpu_model=model, isa=isa,
+                runs_qps=[round(x, 1) for x in runs],
+                scan_only_qps=round(float(np.median(scan_runs)), 1),
+                front_only_qps=round(float(np.median(front_runs)), 1),
+                sample=f"median of 5 runs x {reps} repeats of the same {q.shape[0]}-query batch "
+                       f"through the AVX2 port of the reference's batched tree-AH path "
+                       f"(oracle/lut16_avx2_port.cc: SearchBatchedParallel chunking, pshufb LUT16 "
+                       f"with int16 accumulation, emulate-mode FastTopNeighbors, partition scores "
+                       f"8 centers per AVX2 vector in the many-to-many order), {threads} threads "
+                       f"= every core this process may use ({aff} in its affinity mask, capped "
+                       f"by the cgroup CPU quota); scan_only_qps = the leaf scan phase alone "
+                       f"(its CPU seconds / cores)",
                 id_mismatch_vs_gpu=mismatch)
 
 
@@ -194,11 +263,9 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    scan_bytes = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        scan_bytes.append(nat.timings()["scan_code_bytes"])
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -216,11 +283,12 @@ def main():
     # eagerly: events inside a captured graph carry no timestamps)
     nat.set_profiling(True)
     step()
-    scan_ms, stage = [], {}
+    scan_ms, stage, scan_bytes = [], {}, []
     for _ in range(args.steps):
         step()
         t = nat.timings()
         scan_ms.append(t["scan_ms"])
+        scan_bytes.append(t["scan_code_bytes"])
         for k in ("partition_ms", "lut_ms", "invert_ms", "seed_scan_ms", "seed_select_ms",
                   "scan_ms", "select_ms", "total_ms"):
             stage[k] = stage.get(k, 0.0) + t[k] / args.steps
@@ -310,7 +378,7 @@ def main():
             "max_rel_dist_err": float(np.max(np.abs(gds - od) / np.maximum(np.abs(od), 1e-30))),
         }
         if not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            threads = args.cpu_threads or host_threads()[0]
             log(f"cpu baseline with {threads} threads ...")
             result["cpu_baseline"] = cpu_baseline(ix, q, out_idx.cpu().numpy().astype(np.uint32),
                                                   threads)

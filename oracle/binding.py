@@ -57,7 +57,7 @@ def lib():
         L.orc_avx2_prepare.argtypes = [vp]
         L.orc_avx2_prepare.restype = vp
         L.orc_avx2_release.argtypes = [vp]
-        L.orc_search_avx2.argtypes = [vp, vp] + [ctypes.c_int32] * 6 + [vp, vp, vp]
+        L.orc_search_avx2.argtypes = [vp, vp] + [ctypes.c_int32] * 6 + [vp, vp, vp, vp]
         L.orc_search_avx2.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -179,11 +179,16 @@ class Avx2Port:
         idx = np.zeros((nq, final_nn), np.uint32)
         dist = np.zeros((nq, final_nn), np.float32)
         cnt = np.zeros(nq, np.int32)
+        ph = np.zeros(3, np.float64)
         rc = lib().orc_search_avx2(self._h, q.ctypes.data, nq, leaves, pre_nn, final_nn,
                                    int(reorder), nthreads, idx.ctypes.data, dist.ctypes.data,
-                                   cnt.ctypes.data)
+                                   cnt.ctypes.data, ph.ctypes.data)
         if rc != 0:
             raise RuntimeError(f"orc_search_avx2 failed ({rc})")
+        # CPU seconds (summed over threads) of the last call: partition +
+        # top-L + LUT, the leaf scan (LUT16 + FastTopNeighbors), finish +
+        # dedupe + reorder
+        self.last_phase_s = dict(front=float(ph[0]), scan=float(ph[1]), tail=float(ph[2]))
         return idx, dist, cnt
 
     def close(self):

@@ -90,6 +90,33 @@ inline uint32_t PushMask(const int16_t acc[32], int16_t thr) {
   return uint32_t(_mm256_movemask_epi8(packed));
 }
 
+// Partition scores with the centers transposed, eight per vector: per
+// center the chain acc <- fma(-q_d, c_d, acc) over d ascending (dot) or from
+// ||c||^2 + ||q||^2 with 2 c_d (squared L2) -- fnmadd is that single-rounding
+// fma, so every score equals PartitionScoresOne's bit for bit.
+void PartitionScoresT(const float* q, int dim, const float* ct, int nlp, int nl, int metric,
+                      const float* cnorms, float qnorm, float* out) {
+  for (int c = 0; c < nlp; c += 8) {
+    __m256 acc;
+    if (metric == ORC_METRIC_DOT) {
+      acc = _mm256_setzero_ps();
+    } else {
+      alignas(32) float init[8];
+      for (int i = 0; i < 8; ++i) init[i] = c + i < nl ? cnorms[c + i] + qnorm : 0.0f;
+      acc = _mm256_load_ps(init);
+    }
+    for (int d = 0; d < dim; ++d) {
+      const __m256 qd = _mm256_set1_ps(q[d]);
+      __m256 cd = _mm256_loadu_ps(ct + size_t(d) * nlp + c);
+      if (metric != ORC_METRIC_DOT) cd = _mm256_mul_ps(cd, _mm256_set1_ps(2.0f));
+      acc = _mm256_fnmadd_ps(qd, cd, acc);
+    }
+    alignas(32) float r[8];
+    _mm256_store_ps(r, acc);
+    for (int i = 0; i < 8 && c + i < nl; ++i) out[c + i] = r[i];
+  }
+}
+
 }  // namespace
 #endif  // __AVX2__
 
@@ -98,11 +125,14 @@ inline uint32_t PushMask(const int16_t acc[32], int16_t thr) {
 namespace orc_port {
 using GroupFn = void (*)(const uint8_t*, int, const uint8_t*, int16_t*);
 using MaskFn = uint32_t (*)(const int16_t*, int16_t);
+using PartFn = void (*)(const float*, int, const float*, int, int, int, const float*, float,
+                        float*);
 void* Prepare(const orc_index* ix);
 void Release(void* p);
 int Run(void* prepared, const float* queries, int nq, int leaves, int pre_nn,
         int final_nn, int do_reorder, int nthreads, uint32_t* out_idx,
-        float* out_dist, int32_t* out_count, GroupFn group_fn, MaskFn mask_fn);
+        float* out_dist, int32_t* out_count, GroupFn group_fn, MaskFn mask_fn,
+        PartFn part_fn, double* phase_s);
 }  // namespace orc_port
 
 extern "C" {
@@ -111,15 +141,15 @@ void orc_avx2_release(void* p) { orc_port::Release(p); }
 int orc_search_avx2(void* prepared, const float* queries, int32_t nq,
                     int32_t leaves, int32_t pre_nn, int32_t final_nn,
                     int32_t do_reorder, int32_t nthreads, uint32_t* out_idx,
-                    float* out_dist, int32_t* out_count) {
+                    float* out_dist, int32_t* out_count, double* phase_s) {
 #if defined(__AVX2__)
   return orc_port::Run(prepared, queries, nq, leaves, pre_nn, final_nn,
                        do_reorder, nthreads, out_idx, out_dist, out_count,
-                       &Lut16Group, &PushMask);
+                       &Lut16Group, &PushMask, &PartitionScoresT, phase_s);
 #else
   (void)prepared; (void)queries; (void)nq; (void)leaves; (void)pre_nn;
   (void)final_nn; (void)do_reorder; (void)nthreads; (void)out_idx;
-  (void)out_dist; (void)out_count;
+  (void)out_dist; (void)out_count; (void)phase_s;
   return -2;
 #endif
 }

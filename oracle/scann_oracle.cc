@@ -24,6 +24,8 @@
 #include "scann_oracle.h"
 
 #include <algorithm>
+#include <ctime>
+#include <mutex>
 #include <atomic>
 #include <cfloat>
 #include <cmath>
@@ -902,12 +904,20 @@ int32_t orc_fast_topn_replay(const uint32_t* idx, const float* dist, int32_t n,
 namespace orc_port {
 using GroupFn = void (*)(const uint8_t*, int, const uint8_t*, int16_t*);
 using MaskFn = uint32_t (*)(const int16_t*, int16_t);
+// Partition scores of one query against the transposed centers ct[dim][nlp]
+// (nlp = nl rounded up to 8), the same per-center FMA chain as
+// PartitionScoresOne, eight centers per vector (many_to_many_impl.inc:522-560
+// runs the reference's chain across centers the same way).
+using PartFn = void (*)(const float* q, int dim, const float* ct, int nlp, int nl, int metric,
+                        const float* cnorms, float qnorm, float* out);
 
 struct Prepared {
   const orc_index* ix;
   orc::IndexView view;
   std::vector<std::vector<uint8_t>> packed;  // per leaf, reference layout
   std::vector<int> leaf_order;               // leaf_tokens_by_norm_
+  std::vector<float> ct;                     // [dim][nlp] transposed centers
+  int nlp = 0;
 };
 
 void* Prepare(const orc_index* ix) {
@@ -929,6 +939,11 @@ void* Prepare(const orc_index* ix) {
   }
   p->leaf_order.resize(nl);
   for (int l = 0; l < nl; ++l) p->leaf_order[p->view.leaf_rank_by_norm[l]] = l;
+  const int dim = ix->dim;
+  p->nlp = (nl + 7) & ~7;
+  p->ct.assign(size_t(dim) * p->nlp, 0.0f);
+  for (int c = 0; c < nl; ++c)
+    for (int d = 0; d < dim; ++d) p->ct[size_t(d) * p->nlp + c] = ix->centers[size_t(c) * dim + d];
   return p;
 }
 
@@ -936,7 +951,8 @@ void Release(void* p) { delete static_cast<Prepared*>(p); }
 
 int Run(void* prepared, const float* queries, int nq, int leaves, int pre_nn,
         int final_nn, int do_reorder, int nthreads, uint32_t* out_idx,
-        float* out_dist, int32_t* out_count, GroupFn group_fn, MaskFn mask_fn) {
+        float* out_dist, int32_t* out_count, GroupFn group_fn, MaskFn mask_fn,
+        PartFn part_fn, double* phase_s) {
   auto* P = static_cast<Prepared*>(prepared);
   if (!P || leaves <= 0 || final_nn < 0 || nq < 0) return -1;
   const orc_index* ix = P->ix;
@@ -950,7 +966,19 @@ int Run(void* prepared, const float* queries, int nq, int leaves, int pre_nn,
   // SearchBatchedParallel chunking: min(max(1, ceil(nq/threads)), 256).
   const int chunk = std::min(std::max(1, (nq + nthreads - 1) / nthreads), 256);
   const int nchunks = (nq + chunk - 1) / chunk;
+  // CPU seconds per phase: [0] partition + top-L + LUT, [1] the leaf
+  // scan (LUT16 + FastTopNeighbors), [2] finish + dedupe + reorder
+  std::mutex tmu;
+  double tsum[3] = {0.0, 0.0, 0.0};
+  // per-thread CPU time (not wall time: robust to a CPU quota below the
+  // thread count)
+  auto cpu_now = []() {
+    timespec ts;
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+    return double(ts.tv_sec) + 1e-9 * double(ts.tv_nsec);
+  };
   orc::ParallelFor(nchunks, nthreads, [&](int ci) {
+    const double c0 = cpu_now();
     const int q0 = ci * chunk, nqc = std::min(chunk, nq - q0);
     std::vector<orc::Lut> luts(nqc);
     std::vector<float> invs(nqc);
@@ -960,8 +988,12 @@ int Run(void* prepared, const float* queries, int nq, int leaves, int pre_nn,
     std::vector<float> scratch(nl);
     for (int j = 0; j < nqc; ++j) {
       const float* q = queries + size_t(q0 + j) * dim;
-      orc::PartitionScoresOne(q, dim, ix->centers, nl, ix->metric, v.cnorms,
-                              scratch.data());
+      if (part_fn)
+        part_fn(q, dim, P->ct.data(), P->nlp, nl, ix->metric, v.cnorms.data(),
+                ix->metric == ORC_METRIC_DOT ? 0.0f : orc::QuerySqNorm(q, dim), scratch.data());
+      else
+        orc::PartitionScoresOne(q, dim, ix->centers, nl, ix->metric, v.cnorms,
+                                scratch.data());
       std::vector<int> lf;
       std::vector<float> sc;
       orc::TopL(scratch.data(), nl, leaves, &lf, &sc);
@@ -971,6 +1003,7 @@ int Run(void* prepared, const float* queries, int nq, int leaves, int pre_nn,
       invs[j] = static_cast<float>(1.0 / static_cast<double>(luts[j].mult));
       tops.emplace_back(size_t(kk));
     }
+    const double c1 = cpu_now();
     int16_t acc[32];
     for (int leaf : P->leaf_order) {
       const auto& ql = by_leaf[leaf];
@@ -1015,6 +1048,7 @@ int Run(void* prepared, const float* queries, int nq, int leaves, int pre_nn,
         bs += nbatch;
       }
     }
+    const double c2 = cpu_now();
     for (int j = 0; j < nqc; ++j) {
       const int qi = q0 + j;
       const float* q = queries + size_t(qi) * dim;
@@ -1040,7 +1074,14 @@ int Run(void* prepared, const float* queries, int nq, int leaves, int pre_nn,
             has ? r[t].second : std::numeric_limits<float>::quiet_NaN();
       }
     }
+    const double c3 = cpu_now();
+    std::lock_guard<std::mutex> lk(tmu);
+    tsum[0] += c1 - c0;
+    tsum[1] += c2 - c1;
+    tsum[2] += c3 - c2;
   });
+  if (phase_s)
+    for (int i = 0; i < 3; ++i) phase_s[i] = tsum[i];
   return 0;
 }
 }  // namespace orc_port

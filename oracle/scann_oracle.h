@@ -120,13 +120,16 @@ int32_t orc_fast_topn_replay(const uint32_t* idx, const float* dist,
  * reference does this when it builds its leaf searchers, searcher.cc:108-111)
  * and returns NULL for indexes the port does not cover (non-residual, or the
  * global top-N path disabled).  orc_search_avx2 returns -2 if the library was
- * built without AVX2. */
+ * built without AVX2.  Partition scoring runs eight centers per AVX2 vector
+ * over transposed centers (the reference's many-to-many order), bit-equal to
+ * the scalar chain. */
 void* orc_avx2_prepare(const orc_index* idx);
 void orc_avx2_release(void* prepared);
 int orc_search_avx2(void* prepared, const float* queries, int32_t nq,
                     int32_t leaves, int32_t pre_nn, int32_t final_nn,
                     int32_t do_reorder, int32_t nthreads, uint32_t* out_idx,
-                    float* out_dist, int32_t* out_count);
+                    float* out_dist, int32_t* out_count,
+                    double* phase_s /* [3] CPU seconds: front, scan, tail; or NULL */);
 
 #ifdef __cplusplus
 }

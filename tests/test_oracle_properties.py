@@ -62,6 +62,8 @@ def test_avx2_port_equals_emulate(oracle, small_dot, reorder):
     np.testing.assert_array_equal(pi, ei)
     np.testing.assert_array_equal(pd.view(np.uint32), ed.view(np.uint32))
     np.testing.assert_array_equal(pc, ec)
+    assert set(port.last_phase_s) == {"front", "scan", "tail"}
+    assert all(v >= 0.0 for v in port.last_phase_s.values())
 
 
 def test_emulate_vs_ideal_mismatch_small(oracle):
