@@ -69,20 +69,19 @@ struct WorkItem {
   uint64_t member_off;   // the leaf's first member
 };
 
-// Per (work item, query slot c < 32): everything the scan needs about that
-// (query, leaf) pair -- the query, the largest LUT16 sum whose distance can
-// pass its threshold (kNoSum for an empty slot), the partition distance
-// (residual bias), the query's 1/multiplier and threshold key -- so that an
-// item's setup has no dependent loads (32 B, two dwordx4 per lane).
+// Per (work item, query slot c < 32): the (query, leaf) pair -- the query
+// (kNoQuery for an empty slot), the partition distance (residual bias) and
+// the query's 1/multiplier; one dwordx4 per lane.  Written by the pair
+// scatter (beside the seed pass, which owns the thresholds); the scan derives
+// the slot's sum limit from the query's threshold key at a segment's start.
 struct ItemLane {
   uint32_t qid;
-  int32_t amax;
   float bias;
   float inv;
-  uint64_t tau;
-  uint64_t pad;
+  uint32_t pad;
 };
-constexpr int32_t kNoSum = -2147483647 - 1;   // ItemLane::amax of an empty slot
+constexpr uint32_t kNoQuery = 0xFFFFFFFFu;     // ItemLane::qid of an empty slot
+constexpr int32_t kNoSum = -2147483647 - 1;   // the sum limit of an empty slot
 
 struct ScanArgs {
   const uint8_t* tiles;
@@ -108,7 +107,8 @@ struct ScanArgs {
 struct SeedArgs {
   const int32_t* topl_leaf;   // [nq][L]
   const float* topl_dist;     // [nq][L]
-  // the inversion: every (query, leaf) pair's slot in its leaf's work items
+  // the inversion (pair scatter): every (query, leaf) pair's slot in its
+  // leaf's work items
   const uint32_t* rank;       // [nq][L] position inside the leaf's list
   const uint32_t* leaf_item0; // [nl] the leaf's first work item
   ItemLane* lanes;            // [work items][32]
@@ -240,7 +240,11 @@ hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int va
                       hipStream_t s);
 // Resident scan workgroups per CU (occupancy of the index's instantiation).
 hipError_t ScanBlocksPerCU(const DeviceIndex& ix, int* blocks);
+// The per-query thresholds (tau_key) from the seed leaves.
 hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s);
+// Every (query, leaf) pair's lane record into its leaf's work items (after
+// LaunchWorklist; independent of LaunchSeed).
+hipError_t LaunchPairScatter(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s);
 // The rank kernel (one block per query, <= kSelMax keys in LDS) for k' <=
 // kSelMax, the block kernel otherwise; both rescan overflowed lists first.
 hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s);

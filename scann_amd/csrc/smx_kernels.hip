@@ -873,11 +873,9 @@ __global__ void __launch_bounds__(64) items_kernel(
     const uint32_t ne = kQueriesPerTile - first;
     for (uint32_t e = lane; e < ne * chunks; e += 64) {
       ItemLane v;
-      v.qid = 0;
-      v.amax = kNoSum;
+      v.qid = kNoQuery;
       v.bias = 0.0f;
       v.inv = 0.0f;
-      v.tau = 0;
       v.pad = 0;
       lanes[size_t(item0 + (qt - 1) * chunks + e / ne) * kQueriesPerTile + first + e % ne] = v;
     }
@@ -1174,35 +1172,36 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
   return s_T;
 }
 
-// Per query: its threshold (SeedTau), then its (query, leaf) pairs into the
-// scan's work-item lanes -- slot rank % 32 of query tile rank / 32, in every
-// chunk of the leaf -- with the pair's bias and sum limit.  This is the
-// scatter half of InvertCentersToSearch (tree_ah_hybrid_residual.cc:610-622).
+// Per query: its threshold key (SeedTau).
 template <int K>
 __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
   const int qi = blockIdx.x;
   const uint64_t T = SeedTau<K>(a, qi);
   if (threadIdx.x == 0) a.tau_key[qi] = T;
-  const float inv = a.inv[qi];
-  const int smin = -128 * a.nb, smax = 128 * a.nb;
-  for (int i = threadIdx.x; i < a.L; i += blockDim.x) {
-    const int32_t leaf = a.topl_leaf[size_t(qi) * a.L + i];
-    if (leaf < 0) continue;
-    const uint32_t r = a.rank[size_t(qi) * a.L + i];
-    const uint32_t n = a.leaf_size[leaf];
-    const uint32_t chunks = LeafChunks(n, a.chunk_tiles);
-    const float bias = a.residual ? a.topl_dist[size_t(qi) * a.L + i] : 0.0f;
-    ItemLane v;
-    v.qid = uint32_t(qi);
-    v.amax = T == kNoThreshold ? smax : SumLimit(FromOrdered(uint32_t(T >> 32)), inv, bias, smin, smax);
-    v.bias = bias;
-    v.inv = inv;
-    v.tau = T;
-    v.pad = 0;
-    const uint32_t w0 = a.leaf_item0[leaf] + (r / kQueriesPerTile) * chunks;
-    for (uint32_t ch = 0; ch < chunks; ++ch) a.lanes[size_t(w0 + ch) * kQueriesPerTile + (r % kQueriesPerTile)] = v;
-  }
-  SMX_PHASE(1, qi, 4);
+}
+
+// Every (query, leaf) pair into the scan's work-item lanes -- slot rank % 32
+// of query tile rank / 32, in every chunk of the leaf -- with the pair's bias
+// and the query's 1/multiplier: the scatter half of InvertCentersToSearch
+// (tree_ah_hybrid_residual.cc:610-622).  One thread per pair; runs beside
+// the seed pass (they share no buffer).
+__global__ void __launch_bounds__(256) pair_scatter_kernel(SeedArgs a, int nq) {
+  const size_t p = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (p >= size_t(nq) * a.L) return;
+  const int32_t leaf = a.topl_leaf[p];
+  if (leaf < 0) return;
+  const uint32_t qi = uint32_t(p / a.L);
+  const uint32_t r = a.rank[p];
+  const uint32_t n = a.leaf_size[leaf];
+  const uint32_t chunks = LeafChunks(n, a.chunk_tiles);
+  ItemLane v;
+  v.qid = qi;
+  v.bias = a.residual ? a.topl_dist[p] : 0.0f;
+  v.inv = a.inv[qi];
+  v.pad = 0;
+  const uint32_t w0 = a.leaf_item0[leaf] + (r / kQueriesPerTile) * chunks;
+  for (uint32_t ch = 0; ch < chunks; ++ch)
+    a.lanes[size_t(w0 + ch) * kQueriesPerTile + (r % kQueriesPerTile)] = v;
 }
 
 
@@ -1527,7 +1526,10 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       }
       // the segment's lane records first (their wait then leaves the B loads
       // in flight), then the B fragments and the first code tile
+      // an empty slot (kNoQuery) loads query 0's rows and never passes (amax)
+      const uint32_t lq = qid == kNoQuery ? 0u : qid;
       const ItemLane cl = a.lanes[size_t(item) * Q + c];
+      const uint64_t tau = a.tau_key[lq];
       __builtin_amdgcn_sched_barrier(0);
       const SegDesc& sd = s_desc[sg];
       const uint64_t toff = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(sd.tile_off >> 32))) << 32) |
@@ -1540,7 +1542,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       v4i b[K];
       uint32_t codes[NW] = {};
       const uint8_t* tb = a.tiles + toff * 64ull * W + size_t(lane) * W;
-      const v4i* bsrc = reinterpret_cast<const v4i*>(a.lut) + size_t(qid) * 2 * K + h;
+      const v4i* bsrc = reinterpret_cast<const v4i*>(a.lut) + size_t(lq) * 2 * K + h;
       auto load_b = [&]() {
 #pragma unroll
         for (int s2 = 0; s2 < K; ++s2) b[s2] = bsrc[2 * s2];
@@ -1559,15 +1561,21 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         }
       }
 
-      const int amax = cl.amax;
+      // the slot's sum limit: the largest LUT16 sum whose distance can pass
+      // the query's threshold (d is monotone in the sum)
+      int amax = kNoSum;
+      if (qid != kNoQuery)
+        amax = tau == kNoThreshold ? 128 * a.nb
+                                   : SumLimit(FromOrdered(uint32_t(tau >> 32)), cl.inv, cl.bias,
+                                              -128 * a.nb, 128 * a.nb);
       if (flush) flush_prev();
       if (lane < Q) {
         QParam v;
-        v.qid = cl.qid;
-        v.amax = cl.amax;
+        v.qid = qid;
+        v.amax = amax;
         v.bias = cl.bias;
         v.inv = cl.inv;
-        v.tau = cl.tau;
+        v.tau = tau;
         wl.qp[lane] = v;
         wl.qcnt[lane] = 0;
       }
@@ -2728,6 +2736,15 @@ hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStrea
     default:
       return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t LaunchPairScatter(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s) {
+  (void)ix;
+  const size_t pairs = size_t(nq) * size_t(a.L);
+  if (pairs == 0) return hipSuccess;
+  hipLaunchKernelGGL(pair_scatter_kernel, dim3(unsigned((pairs + 255) / 256)), dim3(256), 0, s, a,
+                     nq);
   return hipGetLastError();
 }
 

@@ -145,6 +145,8 @@ struct smx_index {
   smx_timings timings{};
   hipEvent_t ev[16] = {};
   hipEvent_t done_ev = nullptr;      // the last call's end (cross-stream ordering)
+  hipStream_t side = nullptr;        // the fork/join branch of every call
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   hipStream_t last_stream = nullptr;
   // scan variant 8 (diagnostics): per-item stamps, dumped to $SMX_STAMPS
   unsigned long long* stamps = nullptr;
@@ -527,12 +529,23 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     f.inv = w.inv;
     SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s, &f));
     Mark(h, 1, s);
-    Mark(h, 2, s);
+    // Fork.  Side stream: the work list and the pairs' lane records; this
+    // stream: the seed thresholds.  Write sets ("Two streams"):
+    // side = leaf_item0, pos_unit0, gunits, work, lanes, wave_start,
+    // stats[3..7]; seed = tau.  Both only read the front end's outputs,
+    // written before the fork; the per-call state reset happens in the
+    // partition kernel, before the fork as well.
+    SMX_HIP(hipEventRecord(h->fork_ev, s));
+    SMX_HIP(hipStreamWaitEvent(h->side, h->fork_ev, 0));
     SMX_HIP(smx::LaunchWorklist(ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes,
-                                w.wave_start, h->grid, stats + 3, code_bytes, h->chunk_tiles, s));
-    Mark(h, 3, s);
-    SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));   // thresholds + the pairs' item lanes
+                                w.wave_start, h->grid, stats + 3, code_bytes, h->chunk_tiles,
+                                h->side));
+    SMX_HIP(smx::LaunchPairScatter(ix, sa, nq, h->side));
+    Mark(h, 3, h->side);
+    SMX_HIP(hipEventRecord(h->join_ev, h->side));
+    SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
     Mark(h, 4, s);
+    SMX_HIP(hipStreamWaitEvent(s, h->join_ev, 0));   // join
     Mark(h, 5, s);
     SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s));
     Mark(h, 6, s);
@@ -629,10 +642,12 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   smx_timings& t = h->timings;
   if (h->profiling) {
     // The stream is idle here, so reading the events costs no extra sync.
+    // the LUT build runs inside the top-L launch; the inversion (side
+    // stream) and the seed overlap, each timed from the fork
     t.partition_ms = Elapsed(h, 0, 1);
-    t.lut_ms = Elapsed(h, 1, 2);
-    t.invert_ms = Elapsed(h, 2, 3);
-    t.seed_scan_ms = Elapsed(h, 3, 4);
+    t.lut_ms = 0.0f;
+    t.invert_ms = Elapsed(h, 1, 3);
+    t.seed_scan_ms = Elapsed(h, 1, 4);
     t.seed_select_ms = 0.0f;
     t.scan_ms = Elapsed(h, 5, 6);
     t.select_ms = Elapsed(h, 6, 7);
@@ -715,7 +730,10 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
     return Fail(SMX_DEVICE_ERROR, "hipStreamCreate failed");
   }
   for (auto& e : h->ev) (void)hipEventCreate(&e);
-  if (hipEventCreateWithFlags(&h->done_ev, hipEventDisableTiming) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->done_ev, hipEventDisableTiming) != hipSuccess) {
     smx_index_destroy(h);
     return Fail(SMX_DEVICE_ERROR, "hipEventCreate failed");
   }
@@ -752,6 +770,12 @@ int smx_index_destroy(smx_index* h) {
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
   if (h->done_ev) (void)hipEventDestroy(h->done_ev);
+  if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
+  if (h->join_ev) (void)hipEventDestroy(h->join_ev);
+  if (h->side) {
+    (void)hipStreamSynchronize(h->side);
+    (void)hipStreamDestroy(h->side);
+  }
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return SMX_OK;

@@ -224,3 +224,41 @@ def test_pickled_docids_are_never_loaded(tmp_path):
     (tmp_path / "scann_docids.pkl").write_bytes(b"\x80\x04N.")
     with pytest.raises(ValueError, match="pickle"):
         scann_ops_pybind.load_searcher(str(tmp_path))
+
+
+def test_schema_matches_reference_protos():
+    """assets.py's field table agrees with the reference's .proto files
+    (tests/golden/proto_fields.json, parsed by tests/golden/make_proto_fields.py
+    in the build container): every field the codec knows has the reference's
+    number and type, every enum value the reference's number."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "proto_fields.json")
+    with open(path) as f:
+        ref = json.load(f)
+    msgs, enums = ref["messages"], ref["enums"]
+    bad = []
+    for msg, fields in assets._SCHEMA.items():
+        pm = msgs.get(msg)
+        if pm is None:
+            bad.append(("message", msg))
+            continue
+        for num, (name, kind, sub) in fields.items():
+            f = pm.get(name)
+            if f is None:
+                bad.append(("field", msg, name))
+                continue
+            if f["number"] != num:
+                bad.append(("number", msg, name, num, f["number"]))
+            if kind == "msg":
+                if f["type"] != sub:
+                    bad.append(("message type", msg, name, sub, f["type"]))
+            elif kind == "enum":
+                en = enums.get(f"{msg}.{f['type']}", enums.get(f["type"]))
+                if en is None:
+                    bad.append(("enum", msg, name, f["type"]))
+                    continue
+                for ename, ev in sub.items():
+                    if en.get(ename) != ev:
+                        bad.append(("enum value", msg, name, ename, ev, en.get(ename)))
+            elif f["type"] != kind:
+                bad.append(("type", msg, name, kind, f["type"]))
+    assert not bad, bad
