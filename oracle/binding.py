@@ -54,6 +54,9 @@ def lib():
         L.orc_exact_distance.restype = ctypes.c_float
         L.orc_fast_topn_replay.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp]
         L.orc_fast_topn_replay.restype = ctypes.c_int32
+        L.orc_avq_encode.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_int32,
+                                     ctypes.c_int32, ctypes.c_double, vp]
+        L.orc_avq_encode.restype = None
         L.orc_avx2_prepare.argtypes = [vp]
         L.orc_avx2_prepare.restype = vp
         L.orc_avx2_release.argtypes = [vp]
@@ -161,6 +164,18 @@ def fast_topn_replay(ids, dists, k):
     n = lib().orc_fast_topn_replay(ids.ctypes.data, dists.ctypes.data, len(ids), k,
                                    oi.ctypes.data, od.ctypes.data, ngc.ctypes.data)
     return oi[:n], od[:n], int(ngc[0])
+
+
+def avq_encode(residuals, originals, codebook, threshold):
+    """The oracle's row-by-row AVQ noise-shaped encoding, uint8 [n, B]."""
+    r = _c(residuals, np.float32)
+    x = _c(originals, np.float32)
+    cb = _c(codebook, np.float32)
+    nb, _, dpb = cb.shape
+    out = np.zeros((r.shape[0], nb), np.uint8)
+    lib().orc_avq_encode(r.ctypes.data, x.ctypes.data, r.shape[0], r.shape[1], cb.ctypes.data,
+                         nb, dpb, float(threshold), out.ctypes.data)
+    return out
 
 
 class Avx2Port:

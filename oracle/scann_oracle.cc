@@ -894,6 +894,94 @@ int32_t orc_fast_topn_replay(const uint32_t* idx, const float* dist, int32_t n,
   return int32_t(r.size());
 }
 
+// AVQ noise-shaped encoding of n rows: IndexDatapointNoiseShaped
+// (asymmetric_hashing_impl.cc:434-503) with ComputeResidualStats (:300-343,
+// ComputeResidualStatsForCluster :283-298), ComputeParallelCostMultiplier
+// (:268-274), InitializeToMinResidualNorm (:345-358) and
+// OptimizeSingleSubspace (:372-404), one row at a time.  Blocks are chunks of
+// dims_per_block coordinates, the last one zero-padded.  ||x||^2 of the cost
+// multiplier is accumulated in coordinate order like the chunked norm (the
+// reference's SquaredL2Norm order is its SIMD target's).  Blocks with equal
+// residual norms keep block order in the visiting sort.
+void orc_avq_encode(const float* residuals, const float* originals, int32_t n, int32_t dim,
+                    const float* codebook, int32_t nb, int32_t dpb, double threshold,
+                    uint8_t* out) {
+  const int nc = 16;
+  for (int32_t row = 0; row < n; ++row) {
+    const float* r = residuals + size_t(row) * dim;
+    const float* x = originals + size_t(row) * dim;
+    auto coord = [&](const float* v, int b, int i) -> double {
+      const int d = b * dpb + i;
+      return d < dim ? static_cast<double>(v[d]) : 0.0;
+    };
+    double chunked_norm = 0.0;
+    for (int b = 0; b < nb; ++b)
+      for (int i = 0; i < dpb; ++i) chunked_norm += coord(x, b, i) * coord(x, b, i);
+    const double sq_norm = chunked_norm;
+    chunked_norm = std::sqrt(chunked_norm);
+    const double inv_norm = 1.0 / chunked_norm;
+    std::vector<double> rn(size_t(nb) * nc), par(size_t(nb) * nc);
+    for (int b = 0; b < nb; ++b)
+      for (int c = 0; c < nc; ++c) {
+        double a = 0.0, p = 0.0;
+        for (int i = 0; i < dpb; ++i) {
+          const double rc = coord(r, b, i) - static_cast<double>(codebook[(size_t(b) * nc + c) * dpb + i]);
+          a += rc * rc;
+          p += rc * coord(x, b, i) * inv_norm;
+        }
+        rn[size_t(b) * nc + c] = a;
+        par[size_t(b) * nc + c] = p;
+      }
+    const double t2 = threshold * threshold;
+    const double eta = (t2 / sq_norm) / ((1.0 - t2 / sq_norm) / (double(dim) - 1.0));
+    std::vector<int> code(nb);
+    for (int b = 0; b < nb; ++b) {
+      int best = 0;
+      for (int c = 1; c < nc; ++c)
+        if (rn[size_t(b) * nc + c] < rn[size_t(b) * nc + best]) best = c;
+      code[b] = best;
+    }
+    double P = 0.0;
+    for (int b = 0; b < nb; ++b) P += par[size_t(b) * nc + code[b]];
+    std::vector<int> order(nb);
+    for (int b = 0; b < nb; ++b) order[b] = b;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+      return rn[size_t(a) * nc + code[a]] > rn[size_t(b) * nc + code[b]];
+    });
+    bool changed = true;
+    for (int round = 0; changed && round < 10; ++round) {
+      changed = false;
+      for (int i = 0; i < nb; ++i) {
+        const int b = order[i];
+        const int cur = code[b];
+        const double old_rn = rn[size_t(b) * nc + cur], old_par = par[size_t(b) * nc + cur];
+        int new_c = cur;
+        double best_cost = 0.0, best_p = P;
+        for (int c = 0; c < nc; ++c) {
+          if (c == cur) continue;
+          const double new_p = P - old_par + par[size_t(b) * nc + c];
+          const double pnd = new_p * new_p - P * P;
+          if (pnd > 0.0) continue;
+          const double rnd = rn[size_t(b) * nc + c] - old_rn;
+          const double perp = rnd - pnd;
+          const double cost = eta * pnd + perp;
+          if (cost < best_cost) {
+            new_c = c;
+            best_cost = cost;
+            best_p = new_p;
+          }
+        }
+        if (new_c != cur) {
+          P = best_p;
+          code[b] = new_c;
+          changed = true;
+        }
+      }
+    }
+    for (int b = 0; b < nb; ++b) out[size_t(row) * nb + b] = uint8_t(code[b]);
+  }
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------

@@ -113,6 +113,13 @@ int32_t orc_fast_topn_replay(const uint32_t* idx, const float* dist,
                              int32_t n, int32_t k, uint32_t* out_idx,
                              float* out_dist, int32_t* out_num_gc);
 
+/* AVQ noise-shaped AH encoding (IndexDatapointNoiseShaped,
+ * asymmetric_hashing_impl.cc:434-503) of n rows: residuals and the original
+ * rows [n][dim], codebook [nb][16][dpb], threshold T; codes [n][nb]. */
+void orc_avq_encode(const float* residuals, const float* originals, int32_t n, int32_t dim,
+                    const float* codebook, int32_t nb, int32_t dpb, double threshold,
+                    uint8_t* out);
+
 /* AVX2 port of the reference's hot loop (lut16_avx2.inc) driving the same
  * emulate-mode pipeline, multithreaded like SearchBatchedParallel
  * (scann.cc:478-501).  Used only as bench.py's cpu_baseline.

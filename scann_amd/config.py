@@ -115,6 +115,7 @@ class SearchConfig:
     reorder_num_neighbors: Optional[int] = None
     soar_lambda: Optional[float] = None
     overretrieve_factor: float = 2.0
+    noise_shaping_threshold: Optional[float] = None   # AVQ; None / NaN = plain encoding
     raw: Optional[Dict[str, List[Any]]] = None
 
     @property
@@ -123,6 +124,20 @@ class SearchConfig:
 
 
 _DISTANCES = {"DotProductDistance": "dot_product", "SquaredL2Distance": "squared_l2"}
+
+
+def _noise_shaping(ah) -> Optional[float]:
+    """AsymmetricHasherConfig.noise_shaping_threshold (NaN = off).  Noise-shaped
+    training of the codebooks (use_noise_shaped_training) is not implemented
+    and is rejected rather than ignored."""
+    if _get(ah, "use_noise_shaped_training"):
+        raise ValueError("use_noise_shaped_training is not supported (AVQ applies to the "
+                         "encoding; the codebooks are trained by plain k-means)")
+    t = _get(ah, "noise_shaping_threshold")
+    if t is None:
+        return None
+    t = float(t)
+    return None if t != t else t
 
 
 def search_config_from_text(text: str) -> SearchConfig:
@@ -170,4 +185,5 @@ def search_config_from_tree(tree: Dict[str, List[Any]]) -> SearchConfig:
         reorder_num_neighbors=None if reorder is None else int(reorder),
         soar_lambda=None if spill is None else float(_get(spill, "orthogonality_amplification_lambda", default=1.5)),
         overretrieve_factor=float(_get(spill, "overretrieve_factor", default=2.0)) if spill else 2.0,
+        noise_shaping_threshold=_noise_shaping(ah),
         raw=tree)

@@ -13,8 +13,10 @@ builder API:
 * residuals against the assigned center for tree + dot product
   (tree_ah_hybrid_residual.cc:185-224, scann_builder.py:429-431);
 * one 16-center k-means codebook per block (asymmetric_hashing_impl.cc:41-198)
-  and nearest-center encoding (anisotropic AVQ noise shaping is not
-  reproduced; the searcher takes any codes);
+  and nearest-center encoding, or -- with a noise_shaping_threshold (the
+  builder's anisotropic_quantization_threshold) -- the anisotropic (AVQ)
+  noise-shaped encoding of IndexDatapointNoiseShaped
+  (asymmetric_hashing_impl.cc:268-503), on the GPU when one is visible;
 * optional SOAR spilling: a second leaf per datapoint minimising
   ||x - c||^2 + lambda * <r, x - c>^2 / ||r||^2 with r the primary residual
   (SOAR's orthogonality-amplified loss, kmeans_tree_partitioner.cc:926-997),
@@ -133,6 +135,121 @@ def encode(residuals: np.ndarray, codebook: np.ndarray, chunk: int = 1 << 15) ->
     return out
 
 
+def _avq_parallel_cost_multiplier(t: float, sq_norm, dims: int):
+    """ComputeParallelCostMultiplier (asymmetric_hashing_impl.cc:268-274)."""
+    parallel = (t * t) / sq_norm
+    perpendicular = (1.0 - (t * t) / sq_norm) / (dims - 1.0)
+    return parallel / perpendicular
+
+
+def encode_avq(residuals: np.ndarray, originals: np.ndarray, codebook: np.ndarray,
+               threshold: float, chunk: int = 1 << 15) -> np.ndarray:
+    """Noise-shaped (AVQ) codes, uint8 [n, B]: IndexDatapointNoiseShaped
+    (asymmetric_hashing_impl.cc:434-503) for every row, vectorised over rows.
+
+    Per row, in double: the per-block, per-center residual norm sum (r - c)^2
+    and parallel component sum (r - c) * x / ||x|| (ComputeResidualStats,
+    :283-343; sums over a block's dims in dim order); start from each block's
+    nearest center (InitializeToMinResidualNorm, first minimum); blocks
+    visited by their residual norm, largest first; up to 10 rounds of
+    coordinate descent where a block moves to the center with the most
+    negative eta * d_parallel^2 + d_perpendicular among those that do not
+    grow the parallel component (OptimizeSingleSubspace, :366-404, first
+    minimum in center order).  A row whose round changes nothing would repeat
+    it, so running every row 10 rounds equals the reference's early exit.
+    Ties between equal block residual norms keep block order (the
+    reference's ZipSortBranchOptimized leaves their order unspecified)."""
+    num_blocks, nc, dpb = codebook.shape
+    n, dim = originals.shape
+    out = np.empty((n, num_blocks), np.uint8)
+    torch, dev = _torch_device()
+    if torch is not None:
+        xp_from = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    else:
+        xp_from = lambda a: a  # noqa: E731
+    cb = xp_from(codebook.astype(np.float64))                    # [B, 16, dpb]
+    for s in range(0, n, chunk):
+        r = xp_from(_block_view(residuals[s:s + chunk], num_blocks, dpb).astype(np.float64))
+        x = xp_from(_block_view(originals[s:s + chunk], num_blocks, dpb).astype(np.float64))
+        m = r.shape[0]
+        # ||x||^2 accumulated over the chunked coordinates in order; 1/sqrt
+        sqn = None
+        for b in range(num_blocks):
+            for i in range(dpb):
+                t = x[:, b, i] * x[:, b, i]
+                sqn = t if sqn is None else sqn + t
+        inv_norm = 1.0 / (torch.sqrt(sqn) if torch is not None else np.sqrt(sqn))
+        rn = None
+        par = None
+        for i in range(dpb):
+            d = r[:, :, None, i] - cb[None, :, :, i]                  # [m, B, 16]
+            t_rn = d * d
+            t_par = (d * x[:, :, None, i]) * inv_norm[:, None, None]
+            rn = t_rn if rn is None else rn + t_rn
+            par = t_par if par is None else par + t_par
+        eta = _avq_parallel_cost_multiplier(float(threshold), sqn, dim)     # [m]
+        if torch is not None:
+            codes = torch.argmin(rn, dim=2)                                  # first minimum
+            rows = torch.arange(m, device=dev)
+            cur_par = torch.gather(par, 2, codes[:, :, None])[:, :, 0]
+            P = torch.zeros(m, dtype=torch.float64, device=dev)
+            for b in range(num_blocks):
+                P = P + cur_par[:, b]
+            cur_rn = torch.gather(rn, 2, codes[:, :, None])[:, :, 0]
+            order = torch.argsort(-cur_rn, dim=1, stable=True)
+            kidx = torch.arange(nc, device=dev)[None, :]
+            inf = torch.tensor(float("inf"), dtype=torch.float64, device=dev)
+            for _ in range(10):
+                for i in range(num_blocks):
+                    b = order[:, i]
+                    st_rn = rn[rows, b]                                      # [m, 16]
+                    st_par = par[rows, b]
+                    cur = codes[rows, b]
+                    old_rn = st_rn[rows, cur]
+                    old_par = st_par[rows, cur]
+                    new_p = (P - old_par)[:, None] + st_par
+                    pnd = new_p * new_p - (P * P)[:, None]
+                    rnd = st_rn - old_rn[:, None]
+                    cost = eta[:, None] * pnd + (rnd - pnd)
+                    ok = (pnd <= 0.0) & (kidx != cur[:, None])
+                    cost = torch.where(ok, cost, inf)
+                    best = torch.argmin(cost, dim=1)
+                    take = cost[rows, best] < 0.0
+                    codes[rows[take], b[take]] = best[take]
+                    P = torch.where(take, new_p[rows, best], P)
+            out[s:s + m] = codes.to(torch.uint8).cpu().numpy()
+        else:
+            codes = np.argmin(rn, axis=2)
+            rows = np.arange(m)
+            cur_par = np.take_along_axis(par, codes[:, :, None], 2)[:, :, 0]
+            P = np.zeros(m)
+            for b in range(num_blocks):
+                P = P + cur_par[:, b]
+            cur_rn = np.take_along_axis(rn, codes[:, :, None], 2)[:, :, 0]
+            order = np.argsort(-cur_rn, axis=1, kind="stable")
+            kidx = np.arange(nc)[None, :]
+            for _ in range(10):
+                for i in range(num_blocks):
+                    b = order[:, i]
+                    st_rn = rn[rows, b]
+                    st_par = par[rows, b]
+                    cur = codes[rows, b]
+                    old_rn = st_rn[rows, cur]
+                    old_par = st_par[rows, cur]
+                    new_p = (P - old_par)[:, None] + st_par
+                    pnd = new_p * new_p - (P * P)[:, None]
+                    rnd = st_rn - old_rn[:, None]
+                    cost = eta[:, None] * pnd + (rnd - pnd)
+                    ok = (pnd <= 0.0) & (kidx != cur[:, None])
+                    cost = np.where(ok, cost, np.inf)
+                    best = np.argmin(cost, axis=1)
+                    take = cost[rows, best] < 0.0
+                    codes[rows[take], b[take]] = best[take]
+                    P = np.where(take, new_p[rows, best], P)
+            out[s:s + m] = codes.astype(np.uint8)
+    return out
+
+
 def soar_assign(x: np.ndarray, centers: np.ndarray, primary: np.ndarray, lam: float,
                 chunk: int = 1 << 15) -> np.ndarray:
     """Secondary leaf per row with the SOAR loss (never the primary leaf)."""
@@ -171,7 +288,8 @@ def build_tree_ah(db: np.ndarray, metric: int, num_leaves: int,
                   training_iterations: int = 12, ah_training_iterations: int = 10,
                   ah_training_sample_size: int = 100000, residual: Optional[bool] = None,
                   keep_dataset: bool = True, soar_lambda: Optional[float] = None,
-                  overretrieve_factor: float = 2.0, seed: int = 0) -> TreeAHIndex:
+                  overretrieve_factor: float = 2.0, seed: int = 0,
+                  noise_shaping_threshold: Optional[float] = None) -> TreeAHIndex:
     db = np.ascontiguousarray(db, dtype=np.float32)
     n, dim = db.shape
     if residual is None:
@@ -197,7 +315,12 @@ def build_tree_ah(db: np.ndarray, metric: int, num_leaves: int,
     if resid.shape[0] > ah_training_sample_size:
         samp = resid[np.sort(rng.choice(resid.shape[0], ah_training_sample_size, replace=False))]
     codebook = train_codebook(samp, num_blocks, dims_per_block, ah_training_iterations, seed + 2)
-    codes = encode(resid, codebook)
+    if noise_shaping_threshold is not None and not math.isnan(noise_shaping_threshold):
+        # AVQ: the parallel direction is the datapoint's own (the original
+        # row, for a residual index and for a SOAR copy alike)
+        codes = encode_avq(resid, db[members], codebook, float(noise_shaping_threshold))
+    else:
+        codes = encode(resid, codebook)
     return TreeAHIndex(metric=metric, dim=dim, num_blocks=num_blocks,
                        dims_per_block=dims_per_block, residual=bool(residual),
                        centers=centers, codebook=codebook, leaf_offsets=offsets,

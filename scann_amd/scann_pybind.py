@@ -48,7 +48,7 @@ class ScannNumpy:
                 ah_training_sample_size=cfg.ah_training_sample_size,
                 residual=cfg.residual, keep_dataset=cfg.has_reordering,
                 soar_lambda=cfg.soar_lambda, overretrieve_factor=cfg.overretrieve_factor,
-                seed=seed)
+                seed=seed, noise_shaping_threshold=cfg.noise_shaping_threshold)
         self._config_text = config
         self._index = index
         self._native = _native.NativeIndex(index, device=device)
