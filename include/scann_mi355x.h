@@ -155,12 +155,26 @@ int smx_search_batched(smx_index* index, const float* queries, int32_t nq,
                        uint32_t* out_idx, float* out_dist, int32_t* out_count);
 
 /* Same with device buffers, enqueued on `stream` (hipStream_t; NULL = the
- * handle's own stream).  Synchronises only to check the candidate-buffer
- * overflow flag.  d_out_count may be NULL. */
+ * handle's own stream) with no host synchronisation: the results are ready
+ * when the stream reaches them (candidate-list overflow is handled on the
+ * device).  Calls on different streams are ordered after one another (the
+ * handle's workspace is shared).  d_out_count may be NULL. */
 int smx_search_batched_device(smx_index* index, const float* d_queries, int32_t nq,
                               int32_t dim, const smx_search_params* params,
                               uint32_t* d_out_idx, float* d_out_dist,
                               int32_t* d_out_count, void* stream);
+
+/* Single-query search (ScannNumpy::Search / ScannInterface::Search,
+ * scann_npy.cc, scann.cc; TreeAHHybridResidual::FindNeighborsImpl,
+ * tree_ah_hybrid_residual.cc:870-978) with host buffers: one query [dim],
+ * out_idx / out_dist [final_nn].  Its partition scores follow the
+ * single-query path's one-to-many order (kmeans_tree_node.h:159-163 ->
+ * one_to_many_symmetric.h:376-503), not the batched transposed chain, so its
+ * leaf biases -- and at exact ties its neighbors -- are those of the
+ * reference's search(), not of search_batched(). */
+int smx_search(smx_index* index, const float* query, int32_t dim,
+               const smx_search_params* params, uint32_t* out_idx, float* out_dist,
+               int32_t* out_count);
 
 /* ---- range-split shards -------------------------------
  * Each rank searches its shard, producing its exact local top-k' by (approx

@@ -17,6 +17,7 @@ _lib = None
 
 MODE_IDEAL = 0
 MODE_EMULATE = 1
+PARTITION_ONE_TO_MANY = 4   # or-ed into mode: the single-query partition scores
 
 _f32p = ctypes.POINTER(ctypes.c_float)
 _u32p = ctypes.POINTER(ctypes.c_uint32)

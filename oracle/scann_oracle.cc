@@ -610,7 +610,13 @@ static void QueryPreReorder(const IndexView& v, const float* q, int L,
   const orc_index* ix = v.ix;
   const int nl = ix->num_leaves, nb = ix->num_blocks, dim = ix->dim;
   scratch->resize(nl);
-  PartitionScoresOne(q, dim, ix->centers, nl, ix->metric, v.cnorms, scratch->data());
+  if (mode & ORC_PARTITION_ONE_TO_MANY) {
+    for (int c = 0; c < nl; ++c)
+      (*scratch)[c] = ExactDistance(q, ix->centers + size_t(c) * dim, dim, ix->metric);
+  } else {
+    PartitionScoresOne(q, dim, ix->centers, nl, ix->metric, v.cnorms, scratch->data());
+  }
+  mode &= 3;
   std::vector<int> leaves;
   std::vector<float> biases;
   TopL(scratch->data(), nl, L, &leaves, &biases);

@@ -26,6 +26,11 @@ extern "C" {
 
 enum { ORC_METRIC_DOT = 0, ORC_METRIC_SQUARED_L2 = 1 };
 enum { ORC_MODE_IDEAL = 0, ORC_MODE_EMULATE = 1 };
+/* or'ed into mode: partition scores of the single-query path (ScannInterface::
+ * Search -> KMeansTreeNode, kmeans_tree_node.h:159-163: DenseDistanceOneToMany,
+ * one_to_many_symmetric.h:376-503, the A.8 accumulator order of ExactDistance)
+ * instead of the batched transposed FMA chain. */
+enum { ORC_PARTITION_ONE_TO_MANY = 4 };
 
 /* Same field layout as smx_index_desc in include/scann_mi355x.h. */
 typedef struct orc_index {

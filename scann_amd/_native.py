@@ -50,6 +50,7 @@ SIGNATURES = {
     "smx_index_destroy": (ctypes.c_int, [_vp]),
     "smx_index_info": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "smx_search_batched": (ctypes.c_int, [_vp, _vp, _i32, _i32, ctypes.POINTER(SearchParams), _vp, _vp, _vp]),
+    "smx_search": (ctypes.c_int, [_vp, _vp, _i32, ctypes.POINTER(SearchParams), _vp, _vp, _vp]),
     "smx_search_batched_device": (ctypes.c_int, [_vp, _vp, _i32, _i32, ctypes.POINTER(SearchParams), _vp, _vp, _vp, _vp]),
     "smx_partition_topl": (ctypes.c_int, [_vp, _vp, _i32, _i32, _vp, _vp]),
     "smx_create_lookup_tables": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp]),
@@ -159,6 +160,20 @@ class NativeIndex:
                                           idx.ctypes.data, dist.ctypes.data, cnt.ctypes.data),
               "Error during search")
         return idx, dist, cnt
+
+    def search(self, query, leaves, pre_nn, final_nn, reorder=True):
+        """One query through the single-query numerics (smx_search)."""
+        q = _c(query, np.float32)
+        if q.ndim != 1:
+            raise ValueError("Query must be one-dimensional")
+        p = SearchParams(int(leaves), int(pre_nn), int(final_nn), int(bool(reorder)))
+        idx = np.zeros(final_nn, np.uint32)
+        dist = np.zeros(final_nn, np.float32)
+        cnt = np.zeros(1, np.int32)
+        check(self.lib.smx_search(self.h, q.ctypes.data, q.shape[0], ctypes.byref(p),
+                                  idx.ctypes.data, dist.ctypes.data, cnt.ctypes.data),
+              "Error during search")
+        return idx, dist, int(cnt[0])
 
     def search_batched_device(self, q_ptr, nq, leaves, pre_nn, final_nn, reorder,
                               out_idx_ptr, out_dist_ptr, out_count_ptr=None, stream=None):

@@ -216,6 +216,7 @@ struct FrontArgs {
   int8_t* lut = nullptr;            // [nq][2K][16]
   float* mult = nullptr;            // [nq]
   float* inv = nullptr;             // [nq]
+  int one_to_many = 0;              // the single-query partition scores (A.8 order)
 };
 hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int nq,
                                int L, int32_t* out_leaf, float* out_dist,

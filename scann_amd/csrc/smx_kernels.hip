@@ -1930,6 +1930,27 @@ __device__ float ExactDistance(const float* __restrict__ q, const float* __restr
   return r;
 }
 
+// Partition scores of the single-query path (ScannInterface::Search ->
+// KMeansTreeNode, kmeans_tree_node.h:159-163): DenseDistanceOneToMany, whose
+// AVX2 kernel (one_to_many_symmetric.h:376-503) accumulates each center in
+// the A.8 order of ExactDistance -- not the batched transposed FMA chain of
+// partition_scores_kernel, so its biases differ in the last bits.  One
+// thread per (query, center); also the per-call state reset.
+__global__ void __launch_bounds__(256) partition_scores_a8_kernel(
+    const float* __restrict__ queries, int nq, int dim, const float* __restrict__ centers,
+    int nl, int metric, float* __restrict__ scores, StateInit init) {
+  const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t gs = gridDim.x * blockDim.x;
+  for (uint32_t i = gt; i < init.n_counters; i += gs) init.counters[size_t(i) * kCounterStride] = 0u;
+  for (uint32_t i = gt; i < init.n_stats; i += gs) init.stats[i] = 0u;
+  for (uint32_t i = gt; i < init.n_cand; i += gs) init.cand_count[size_t(i) * kCounterStride] = 0u;
+  for (uint32_t i = gt; i < init.n_tau; i += gs) init.tau[i] = kNoThreshold;
+  const size_t p = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (p >= size_t(nq) * nl) return;
+  const int qi = int(p / nl), c = int(p % nl);
+  scores[p] = ExactDistance(queries + size_t(qi) * dim, centers + size_t(c) * dim, dim, metric);
+}
+
 // ---------------------------------------------------------------------------
 // Final selection per query: exact k' best by (distance, tie id) among the
 // candidates, tie -> global id, SOAR de-duplication, exact reorder, and the
@@ -2582,10 +2603,16 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   tail.rank = f.rank;
   tail.lut = LutParams{queries, ix.dim, ix.codebook, ix.nb, ix.dpb, 2 * ix.ksteps, ix.metric,
                        ix.residual, (dbg & 2) ? nullptr : f.lut, f.mult, f.inv, nullptr};
-  hipLaunchKernelGGL(partition_scores_kernel,
-                     dim3((nq + kPartTile - 1) / kPartTile, (ix.nl + kPartTile - 1) / kPartTile),
-                     dim3(256), 0, s, queries, nq, ix.dim, ix.centers, ix.cnorm, ix.nl, ix.metric,
-                     scores, f.init);
+  if (f.one_to_many) {
+    const size_t n = size_t(nq) * ix.nl;
+    hipLaunchKernelGGL(partition_scores_a8_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s,
+                       queries, nq, ix.dim, ix.centers, ix.nl, ix.metric, scores, f.init);
+  } else {
+    hipLaunchKernelGGL(partition_scores_kernel,
+                       dim3((nq + kPartTile - 1) / kPartTile, (ix.nl + kPartTile - 1) / kPartTile),
+                       dim3(256), 0, s, queries, nq, ix.dim, ix.centers, ix.cnorm, ix.nl, ix.metric,
+                       scores, f.init);
+  }
   // static LDS of the kernel besides the dynamic key buffers: the LUT build's
   // raw table and reduction (~5 KB) and the selection's words
   constexpr size_t kStaticLds = 6 * 1024;

@@ -393,7 +393,8 @@ float Elapsed(smx_index* h, int a, int b) {
 // reorder and output the pre-reorder set (width pre_nn).
 int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int final_nn,
               bool reorder, bool pre_only, uint32_t* out_idx, float* out_dist,
-              int32_t* out_count, hipStream_t s, smx::ShardEntry* shard_out = nullptr) {
+              int32_t* out_count, hipStream_t s, smx::ShardEntry* shard_out = nullptr,
+              bool single = false) {
   smx::DeviceIndex& ix = h->ix;
   if (nq == 0) return SMX_OK;
   L = std::min(L, ix.nl);
@@ -527,6 +528,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     f.lut = w.lut;
     f.mult = w.mult;
     f.inv = w.inv;
+    f.one_to_many = single ? 1 : 0;
     SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s, &f));
     Mark(h, 1, s);
     // Fork.  Side stream: the work list and the pairs' lane records; this
@@ -565,7 +567,8 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   if (h->use_graph && !h->profiling && s) {
     const uint64_t key[GraphKeyWords] = {
         uint64_t(reinterpret_cast<uintptr_t>(queries)), uint64_t(nq), uint64_t(L), uint64_t(pnn),
-        uint64_t(final_nn), uint64_t(reorder) | uint64_t(pre_only) << 1 | uint64_t(h->profiling) << 2,
+        uint64_t(final_nn), uint64_t(reorder) | uint64_t(pre_only) << 1 | uint64_t(h->profiling) << 2 |
+                                uint64_t(single) << 3,
         uint64_t(reinterpret_cast<uintptr_t>(out_idx)), uint64_t(reinterpret_cast<uintptr_t>(out_dist)),
         uint64_t(reinterpret_cast<uintptr_t>(out_count)), uint64_t(reinterpret_cast<uintptr_t>(shard_out)),
         uint64_t(reinterpret_cast<uintptr_t>(s)), w.gen, uint64_t(w.cap), uint64_t(seed),
@@ -803,9 +806,14 @@ int smx_search_batched_device(smx_index* h, const float* d_queries, int32_t nq, 
                    p->reorder != 0, false, d_out_idx, d_out_dist, d_out_count, s);
 }
 
-int smx_search_batched(smx_index* h, const float* queries, int32_t nq, int32_t dim,
-                       const smx_search_params* p, uint32_t* out_idx, float* out_dist,
-                       int32_t* out_count) {
+}  // extern "C"
+
+namespace {
+
+// Host-buffer search: queries in, (ids, distances, counts) out, synchronous.
+int SearchHost(smx_index* h, const float* queries, int32_t nq, int32_t dim,
+               const smx_search_params* p, uint32_t* out_idx, float* out_dist,
+               int32_t* out_count, bool single) {
   int rc = CheckSearchArgs(h, nq, dim, p);
   if (rc) return rc;
   if (nq > 0 && (!queries || !out_idx || !out_dist))
@@ -824,7 +832,7 @@ int smx_search_batched(smx_index* h, const float* queries, int32_t nq, int32_t d
   SMX_HIP(hipMemcpyAsync(w.queries, queries, sizeof(float) * size_t(nq) * dim,
                          hipMemcpyHostToDevice, s));
   rc = RunSearch(h, w.queries, nq, p->leaves_to_search, p->pre_reorder_nn, p->final_nn,
-                 p->reorder != 0, false, w.out_idx, w.out_dist, w.out_count, s);
+                 p->reorder != 0, false, w.out_idx, w.out_dist, w.out_count, s, nullptr, single);
   if (rc) return rc;
   SMX_HIP(hipMemcpyAsync(out_idx, w.out_idx, sizeof(uint32_t) * size_t(nq) * width,
                          hipMemcpyDeviceToHost, s));
@@ -834,6 +842,21 @@ int smx_search_batched(smx_index* h, const float* queries, int32_t nq, int32_t d
     SMX_HIP(hipMemcpyAsync(out_count, w.out_count, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, s));
   SMX_HIP(hipStreamSynchronize(s));
   return SMX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int smx_search_batched(smx_index* h, const float* queries, int32_t nq, int32_t dim,
+                       const smx_search_params* p, uint32_t* out_idx, float* out_dist,
+                       int32_t* out_count) {
+  return SearchHost(h, queries, nq, dim, p, out_idx, out_dist, out_count, false);
+}
+
+int smx_search(smx_index* h, const float* query, int32_t dim, const smx_search_params* p,
+               uint32_t* out_idx, float* out_dist, int32_t* out_count) {
+  return SearchHost(h, query, 1, dim, p, out_idx, out_dist, out_count, true);
 }
 
 int smx_shard_width(const smx_index* h, const smx_search_params* p, int32_t* out_k) {

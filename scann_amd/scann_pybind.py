@@ -77,12 +77,17 @@ class ScannNumpy:
         return idx, dist * np.float32(self._result_multiplier)
 
     def search(self, query, final_nn=-1, pre_reorder_nn=-1, leaves=-1):
+        """ScannNumpy::Search: one query through the single-query path's
+        numerics (one-to-many partition scores, smx_search)."""
         q = np.ascontiguousarray(query, dtype=np.float32)
         if q.ndim != 1:
             raise ValueError("Query must be one-dimensional")
-        idx, dist = self._run(q[None, :], final_nn, pre_reorder_nn, leaves)
-        keep = ~np.isnan(dist[0])
-        return idx[0][keep], dist[0][keep]
+        final_nn, pre, leaves = self._resolve(final_nn, pre_reorder_nn, leaves)
+        try:
+            idx, dist, n = self._native.search(q, leaves, pre, final_nn, self._cfg.has_reordering)
+        except _native.SmxError as e:
+            raise RuntimeError(f"Error during search: {e}") from None
+        return idx[:n], dist[:n] * np.float32(self._result_multiplier)
 
     def search_batched(self, queries, final_nn=-1, pre_reorder_nn=-1, leaves=-1,
                        parallel=False, batch_size=0):

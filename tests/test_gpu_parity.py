@@ -284,3 +284,21 @@ def test_device_entry_point_is_stream_ordered(native, oracle, small_dot):
     for oi_, od_ in outs:
         np.testing.assert_array_equal(oi_.cpu().numpy().view(np.uint32), oi)
         np.testing.assert_allclose(od_.cpu().numpy(), od, rtol=RTOL)
+
+
+@pytest.mark.parametrize("fix", ["small_dot", "small_l2"])
+@pytest.mark.parametrize("reorder", [False, True])
+def test_single_query_search_matches_oracle(native, oracle, fix, reorder, request):
+    """f4: search() (smx_search) scores partitions in the single-query
+    one-to-many order; against the oracle's PARTITION_ONE_TO_MANY mode the
+    ids and distance bits agree (without reorder the distances carry the
+    leaf biases, so the biases are pinned too)."""
+    ix, db, q = request.getfixturevalue(fix)
+    n = _nat(native, ix)
+    mode = oracle.MODE_IDEAL | oracle.PARTITION_ONE_TO_MANY
+    for i in range(12):
+        gi, gd, gc = n.search(q[i], 12, 100, 10, reorder)
+        oi, od, oc = oracle.search(ix, q[i:i + 1], 12, 100, 10, reorder, mode)
+        assert gc == int(oc[0])
+        np.testing.assert_array_equal(gi[:gc], oi[0, :gc])
+        np.testing.assert_array_equal(gd[:gc].view(np.uint32), od[0, :gc].view(np.uint32))
