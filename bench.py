@@ -63,6 +63,7 @@ CONFIGS = {
                  metric_name="QPS at recall@10, SIFT1M shape (BASELINE.json configs[2]), batch=1000"),
 }
 CFG = CONFIGS["glove"]
+SWEEP_LEAVES = (10, 20, 30, 40, 50, 60, 70, 80, 100, 150)
 
 
 def scan_k(num_blocks):
@@ -151,8 +152,14 @@ def cpu_baseline(ix, q, gpu_idx, threads):
     oracle.build()
     try:
         port = oracle.Avx2Port(ix)
-    except ValueError:   # pipeline B (non-residual): the oracle's C restatement
+    except ValueError:   # residual without the global top-N path: the C restatement
         return cpu_baseline_restatement(ix, q, gpu_idx, threads)
+    pipeline = ("pipeline A: tree_ah_hybrid_residual.cc batched path, leaves in "
+                "leaf_tokens_by_norm_ order, int16 truncated prefilter over the global "
+                "FastTopNeighbors" if ix.residual else
+                "pipeline B: tree_x_hybrid_smmd.cc optimized batched path, leaves in ascending "
+                "id, per-leaf FastTopNeighbors<int16_t> with the global epsilon at visit time, "
+                "merged into the global FastTopNeighbors<float>")
     model, isa = cpu_info()
     port.search(q, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True, threads)  # warm-up + calibration
     t = time.perf_counter()
@@ -174,6 +181,8 @@ def cpu_baseline(ix, q, gpu_idx, threads):
         # a phase's CPU seconds spread over the cores
         scan_runs.append(nqs * threads / max(scan_s, 1e-9))
         front_runs.append(nqs * threads / max(front_s, 1e-9))
+    # the port replays the reference's emulate semantics; the GPU computes the
+    # ideal exact top-k', so this is the emulate-vs-GPU id mismatch
     mismatch = float((out[0] != gpu_idx).mean())
     port.close()
     return dict(value=round(float(np.median(runs)), 1), unit="queries/s", cores=threads,
@@ -183,8 +192,9 @@ def cpu_baseline(ix, q, gpu_idx, threads):
                 front_only_qps=round(float(np.median(front_runs)), 1),
                 sample=f"median of 5 runs x {reps} repeats of the same {q.shape[0]}-query batch "
                        f"through the AVX2 port of the reference's batched tree-AH path "
-                       f"(oracle/lut16_avx2_port.cc: SearchBatchedParallel chunking, pshufb LUT16 "
-                       f"with int16 accumulation, emulate-mode FastTopNeighbors, partition scores "
+                       f"({pipeline}; oracle/lut16_avx2_port.cc: SearchBatchedParallel chunking, "
+                       f"pshufb LUT16 with int16 accumulation, emulate-mode FastTopNeighbors, "
+                       f"partition scores "
                        f"8 centers per AVX2 vector in the many-to-many order), {threads} threads "
                        f"= every core this process may use ({aff} in its affinity mask, capped "
                        f"by the cgroup CPU quota); scan_only_qps = the leaf scan phase alone "
@@ -220,6 +230,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="glove")
+    ap.add_argument("--no-sweep", action="store_true",
+                    help="skip the leaves_to_search QPS-recall operating points")
+    ap.add_argument("--sweep-steps", type=int, default=20)
     args = ap.parse_args()
     global CFG, LEAVES, LEAVES_TO_SEARCH
     CFG = CONFIGS[args.config]
@@ -251,8 +264,8 @@ def main():
     out_dist = torch.zeros((NQ, FINAL_NN), dtype=torch.float32, device=dev)
     out_cnt = torch.zeros(NQ, dtype=torch.int32, device=dev)
 
-    def step():
-        nat.search_batched_device(qd.data_ptr(), NQ, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True,
+    def step(leaves=LEAVES_TO_SEARCH):
+        nat.search_batched_device(qd.data_ptr(), NQ, leaves, PRE_NN, FINAL_NN, True,
                                   out_idx.data_ptr(), out_dist.data_ptr(), out_cnt.data_ptr())
 
     # timed steps: the library replays its captured hipGraph of the pipeline
@@ -299,6 +312,28 @@ def main():
     gidx = out_idx.cpu().numpy().astype(np.int64)
     truth = synthetic.brute_force_topk(db, q, FINAL_NN, CFG["metric"])
     recall = synthetic.recall_at_k(gidx, truth, FINAL_NN)
+
+    # QPS-recall operating points (QPS at the smallest
+    # leaves_to_search reaching recall@10 >= 0.95); the headline value stays
+    # at the configured leaves_to_search.  Same batch, same timing method.
+    points = []
+    if not args.no_sweep:
+        for lv in SWEEP_LEAVES:
+            if lv > LEAVES:
+                continue
+            for _ in range(3):
+                step(lv)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(args.sweep_steps):
+                step(lv)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+            r = synthetic.recall_at_k(out_idx.cpu().numpy().astype(np.int64), truth, FINAL_NN)
+            points.append({"leaves_to_search": lv, "qps": round(NQ * args.sweep_steps / dt, 1),
+                           "recall_at_10": round(r, 4)})
+        step()
+        torch.cuda.synchronize()
 
     avg_scan_ms = float(np.mean(scan_ms))
     bytes_per_launch = float(np.mean(scan_bytes))
@@ -363,6 +398,10 @@ def main():
                 "lookups_per_s": round(2.0 * bytes_per_launch / (avg_scan_ms * 1e-3), 1),
             },
             "stage_ms": {k: round(v, 4) for k, v in stage.items()},
+            "operating_points": points,
+            "qps_at_recall_0.95": next(({"leaves_to_search": p["leaves_to_search"],
+                                         "qps": p["qps"], "recall_at_10": p["recall_at_10"]}
+                                        for p in points if p["recall_at_10"] >= 0.95), None),
             "candidates_max": t_last["max_candidates"],
         }
         # full-size parity: oracle (ideal mode) on a query subset, ids must match

@@ -55,6 +55,9 @@ def lib():
         L.orc_exact_distance.restype = ctypes.c_float
         L.orc_fast_topn_replay.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp]
         L.orc_fast_topn_replay.restype = ctypes.c_int32
+        L.orc_fast_topn_replay_i16.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_int32,
+                                               ctypes.c_int16, vp, vp, vp]
+        L.orc_fast_topn_replay_i16.restype = ctypes.c_int32
         L.orc_avq_encode.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_int32,
                                      ctypes.c_int32, ctypes.c_double, vp]
         L.orc_avq_encode.restype = None
@@ -167,6 +170,18 @@ def fast_topn_replay(ids, dists, k):
     return oi[:n], od[:n], int(ngc[0])
 
 
+def fast_topn_replay_i16(ids, dists, k, epsilon=32767):
+    """FastTopNeighbors<int16_t>(k, epsilon) replay; FinishUnsorted storage order."""
+    ids, dists = _c(ids, np.uint32), _c(dists, np.int16)
+    oi = np.zeros(max(k, 1), np.uint32)
+    od = np.zeros(max(k, 1), np.int16)
+    ngc = np.zeros(1, np.int32)
+    n = lib().orc_fast_topn_replay_i16(ids.ctypes.data, dists.ctypes.data, len(ids), k,
+                                       int(epsilon), oi.ctypes.data, od.ctypes.data,
+                                       ngc.ctypes.data)
+    return oi[:n], od[:n], int(ngc[0])
+
+
 def avq_encode(residuals, originals, codebook, threshold):
     """The oracle's row-by-row AVQ noise-shaped encoding, uint8 [n, B]."""
     r = _c(residuals, np.float32)
@@ -187,7 +202,7 @@ class Avx2Port:
         self._desc = index.desc()
         self._h = lib().orc_avx2_prepare(ctypes.byref(self._desc))
         if not self._h:
-            raise ValueError("index not covered by the AVX2 port (needs residual + global top-N)")
+            raise ValueError("index not covered by the AVX2 port (residual indexes need the global top-N path)")
 
     def search(self, queries, leaves, pre_nn, final_nn, reorder=True, nthreads=8):
         q = _c(queries, np.float32)

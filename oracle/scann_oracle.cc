@@ -192,10 +192,12 @@ static inline int32_t Accumulate(const uint8_t* codes, int nb,
 }
 
 // ---------------------------------------------------------------------------
-// FastTopNeighbors<float, uint32_t> replay (A.6).  Storage mirrors the
-// reference's sizes so that reads of stale slots beyond sz
-// (UseMasksToFindNewMedian) see the same kind of data; initial contents are
-// zero here (uninitialised in the reference: unpinnable).
+// FastTopNeighbors<DistT, uint32_t> replay (A.6) for DistT = float (the
+// global top-N of both pipelines) and int16_t (pipeline B's per-leaf top-N,
+// querying.h:403-462).  Storage mirrors the reference's sizes so that reads
+// of stale slots beyond sz (UseMasksToFindNewMedian) see the same kind of
+// data; initial contents are zero here (uninitialised in the reference:
+// unpinnable).
 // ---------------------------------------------------------------------------
 static inline uint32_t FinalMask32(size_t n) {
   const size_t r = n % 32;
@@ -204,28 +206,43 @@ static inline uint32_t FinalMask32(size_t n) {
 static inline int Ctz(uint32_t x) { return __builtin_ctz(x); }
 static inline int Popc(uint32_t x) { return __builtin_popcount(x); }
 
-static inline bool CompIV(uint32_t ia, uint32_t ib, float va, float vb) {
-  if (va == vb || std::isunordered(va, vb)) return ia < ib;
+// MaxOrInfinity / DecrementThreshold (fast_top_neighbors_impl.inc:243-251).
+template <typename V> struct DistTraits;
+template <> struct DistTraits<float> {
+  static float Max() { return kInf; }
+  static float Decrement(float t) { return std::nextafter(t, -kInf); }
+};
+template <> struct DistTraits<int16_t> {
+  static int16_t Max() { return std::numeric_limits<int16_t>::max(); }
+  static int16_t Decrement(int16_t t) { return static_cast<int16_t>(t - 1); }
+};
+
+template <typename V>
+static inline bool CompIV(uint32_t ia, uint32_t ib, V va, V vb) {
+  if (va == vb || va != va || vb != vb) return ia < ib;  // equal or unordered
   return va < vb;
 }
-static inline void ZipSwap(size_t a, size_t b, uint32_t* ind, float* val) {
+template <typename V>
+static inline void ZipSwap(size_t a, size_t b, uint32_t* ind, V* val) {
   std::swap(ind[a], ind[b]);
   std::swap(val[a], val[b]);
 }
-static inline float Median3(float v0, float v1, float v2) {
-  const float big = std::max(v0, v1);
-  const float sml = std::min(v0, v1);
+template <typename V>
+static inline V Median3(V v0, V v1, V v2) {
+  const V big = std::max(v0, v1);
+  const V sml = std::min(v0, v1);
   return std::max(sml, std::min(big, v2));
 }
 
 // CalculateSwapMasks (fast_top_neighbors_impl.inc:1-24).
-static size_t SwapMasks(bool eq, const float* val, uint32_t* masks, size_t nm,
-                        uint32_t final_mask, float thr) {
+template <typename V>
+static size_t SwapMasks(bool eq, const V* val, uint32_t* masks, size_t nm,
+                        uint32_t final_mask, V thr) {
   size_t kept = 0;
   for (size_t j = 0; j < nm; ++j) {
     uint32_t m = 0;
     for (int l = 0; l < 32; ++l) {
-      const float v = val[32 * j + l];
+      const V v = val[32 * j + l];
       const bool bit = eq ? (v == thr) : (v < thr);
       m |= uint32_t(bit) << l;
     }
@@ -240,7 +257,8 @@ static size_t SwapMasks(bool eq, const float* val, uint32_t* masks, size_t nm,
 }
 
 // UseMasksToPartition (:44-93).
-static size_t PartitionByMasks(uint32_t* ind, float* val, const uint32_t* masks,
+template <typename V>
+static size_t PartitionByMasks(uint32_t* ind, V* val, const uint32_t* masks,
                                size_t nm) {
   size_t i1 = 0, i2 = nm - 1;
   uint32_t m1 = ~masks[i1];
@@ -277,11 +295,12 @@ static size_t PartitionByMasks(uint32_t* ind, float* val, const uint32_t* masks,
   return w;
 }
 
-// UseMasksToCompact on AVX2 = HwyCompact (hwy-compact.cc:41-66): for every
-// 8-lane slice, Compress (selected lanes first, then the unselected ones in
-// order: CompressIsPartition for 32-bit lanes) stored unaligned at the write
-// cursor.  Order preserving for the kept elements.
-static size_t CompactByMasks(uint32_t* ind, float* val, const uint32_t* masks,
+// UseMasksToCompact for <uint32_t, float> on AVX2 = HwyCompact
+// (hwy-compact.cc:41-66): for every 8-lane slice, Compress (selected lanes
+// first, then the unselected ones in order: CompressIsPartition for 32-bit
+// lanes) stored unaligned at the write cursor.  Order preserving for the
+// kept elements.
+static size_t CompactByMasks(uint32_t* ind, float* val, uint32_t* masks,
                              size_t nm) {
   size_t w = 0;
   for (size_t j = 0; j < nm; ++j) {
@@ -303,6 +322,70 @@ static size_t CompactByMasks(uint32_t* ind, float* val, const uint32_t* masks,
   return w;
 }
 
+// UseMasksToCompact for every other type (fast_top_neighbors_impl.inc:
+// 189-202): UseMaskToCompact for one mask (:96-108), otherwise
+// UseMasksToCompactDoublePorted (:110-187) -- the first two 32-lane chunks
+// are copied behind the last one, then chunks 2, 3, ... are drained two
+// streams at a time (one element of the later chunk, then one of the
+// earlier), which does NOT preserve the kept elements' order.
+template <typename V>
+static size_t CompactByMasks(uint32_t* ind, V* val, uint32_t* masks, size_t nm) {
+  size_t w = 0;
+  if (nm == 1) {
+    uint32_t m = masks[0];
+    while (m) {
+      const int o = Ctz(m);
+      m &= m - 1;
+      ind[w] = ind[o];
+      val[w] = val[o];
+      ++w;
+    }
+    return w;
+  }
+  std::copy(val, val + 64, val + nm * 32);
+  std::copy(ind, ind + 64, ind + nm * 32);
+  masks[nm] = masks[0];
+  masks[nm + 1] = masks[1];
+  const size_t end = nm + 2;
+  uint32_t m1 = masks[2], m2 = masks[3];
+  size_t b1 = 2 * 32, b2 = 3 * 32, mp = 3;
+  for (;;) {
+    if (!m1 || !m2) {
+      bool cooldown = false;
+      do {
+        if (!m1) {
+          m1 = m2;
+          b1 = b2;
+        }
+        if (++mp >= end) {
+          cooldown = true;
+          break;
+        }
+        m2 = masks[mp];
+        b2 += 32;
+      } while (!m1 || !m2);
+      if (cooldown) break;
+    }
+    const int o2 = Ctz(m2), o1 = Ctz(m1);
+    ind[w] = ind[b2 + o2];
+    val[w] = val[b2 + o2];
+    ++w;
+    ind[w] = ind[b1 + o1];
+    val[w] = val[b1 + o1];
+    ++w;
+    m2 &= m2 - 1;
+    m1 &= m1 - 1;
+  }
+  while (m1) {
+    const int o1 = Ctz(m1);
+    m1 &= m1 - 1;
+    ind[w] = ind[b1 + o1];
+    val[w] = val[b1 + o1];
+    ++w;
+  }
+  return w;
+}
+
 static size_t SelectByMasks(uint32_t* to, const uint32_t* from,
                             const uint32_t* masks, size_t nm) {
   size_t w = 0;
@@ -317,10 +400,11 @@ static size_t SelectByMasks(uint32_t* to, const uint32_t* from,
   return w;
 }
 
-static float NewMedian(const float* val, const uint32_t* lt, const uint32_t* eq,
-                       size_t nm) {
+template <typename V>
+static V NewMedian(const V* val, const uint32_t* lt, const uint32_t* eq,
+                   size_t nm) {
   size_t n = 0;
-  float v[3] = {0, 0, 0};
+  V v[3] = {0, 0, 0};
   for (size_t j = 0; j < nm; ++j) {
     uint32_t m = ~(lt[j] + eq[j]);
     while (m) {
@@ -334,9 +418,10 @@ static float NewMedian(const float* val, const uint32_t* lt, const uint32_t* eq,
 }
 
 // ApproxNthElementImpl (fast_top_neighbors_impl.inc:253-391).
+template <typename V>
 static size_t ApproxNth(size_t keep_min, size_t keep_max, size_t sz,
-                        uint32_t* ind, float* val, uint32_t* masks) {
-  float thr = 0.0f;
+                        uint32_t* ind, V* val, uint32_t* masks) {
+  V thr = 0;
   size_t already = 0;
   bool skip = false;
   for (;;) {
@@ -395,7 +480,7 @@ static size_t ApproxNth(size_t keep_min, size_t keep_max, size_t sz,
       n_kept = keep_min;
       tiebreak = scratch[n_needed - 1];
     } else {
-      thr = std::nextafter(thr, -kInf);
+      thr = DistTraits<V>::Decrement(thr);
     }
     val[n_kept] = thr;
     ind[n_kept] = tiebreak;
@@ -403,26 +488,24 @@ static size_t ApproxNth(size_t keep_min, size_t keep_max, size_t sz,
   }
 }
 
-class FastTopN {
+template <typename V>
+class FastTopNT {
  public:
-  explicit FastTopN(size_t k, float eps = kInf) : k_(k), eps_(eps) {
-    const size_t no_realloc = (eps < kInf) ? 128 : 16384;
-    if (k == 0) {
-      cap_ = 32;
-    } else {
-      // k > no_realloc reallocates progressively in the reference
-      // (ReallocateForPureEnn); the oracle allocates the final size.
-      cap_ = ((2 * k + 31) / 32) * 32;
-      (void)no_realloc;
-    }
+  // Init (fast_top_neighbors.h:90-120).  A finite epsilon limits the
+  // no-realloc size to 128 results; beyond it the reference grows the
+  // arrays by doubling (ReallocateForPureEnn, :505-530) without collecting,
+  // so the first GC happens at the same push as with the final capacity,
+  // which is allocated here at once.
+  explicit FastTopNT(size_t k, V eps = DistTraits<V>::Max()) : k_(k), eps_(eps) {
+    cap_ = (k == 0) ? 32 : ((2 * k + 31) / 32) * 32;
     ind_.assign(2 * cap_ + 96, 0);
-    val_.assign(cap_ + 96, 0.0f);
+    val_.assign(cap_ + 96, V(0));
     masks_.assign(2 * cap_ / 32 + 2, 0);
   }
-  float epsilon() const { return eps_; }
+  V epsilon() const { return eps_; }
   size_t size() const { return sz_; }
   // PushNoEpsilonCheck: returns true when the buffer is full (GC needed).
-  bool Push(uint32_t i, float d) {
+  bool Push(uint32_t i, V d) {
     ind_[sz_] = i;
     val_[sz_] = d;
     ++sz_;
@@ -432,7 +515,8 @@ class FastTopN {
     ++num_gc_;
     Gc(k_, (k_ + cap_) / 2 - 1);
   }
-  void Finish(std::vector<std::pair<uint32_t, float>>* out) {
+  // FinishUnsorted (fast_top_neighbors.h:176-183): GC(k, k), storage order.
+  void Finish(std::vector<std::pair<uint32_t, V>>* out) {
     Gc(k_, k_);
     out->resize(sz_);
     for (size_t i = 0; i < sz_; ++i) (*out)[i] = {ind_[i], val_[i]};
@@ -440,6 +524,7 @@ class FastTopN {
   int num_gc() const { return num_gc_; }
 
  private:
+  // GarbageCollect (fast_top_neighbors.h:530-547).
   void Gc(size_t keep_min, size_t keep_max) {
     if (keep_min == 0) {
       sz_ = 0;
@@ -451,12 +536,13 @@ class FastTopN {
     eps_ = val_[sz_];
   }
   size_t k_, cap_, sz_ = 0;
-  float eps_;
+  V eps_;
   int num_gc_ = 0;
   std::vector<uint32_t> ind_;
-  std::vector<float> val_;
+  std::vector<V> val_;
   std::vector<uint32_t> masks_;
 };
+using FastTopN = FastTopNT<float>;
 
 // GetInt16Threshold over (epsilon - bias) * mult (lut16_avx2.inc:397-401,
 // 432-438, 515-519): float min against 32767 then C++ truncation.  Values
@@ -603,6 +689,93 @@ static int32_t SpillK(const IndexView& v, int32_t k) {
   return static_cast<int32_t>(r);
 }
 
+// Pipeline B's per-leaf int16 epsilon: ComputePossiblyFixedPointMaxDistance
+// (asymmetric_hashing_impl.h:207-219) of the global epsilon, then
+// min(., int16 max - 1) + 1 (querying.h:413-423), narrowed to int16 by the
+// FastTopNeighbors<int16_t> constructor.
+static int16_t LeafInt16Epsilon(float eps, float mult) {
+  constexpr int32_t kI32Max = std::numeric_limits<int32_t>::max();
+  int32_t e;
+  if (eps == kInf) {
+    e = kI32Max;
+  } else {
+    const float x = eps * mult;
+    if (x >= static_cast<float>(kI32Max)) {
+      e = kI32Max;
+    } else {
+      const float f = std::floor(x);
+      e = f < -2147483648.0f ? std::numeric_limits<int32_t>::min() : static_cast<int32_t>(f);
+    }
+  }
+  e = std::min<int32_t>(e, std::numeric_limits<int16_t>::max() - 1) + 1;
+  return static_cast<int16_t>(e);
+}
+
+// Pipeline B emulate mode (A.9): the replay of one query through
+// TreeXHybridSMMD::FindNeighborsPreTokenizedBatchedOptimizedImpl
+// (tree_x_hybrid_smmd.cc:718-790), the path the reference takes whenever
+// nq * leaves_to_search >= num_leaves (:660-667).  Leaves are visited in
+// ascending leaf id (InvertQueryTokens, :690-704).  Per leaf: the leaf
+// parameters take the global top-N's epsilon at visit time
+// (CreateParamsSubsetForLeaf, batching.h:96-116); the leaf's AH searcher
+// keeps a FastTopNeighbors<int16_t>(k', eps16) over the raw int16 sums,
+// pushing iff sum < threshold and re-reading the threshold after every GC
+// (GetTopInt16DistancesImpl, lut16_avx2.inc:308-389); FinishUnsorted's
+// contents, scaled by the float reciprocal 1.0f / mult (querying.h:446-455),
+// are pushed in storage order into the global FastTopNeighbors<float> iff
+// d <= epsilon (SingleMachineSearcherBase::FindNeighborsBatchedImpl,
+// single_machine_base.cc:759-808), local ids mapped to global ids.
+// The generic per-query path (nq * L < num_leaves) is not restated.
+static void PipelineBEmulate(const IndexView& v, const std::vector<int>& leaves,
+                             const Lut& lut, float inv, int32_t kk, NN* out) {
+  const orc_index* ix = v.ix;
+  const int nb = ix->num_blocks;
+  std::vector<int> ord(leaves);
+  std::sort(ord.begin(), ord.end());
+  const size_t k = size_t(std::max(kk, 0));
+  FastTopN top(k);  // pre_reordering_epsilon = +inf
+  std::vector<std::pair<uint32_t, int16_t>> local;
+  int32_t acc[32];
+  for (int leaf : ord) {
+    const uint64_t beg = ix->leaf_offsets[leaf];
+    const uint32_t n = uint32_t(ix->leaf_offsets[leaf + 1] - beg);
+    if (n == 0 || k == 0) continue;
+    FastTopNT<int16_t> lt(k, LeafInt16Epsilon(top.epsilon(), lut.mult));
+    int32_t thr = lt.epsilon();
+    const uint32_t groups = (n + 31) / 32;
+    for (uint32_t g = 0; g < groups; ++g) {
+      const int lanes = (g == groups - 1) ? int(n - 32 * g) : 32;
+      for (int l = 0; l < lanes; ++l)
+        acc[l] = Accumulate(ix->member_codes + (beg + 32 * g + l) * nb, nb, lut.u8.data());
+      auto push_mask = [&]() {
+        uint32_t pm = 0;
+        for (int l = 0; l < lanes; ++l) pm |= uint32_t(acc[l] < thr) << l;
+        return pm;
+      };
+      uint32_t pm = push_mask();
+      while (pm) {
+        const int l = Ctz(pm);
+        pm &= pm - 1;
+        if (lt.Push(32 * g + l, static_cast<int16_t>(acc[l]))) {
+          lt.GarbageCollectApprox();
+          thr = lt.epsilon();
+          pm &= push_mask();
+        }
+      }
+    }
+    lt.Finish(&local);
+    float eps = top.epsilon();
+    for (const auto& e : local) {
+      const float d = static_cast<float>(e.second) * inv;
+      if (d <= eps && top.Push(ix->leaf_members[beg + e.first], d)) {
+        top.GarbageCollectApprox();
+        eps = top.epsilon();
+      }
+    }
+  }
+  top.Finish(out);
+}
+
 // One query's pre-reorder candidates (global ids), unsorted.
 static void QueryPreReorder(const IndexView& v, const float* q, int L,
                             int pre_nn, int mode, std::vector<float>* scratch,
@@ -685,6 +858,8 @@ static void QueryPreReorder(const IndexView& v, const float* q, int L,
       p.first = ix->leaf_members[ix->leaf_offsets[leaf] + local];
     }
     *out = std::move(res);
+  } else if (mode == ORC_MODE_EMULATE && !residual) {
+    PipelineBEmulate(v, leaves, lut, inv, kk, out);
   } else {
     // Ideal: exact top-k' by (distance, tie id) over every scanned point.
     std::vector<Cand> cands;
@@ -900,6 +1075,28 @@ int32_t orc_fast_topn_replay(const uint32_t* idx, const float* dist, int32_t n,
   return int32_t(r.size());
 }
 
+int32_t orc_fast_topn_replay_i16(const uint32_t* idx, const int16_t* dist, int32_t n,
+                                 int32_t k, int16_t epsilon, uint32_t* out_idx,
+                                 int16_t* out_dist, int32_t* out_num_gc) {
+  // GetTopInt16DistancesImpl's push loop (lut16_avx2.inc:352-375) on one
+  // FastTopNeighbors<int16_t>(k, epsilon): push iff dist < epsilon, the
+  // threshold re-read after every GC; FinishUnsorted's storage order out.
+  orc::FastTopNT<int16_t> top(size_t(k), epsilon);
+  for (int32_t i = 0; i < n; ++i) {
+    if (dist[i] < top.epsilon()) {
+      if (top.Push(idx[i], dist[i])) top.GarbageCollectApprox();
+    }
+  }
+  std::vector<std::pair<uint32_t, int16_t>> r;
+  top.Finish(&r);
+  for (size_t i = 0; i < r.size(); ++i) {
+    out_idx[i] = r[i].first;
+    out_dist[i] = r[i].second;
+  }
+  if (out_num_gc) *out_num_gc = top.num_gc();
+  return int32_t(r.size());
+}
+
 // AVQ noise-shaped encoding of n rows: IndexDatapointNoiseShaped
 // (asymmetric_hashing_impl.cc:434-503) with ComputeResidualStats (:300-343,
 // ComputeResidualStatsForCluster :283-298), ComputeParallelCostMultiplier
@@ -1007,6 +1204,7 @@ using PartFn = void (*)(const float* q, int dim, const float* ct, int nlp, int n
 
 struct Prepared {
   const orc_index* ix;
+  bool pipeline_b = false;                   // non-residual: tree_x_hybrid_smmd
   orc::IndexView view;
   std::vector<std::vector<uint8_t>> packed;  // per leaf, reference layout
   std::vector<int> leaf_order;               // leaf_tokens_by_norm_
@@ -1015,11 +1213,12 @@ struct Prepared {
 };
 
 void* Prepare(const orc_index* ix) {
-  if (!ix || !ix->residual) return nullptr;
+  if (!ix) return nullptr;
   auto* p = new Prepared;
   p->ix = ix;
+  p->pipeline_b = !ix->residual;
   orc::BuildView(ix, &p->view);
-  if (p->view.shift == 0) {
+  if (!p->pipeline_b && p->view.shift == 0) {
     delete p;
     return nullptr;
   }
@@ -1031,8 +1230,11 @@ void* Prepare(const orc_index* ix) {
     p->packed[l].assign(size_t(nb) * ((n + 31) / 32) * 16, 0);
     orc_pack_codes(ix->member_codes + beg * nb, n, nb, p->packed[l].data());
   }
+  // Pipeline A visits leaves in leaf_tokens_by_norm_ order, pipeline B in
+  // ascending leaf id (tree_x_hybrid_smmd.cc:761).
   p->leaf_order.resize(nl);
-  for (int l = 0; l < nl; ++l) p->leaf_order[p->view.leaf_rank_by_norm[l]] = l;
+  for (int l = 0; l < nl; ++l)
+    p->leaf_order[p->pipeline_b ? l : p->view.leaf_rank_by_norm[l]] = l;
   const int dim = ix->dim;
   p->nlp = (nl + 7) & ~7;
   p->ct.assign(size_t(dim) * p->nlp, 0.0f);
@@ -1094,12 +1296,72 @@ int Run(void* prepared, const float* queries, int nq, int leaves, int pre_nn,
       for (size_t i = 0; i < lf.size(); ++i) by_leaf[lf[i]].push_back({j, sc[i]});
       orc::CreateLut(q, dim, ix->codebook, nb, ix->dims_per_block, ix->metric,
                      nullptr, &luts[j]);
-      invs[j] = static_cast<float>(1.0 / static_cast<double>(luts[j].mult));
+      invs[j] = P->pipeline_b ? 1.0f / luts[j].mult
+                              : static_cast<float>(1.0 / static_cast<double>(luts[j].mult));
       tops.emplace_back(size_t(kk));
     }
     const double c1 = cpu_now();
     int16_t acc[32];
+    if (P->pipeline_b) {
+      // orc::PipelineBEmulate's pushes, leaf-major: per leaf, batches of
+      // <= 3 queries share each code group load (searcher.cc:332-416).
+      std::vector<orc::FastTopNT<int16_t>> lts;
+      std::vector<std::pair<uint32_t, int16_t>> local;
+      for (int leaf : P->leaf_order) {
+        const auto& ql = by_leaf[leaf];
+        const uint64_t beg = ix->leaf_offsets[leaf];
+        const uint32_t n = uint32_t(ix->leaf_offsets[leaf + 1] - beg);
+        if (ql.empty() || n == 0 || kk <= 0) continue;
+        const uint8_t* packed = P->packed[leaf].data();
+        const uint32_t groups = (n + 31) / 32;
+        const uint32_t fmask = orc::FinalMask32(n);
+        for (size_t bs = 0; bs < ql.size();) {
+          const size_t left = ql.size() - bs;
+          const size_t nbatch = left <= 3 ? left : (left >= 6 ? 3 : left / 2);
+          lts.clear();
+          int16_t thr[3];
+          for (size_t t = 0; t < nbatch; ++t) {
+            const int j = ql[bs + t].first;
+            lts.emplace_back(size_t(kk), orc::LeafInt16Epsilon(tops[j].epsilon(), luts[j].mult));
+            thr[t] = lts[t].epsilon();
+          }
+          for (uint32_t g = 0; g < groups; ++g) {
+            const uint8_t* grp = packed + size_t(g) * 16 * nb;
+            for (size_t t = 0; t < nbatch; ++t) {
+              const int j = ql[bs + t].first;
+              group_fn(grp, nb, luts[j].u8.data(), acc);
+              uint32_t pm = mask_fn(acc, thr[t]);
+              if (!pm) continue;
+              if (g == groups - 1) pm &= fmask;
+              while (pm) {
+                const int l = orc::Ctz(pm);
+                pm &= pm - 1;
+                if (lts[t].Push(g * 32 + l, acc[l])) {
+                  lts[t].GarbageCollectApprox();
+                  thr[t] = lts[t].epsilon();
+                  pm &= mask_fn(acc, thr[t]);
+                }
+              }
+            }
+          }
+          for (size_t t = 0; t < nbatch; ++t) {
+            const int j = ql[bs + t].first;
+            lts[t].Finish(&local);
+            float eps = tops[j].epsilon();
+            for (const auto& e : local) {
+              const float d = static_cast<float>(e.second) * invs[j];
+              if (d <= eps && tops[j].Push(ix->leaf_members[beg + e.first], d)) {
+                tops[j].GarbageCollectApprox();
+                eps = tops[j].epsilon();
+              }
+            }
+          }
+          bs += nbatch;
+        }
+      }
+    }
     for (int leaf : P->leaf_order) {
+      if (P->pipeline_b) break;
       const auto& ql = by_leaf[leaf];
       if (ql.empty()) continue;
       const uint32_t n = uint32_t(ix->leaf_offsets[leaf + 1] - ix->leaf_offsets[leaf]);
@@ -1149,6 +1411,7 @@ int Run(void* prepared, const float* queries, int nq, int leaves, int pre_nn,
       orc::NN r;
       tops[j].Finish(&r);
       for (auto& p : r) {
+        if (P->pipeline_b) break;  // global ids already
         const uint32_t leaf = p.first >> shift;
         const uint32_t local = p.first & ((1u << shift) - 1);
         p.first = ix->leaf_members[ix->leaf_offsets[leaf] + local];

@@ -89,7 +89,10 @@ int32_t orc_global_topn_shift(const orc_index* idx);
  * tree_ah_hybrid_residual.cc:631-846, or tree_x_hybrid_smmd.cc:718-790 for
  * non-residual indexes).  mode: ORC_MODE_IDEAL (exact top-k by the
  * reference's total order) or ORC_MODE_EMULATE (sequential AVX2 replay with
- * FastTopNeighbors GC and the int16 truncated prefilter).
+ * FastTopNeighbors GC: pipeline A's int16 truncated prefilter over the
+ * global top-N, or pipeline B's per-leaf int16 FastTopNeighbors merged into
+ * the global top-N at leaf-visit time; residual indexes without the global
+ * top-N path fall back to IDEAL).
  * final_nn/pre_nn/leaves follow scann.cc:406-430: reorder happens iff
  * idx->dataset != NULL and do_reorder != 0.
  * Outputs [nq][final_nn] (padded with idx 0 / NaN), counts [nq].
@@ -118,6 +121,13 @@ int32_t orc_fast_topn_replay(const uint32_t* idx, const float* dist,
                              int32_t n, int32_t k, uint32_t* out_idx,
                              float* out_dist, int32_t* out_num_gc);
 
+/* FastTopNeighbors<int16_t> replay (pipeline B's per-leaf top-N,
+ * querying.h:403-462): push iff dist < epsilon; FinishUnsorted order out. */
+int32_t orc_fast_topn_replay_i16(const uint32_t* idx, const int16_t* dist,
+                                 int32_t n, int32_t k, int16_t epsilon,
+                                 uint32_t* out_idx, int16_t* out_dist,
+                                 int32_t* out_num_gc);
+
 /* AVQ noise-shaped AH encoding (IndexDatapointNoiseShaped,
  * asymmetric_hashing_impl.cc:434-503) of n rows: residuals and the original
  * rows [n][dim], codebook [nb][16][dpb], threshold T; codes [n][nb]. */
@@ -130,8 +140,10 @@ void orc_avq_encode(const float* residuals, const float* originals, int32_t n, i
  * (scann.cc:478-501).  Used only as bench.py's cpu_baseline.
  * orc_avx2_prepare packs every leaf into the reference layout once (the
  * reference does this when it builds its leaf searchers, searcher.cc:108-111)
- * and returns NULL for indexes the port does not cover (non-residual, or the
- * global top-N path disabled).  orc_search_avx2 returns -2 if the library was
+ * and returns NULL for indexes the port does not cover (residual with the
+ * global top-N path disabled).  Non-residual indexes run pipeline B's
+ * emulate semantics (tree_x_hybrid_smmd.cc:718-790, per-leaf int16
+ * FastTopNeighbors), residual ones pipeline A's.  orc_search_avx2 returns -2 if the library was
  * built without AVX2.  Partition scoring runs eight centers per AVX2 vector
  * over transposed centers (the reference's many-to-many order), bit-equal to
  * the scalar chain. */

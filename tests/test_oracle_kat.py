@@ -194,3 +194,22 @@ def test_fast_topn_replay_exact_after_gc(oracle):
     order = np.lexsort((ids, d))[:20]
     assert oi.tolist() == ids[order].tolist()
     assert ngc >= 1
+
+
+@pytest.mark.parametrize("k,n,span,eps", [(20, 600, 12, 32767), (100, 3000, 40, 32767),
+                                          (7, 500, 5, 3), (150, 2000, 400, 300)])
+def test_fast_topn_int16_replay_exact_set(oracle, k, n, span, eps):
+    """Pipeline B's per-leaf FastTopNeighbors<int16_t> (querying.h:403-462):
+    ids pushed in ascending order (local datapoint order), heavy ties; the
+    finished set is the exact top-k by (value, id) of the values < eps, the
+    GC (with the two-stream DoublePorted compaction) having run."""
+    rng = np.random.default_rng(k + n)
+    ids = np.arange(n, dtype=np.uint32)
+    d = rng.integers(0, span, n).astype(np.int16)
+    oi, od, ngc = oracle.fast_topn_replay_i16(ids, d, k, eps)
+    keep = d < eps
+    order = np.lexsort((ids[keep], d[keep]))[:k]
+    assert sorted(zip(od.tolist(), oi.tolist())) == \
+        sorted(zip(d[keep][order].tolist(), ids[keep][order].tolist()))
+    if keep.sum() >= 2 * k:
+        assert ngc >= 1

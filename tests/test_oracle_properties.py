@@ -93,3 +93,55 @@ def test_soar_dedupe_and_spilled_members(oracle):
         row = gi[r, :gc[r]].tolist()
         assert len(row) == len(set(row))          # no duplicate ids after dedupe
         assert list(gd[r, :gc[r]]) == sorted(gd[r, :gc[r]])
+
+
+def _pipeline_b(n=20000, leaves=64, seed=9):
+    ix, db, q = make_index(n=n, d=32, leaves=leaves, metric=1, seed=seed, components=100)
+    assert not ix.residual
+    return ix, db, q
+
+
+@pytest.mark.parametrize("reorder", [True, False])
+def test_avx2_port_equals_emulate_pipeline_b(oracle, reorder):
+    """The port's leaf-major pipeline-B loop (per-leaf int16 top-N merged at
+    visit time, tree_x_hybrid_smmd.cc:718-790) equals the oracle's per-query
+    replay bit for bit (64 queries x 12 leaves >= 64 leaves: the reference's
+    optimized batched path)."""
+    ix, db, q = _pipeline_b()
+    port = oracle.Avx2Port(ix)
+    for nthreads in (1, 4):
+        pi, pd, pc = port.search(q, 12, 100, 10, reorder, nthreads)
+        ei, ed, ec = oracle.search(ix, q, 12, 100, 10, reorder, oracle.MODE_EMULATE)
+        np.testing.assert_array_equal(pi, ei)
+        np.testing.assert_array_equal(pd.view(np.uint32), ed.view(np.uint32))
+        np.testing.assert_array_equal(pc, ec)
+
+
+def test_emulate_vs_ideal_pipeline_b(oracle):
+    """A.9: pipeline B's emulate result (int16 per-leaf epsilon from the
+    global top-k at visit time) against the ideal exact top-k'.  Every
+    emulate distance is a genuine candidate distance; the id mismatch stays
+    below the reference's tolerance between its search modes (1e-3)."""
+    ix, db, q = _pipeline_b()
+    ii, idist, ic = oracle.search_pre_reorder(ix, q, 16, 100, oracle.MODE_IDEAL)
+    ei, edist, ec = oracle.search_pre_reorder(ix, q, 16, 100, oracle.MODE_EMULATE)
+    np.testing.assert_array_equal(ic, ec)
+    mism = float(np.mean([len(set(a) ^ set(b)) / (2 * len(a)) for a, b in zip(ii, ei)]))
+    assert mism < 1e-3
+    # the k'-th distance can only be >= the ideal one
+    assert np.all(edist[:, -1] >= idist[:, -1])
+
+
+def test_emulate_pipeline_b_tight_epsilon(oracle):
+    """Many leaves per query and a small k' (frequent GCs and tight int16
+    epsilons): emulate still returns k' distinct ids whose distances are the
+    LUT16 distances of those ids (checked against the ideal candidate set of
+    a wide search)."""
+    ix, db, q = _pipeline_b(n=12000, leaves=32, seed=4)
+    ei, ed, ec = oracle.search_pre_reorder(ix, q, 32, 5, oracle.MODE_EMULATE)
+    wi, wd, wc = oracle.search_pre_reorder(ix, q, 32, 12000, oracle.MODE_IDEAL)
+    for r in range(q.shape[0]):
+        assert ec[r] == 5 and len(set(ei[r].tolist())) == 5
+        lut = dict(zip(wi[r, :wc[r]].tolist(), wd[r, :wc[r]].view(np.uint32).tolist()))
+        for i, d in zip(ei[r].tolist(), ed[r].view(np.uint32).tolist()):
+            assert lut[i] == d
