@@ -61,6 +61,29 @@ CONFIGS = {
                  data="synthetic (SIFT1M-shaped seeded non-negative rounded mixture; no "
                       "datasets offline)",
                  metric_name="QPS at recall@10, SIFT1M shape (BASELINE.json configs[2]), batch=1000"),
+    # configs[3] / configs[4]: generated on the device (scann_amd/generate.py),
+    # range split; at N=1 this GPU holds rank 0's shard of the `split`-way split
+    "soar100m": dict(n=100_000_000, leaves=10000, leaves_to_search=100, metric=0, seed=4,
+                     generated=True, split=8, soar=1.5, dim=96,
+                     workload="configs[3]: synthetic 100M x 96 dot product + SOAR (lambda 1.5, "
+                              "overretrieve 2), tree-AH 10000 leaves, LUT16 AH 48 blocks x 2 "
+                              "dims, leaves_to_search=100, reorder 100, k=10, batch=1000, "
+                              "range split 8 ways: one rank's shard (12.5M rows, 25M members) "
+                              "+ the merge of 8 shard lists",
+                     data="synthetic, generated on the device (Philox per 65536-row chunk, "
+                          "4096-component unit-norm mixture; SURVEY §8d)",
+                     metric_name="QPS per GPU of a range-split rank, configs[3] (100M x 96 "
+                                 "dot + SOAR, 10000 leaves, 8-way split), batch=1000"),
+    "deep1b": dict(n=1_000_000_000, leaves=50000, leaves_to_search=400, metric=0, seed=5,
+                   generated=True, split=8, soar=None, dim=96,
+                   workload="configs[4]: Deep1B shape 1e9 x 96 dot product, tree-AH 50000 "
+                            "leaves, LUT16 AH 48 blocks x 2 dims, leaves_to_search=400, reorder "
+                            "100, k=10, batch=1000, dataset sharded 8 ways: one rank's shard "
+                            "(125M rows) + the merge of 8 shard lists",
+                   data="synthetic, generated on the device (Philox per 65536-row chunk, "
+                        "4096-component unit-norm mixture; SURVEY §8d)",
+                   metric_name="QPS per GPU of a range-split rank, configs[4] (Deep1B shape, "
+                               "50000 leaves, 8-way shard), batch=1000"),
 }
 CFG = CONFIGS["glove"]
 SWEEP_LEAVES = (10, 20, 30, 40, 50, 60, 70, 80, 100, 150)
@@ -252,6 +275,9 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
+    if CFG.get("generated"):
+        return main_generated(args, rank, world, local, dist, dev)
+
     from scann_amd import _native, synthetic
     db, _, ix = build_index(args.n, seed=CFG["seed"])
     # per-rank query batch from the same mixture (weak scaling)
@@ -305,6 +331,7 @@ def main():
         for k in ("partition_ms", "lut_ms", "invert_ms", "seed_scan_ms", "seed_select_ms",
                   "scan_ms", "select_ms", "total_ms"):
             stage[k] = stage.get(k, 0.0) + t[k] / args.steps
+    t_last = nat.timings()
     nat.set_profiling(False)
     torch.cuda.synchronize()
 
@@ -346,7 +373,6 @@ def main():
     ops_per_launch = 64.0 * bytes_per_launch
     achieved = ops_per_launch / (avg_scan_ms * 1e-3) / 1e12
     peak = 5000.0   # dense i8 MFMA (2x the 2.5 PF bf16 dense peak), MI355X_MICROARCH.md
-    t_last = nat.timings()
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "scan_traffic.json")
     if os.path.exists(tpath) and args.config == "glove":   # measured on the glove workload
@@ -426,6 +452,194 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def main_generated(args, rank, world, local, dist, dev):
+    """configs[3]/[4]: rank `rank` of a `split`-way range split, its shard
+    generated and built on this GPU.  With world == split the ranks run the
+    real split (shard search, one all-gather, merge on every rank); with
+    world == 1 this GPU is rank 0 of the split and the merge runs over `split`
+    copies of its shard list (the all-gather's shape; the xGMI all-gather
+    itself is not in the single-GPU step)."""
+    import torch
+    from scann_amd import generate, synthetic
+    from scann_amd.distributed import NativeShardEngine, all_gather_entries
+    split = CFG["split"]
+    if world not in (1, split):
+        raise SystemExit(f"--config {args.config}: run with 1 or {split} ranks")
+    shard_rank = rank if world == split else 0
+    n = args.n if args.n != 1_183_514 else CFG["n"]
+    t = time.time()
+    ds = generate.GeneratedDataset(n, CFG["dim"], CFG["seed"], device=dev)
+    ix = generate.build_generated_shard(
+        ds, LEAVES, shard_rank, split, soar_lambda=CFG["soar"], seed=CFG["seed"],
+        training_sample_size=max(250_000, 20 * LEAVES), counts_from_all_ranks=False, log=log)
+    log(f"shard {shard_rank}/{split} built in {time.time() - t:.1f}s: {ix.num_members} members")
+    q = ds.queries(NQ, CFG["seed"] + 1000)
+    eng = NativeShardEngine(ix, device=local)
+    qd = torch.from_numpy(q).to(dev)
+    k = eng.shard_width(LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True)
+    local_e = torch.empty((NQ, k, 2), dtype=torch.int64, device=dev)
+    gathered = torch.empty((split, NQ, k, 2), dtype=torch.int64, device=dev)
+    res = {}
+
+    def search():
+        eng.search_shard(qd, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True, local_e)
+
+    def merge():
+        if world == split:
+            g = all_gather_entries(local_e, world)
+        else:
+            gathered.copy_(local_e.unsqueeze(0).expand_as(gathered))
+            g = gathered
+        res["out"] = eng.merge(split, g, NQ, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True)
+
+    def timed(fn, steps):
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if dist is not None:
+            tt = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        return el
+
+    def step():
+        search()
+        merge()
+
+    for _ in range(args.warmup):
+        step()
+    elapsed = timed(step, args.steps)
+    search_s = timed(search, args.steps)
+    merge_s = timed(merge, args.steps)
+    ms_per_step = elapsed * 1000.0 / args.steps
+    # recall@10 of rank 0's merged result against exact brute force over the
+    # rows the split's ranks hold (world == 1: this shard's rows)
+    nat = eng.nat
+    nat.set_profiling(True)
+    search()
+    scan_ms, scan_bytes = [], []
+    for _ in range(min(args.steps, 20)):
+        search()
+        tm = nat.timings()
+        scan_ms.append(tm["scan_ms"])
+        scan_bytes.append(tm["scan_code_bytes"])
+    stages = nat.timings()
+    nat.set_profiling(False)
+    step()
+    torch.cuda.synchronize()
+    if world == 1:   # this rank's own result (the timed merge saw duplicated lists)
+        res["out"] = eng.merge(1, local_e.unsqueeze(0), NQ, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN,
+                               True)
+    gidx = res["out"][0].cpu().numpy().astype(np.int64)
+    c0, c1 = ds.chunk_range(shard_rank, split) if world == 1 else (0, ds.num_chunks)
+    r0, r1 = c0 * generate.CHUNK, min(c1 * generate.CHUNK, n)
+    truth = _generated_truth(ds, q, r0, r1, dev)
+    recall = synthetic.recall_at_k(gidx, truth, FINAL_NN)
+    avg_scan_ms = float(np.mean(scan_ms))
+    bytes_per_launch = float(np.mean(scan_bytes))
+    ops = 64.0 * bytes_per_launch
+    achieved = ops / (avg_scan_ms * 1e-3) / 1e12
+    if rank == 0:
+        result = {
+            "metric": CFG["metric_name"],
+            # the ranks search the same batch jointly: whole-job QPS
+            "value": round(NQ * args.steps / elapsed, 1),
+            "unit": "queries/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None, "dtype": "int8", "data": CFG["data"],
+            "config": {"workload": CFG["workload"], "num_datapoints": n, "dim": CFG["dim"],
+                       "num_leaves": LEAVES, "leaves_to_search": LEAVES_TO_SEARCH,
+                       "pre_reorder_nn": PRE_NN, "final_nn": FINAL_NN, "batch": NQ,
+                       "split": split, "shard_members": int(ix.num_members),
+                       "parallelism": (f"range split x{split}" if world == split else
+                                       f"rank 0 of a {split}-way range split on 1 GPU")},
+            "recall_at_10": round(recall, 4),
+            "recall_reference": ("exact brute force over the shard's rows" if world == 1
+                                 else "exact brute force over the whole dataset"),
+            "shard_search_ms": round(search_s * 1000.0 / args.steps, 4),
+            "merge_ms": round(merge_s * 1000.0 / args.steps, 4),
+            "merge_input": (f"all-gather of {split} ranks" if world == split else
+                            f"{split} copies of this rank's [nq][{k}] list"),
+            "roofline": {
+                "bound": "mfma", "achieved": round(achieved, 1), "peak": 5000.0,
+                "unit": "TFLOP/s", "frac": round(achieved / 5000.0, 4), "traffic": None,
+                "kernel": f"lut16_scan_kernel<{scan_k(ix.num_blocks)}> (main pass)",
+                "avg_launch_ms": round(avg_scan_ms, 5),
+                "algorithmic_code_bytes_per_launch": bytes_per_launch,
+                "algorithmic_ops_per_launch": ops,
+            },
+            "stage_ms": {k2: round(stages[k2], 4) for k2 in
+                         ("partition_ms", "invert_ms", "seed_scan_ms", "scan_ms", "select_ms",
+                          "total_ms")},
+        }
+        if not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline_shard(ix, q, args.cpu_threads or host_threads()[0])
+        print(json.dumps(result), flush=True)
+    nat.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _generated_truth(ds, q, r0, r1, dev):
+    """Exact top-k ids (float64 scores) over generated rows [r0, r1)."""
+    import torch
+    from scann_amd import generate
+    qt = torch.from_numpy(q).to(dev, torch.float64)
+    best_s = torch.full((q.shape[0], FINAL_NN), float("inf"), dtype=torch.float64, device=dev)
+    best_i = torch.zeros((q.shape[0], FINAL_NN), dtype=torch.int64, device=dev)
+    for c in range(r0 // generate.CHUNK, (r1 + generate.CHUNK - 1) // generate.CHUNK):
+        x = ds.chunk(c).to(torch.float64)
+        sc = -(qt @ x.T)
+        s = torch.cat([best_s, sc], 1)
+        i = torch.cat([best_i, torch.arange(c * generate.CHUNK, c * generate.CHUNK + x.shape[0],
+                                            device=dev).expand(q.shape[0], -1)], 1)
+        v, j = torch.topk(s, FINAL_NN, dim=1, largest=False)
+        best_s, best_i = v, torch.gather(i, 1, j)
+    return best_i.cpu().numpy()
+
+
+def cpu_baseline_shard(ix, q, threads):
+    """The AVX2 port over this rank's shard viewed as a standalone index
+    (members renumbered 0..M-1, their float rows as the dataset): the
+    reference's per-rank work, timed on a bounded sample of the batch."""
+    from oracle import binding as oracle
+    from scann_amd.index import TreeAHIndex
+    oracle.build()
+    m = ix.num_members
+    view = TreeAHIndex(metric=ix.metric, dim=ix.dim, num_blocks=ix.num_blocks,
+                       dims_per_block=ix.dims_per_block, residual=ix.residual,
+                       centers=ix.centers, codebook=ix.codebook, leaf_offsets=ix.leaf_offsets,
+                       leaf_members=np.arange(m, dtype=np.uint32), member_codes=ix.member_codes,
+                       num_datapoints=m, dataset=ix.member_rows,
+                       spilling_overretrieve_factor=ix.spilling_overretrieve_factor)
+    port = oracle.Avx2Port(view)
+    model, isa = cpu_info()
+    sub = q[:max(threads, 250)]
+    port.search(sub, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True, threads)
+    runs = []
+    for _ in range(3):
+        t = time.perf_counter()
+        port.search(sub, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True, threads)
+        runs.append(sub.shape[0] / (time.perf_counter() - t))
+    port.close()
+    return dict(value=round(float(np.median(runs)), 1), unit="queries/s", cores=threads,
+                kind="port", cpu_model=model, isa=isa, runs_qps=[round(x, 1) for x in runs],
+                sample=f"median of 3 runs of {sub.shape[0]} queries through the AVX2 port over "
+                       f"this rank's shard as a standalone index ({m} members renumbered, "
+                       f"emulate-mode pipeline A), {threads} threads; no merge")
 
 
 if __name__ == "__main__":
