@@ -64,7 +64,7 @@ CONFIGS = {
     # configs[3] / configs[4]: generated on the device (scann_amd/generate.py),
     # range split; at N=1 this GPU holds rank 0's shard of the `split`-way split
     "soar100m": dict(n=100_000_000, leaves=10000, leaves_to_search=100, metric=0, seed=4,
-                     generated=True, split=8, soar=1.5, dim=96,
+                     generated=True, split=8, soar=1.5, dim=96, components=4096,
                      workload="configs[3]: synthetic 100M x 96 dot product + SOAR (lambda 1.5, "
                               "overretrieve 2), tree-AH 10000 leaves, LUT16 AH 48 blocks x 2 "
                               "dims, leaves_to_search=100, reorder 100, k=10, batch=1000, "
@@ -75,13 +75,13 @@ CONFIGS = {
                      metric_name="QPS per GPU of a range-split rank, configs[3] (100M x 96 "
                                  "dot + SOAR, 10000 leaves, 8-way split), batch=1000"),
     "deep1b": dict(n=1_000_000_000, leaves=50000, leaves_to_search=400, metric=0, seed=5,
-                   generated=True, split=8, soar=None, dim=96,
+                   generated=True, split=8, soar=None, dim=96, components=1 << 17,
                    workload="configs[4]: Deep1B shape 1e9 x 96 dot product, tree-AH 50000 "
                             "leaves, LUT16 AH 48 blocks x 2 dims, leaves_to_search=400, reorder "
                             "100, k=10, batch=1000, dataset sharded 8 ways: one rank's shard "
                             "(125M rows) + the merge of 8 shard lists",
                    data="synthetic, generated on the device (Philox per 65536-row chunk, "
-                        "4096-component unit-norm mixture; SURVEY §8d)",
+                        "131072-component unit-norm mixture; SURVEY §8d)",
                    metric_name="QPS per GPU of a range-split rank, configs[4] (Deep1B shape, "
                                "50000 leaves, 8-way shard), batch=1000"),
 }
@@ -470,7 +470,8 @@ def main_generated(args, rank, world, local, dist, dev):
     shard_rank = rank if world == split else 0
     n = args.n if args.n != 1_183_514 else CFG["n"]
     t = time.time()
-    ds = generate.GeneratedDataset(n, CFG["dim"], CFG["seed"], device=dev)
+    ds = generate.GeneratedDataset(n, CFG["dim"], CFG["seed"], components=CFG["components"],
+                                   device=dev)
     ix = generate.build_generated_shard(
         ds, LEAVES, shard_rank, split, soar_lambda=CFG["soar"], seed=CFG["seed"],
         training_sample_size=max(250_000, 20 * LEAVES), counts_from_all_ranks=False, log=log)

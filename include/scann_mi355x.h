@@ -238,7 +238,8 @@ int smx_lut16_leaf_scores(smx_index* index, int32_t leaf, const uint8_t* lut,
 /* ---- diagnostics ---------------------------------------------------------- */
 int smx_set_profiling(smx_index* index, int32_t enabled);
 int smx_get_timings(const smx_index* index, smx_timings* out);
-/* Tuning knobs: candidate buffer capacity per query, seed leaves used for the
+/* Tuning knobs: candidate buffer capacity per query (0, the default: sized
+ * per call from k', leaves_to_search and the seed leaves), seed leaves used for the
  * per-query threshold, scan kernel variant (0 = the scan, 4 = the scan
  * without its threshold epilogue: a timing ablation whose results are
  * invalid) and tiles per work item (0 keeps the default, 32). */

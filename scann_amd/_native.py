@@ -259,7 +259,7 @@ class NativeIndex:
         check(self.lib.smx_get_timings(self.h, ctypes.byref(t)), "smx_get_timings")
         return t.as_dict()
 
-    def set_tuning(self, candidates_per_query: int = 4096, seed_leaves: int = 4,
+    def set_tuning(self, candidates_per_query: int = 0, seed_leaves: int = 4,
                    scan_variant: int = 0, chunk_tiles: int = 0):
         check(self.lib.smx_set_tuning(self.h, int(candidates_per_query), int(seed_leaves),
                                       int(scan_variant), int(chunk_tiles)), "smx_set_tuning")

@@ -2795,13 +2795,13 @@ hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s) {
   uint32_t kcap = 1;
   while (kcap < a.cap) kcap <<= 1;
   const uint32_t selcap = std::max<uint32_t>(2048u, 2 * kkp2);
-  const size_t lds = size_t(kcap) * 8 + size_t(selcap) * 8 + size_t(kkp2) * 8 +
-                     size_t(a.dim) * 4 + size_t(a.kk) * 8 + (kSelBins + 256) * 4;
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-  if (a.kk <= kSelMax) {   // (shard mode too)
+  if (a.kk <= kSelMax) {   // (shard mode too; the list is read from global memory)
     hipLaunchKernelGGL(final_select_rank_kernel, dim3(nq), dim3(256), 0, s, a);
     return hipGetLastError();
   }
+  const size_t lds = size_t(kcap) * 8 + size_t(selcap) * 8 + size_t(kkp2) * 8 +
+                     size_t(a.dim) * 4 + size_t(a.kk) * 8 + (kSelBins + 256) * 4;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(final_select_kernel, dim3(nq), dim3(256), lds, s, a);
   return hipGetLastError();
 }

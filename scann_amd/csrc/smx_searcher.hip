@@ -131,7 +131,7 @@ struct smx_index {
   hipStream_t stream = nullptr;
   std::mutex mu;
   Workspace ws;
-  uint32_t cap_per_query = 4096;   // candidate list capacity
+  uint32_t cap_per_query = 0;      // candidate list capacity; 0 = sized per call (AutoCap)
   int seed_leaves = 4;
   int scan_variant = 0;            // see smx::LaunchScan
   uint32_t chunk_tiles = 32;       // tiles per work item
@@ -336,13 +336,30 @@ int ValidateDesc(const smx_index_desc* d) {
   return SMX_OK;
 }
 
+// Candidate list capacity per query when none is set.  The seed threshold
+// is the exact k'-th key over `seed` of the query's L leaves, so about
+// k' * L / seed candidates pass it; an overflowing list costs its select
+// block a rescan of the query's L leaves (VALU), so the list is sized 8x
+// that expectation (Deep1B shape, L = 400 of 50000 leaves: 10^4 expected ->
+// 2^17), at least 4096.  The rank select (k' <= 256) reads the list from
+// global memory; the LDS select of larger k' bounds it to 8192.
+uint32_t AutoCap(int L, int kk, int seed) {
+  if (seed <= 0 || kk > 256) return 4096;   // 256 = kSelMax of the rank select
+  const uint64_t want = 8ull * uint64_t(kk) * uint64_t(L) / uint64_t(seed);
+  uint32_t cap = 4096;
+  while (cap < want && cap < (1u << 17)) cap <<= 1;
+  return cap;
+}
+
 int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
   Workspace& w = h->ws;
   const smx::DeviceIndex& ix = h->ix;
   // cap >= 2 k': when a list overflows, its k'-th stored key is strictly
   // below the threshold (keys are unique and all <= it), so every
   // tightening pass drops at least cap - k' keys
-  const uint32_t cap = std::max<uint32_t>(h->cap_per_query, 2u * uint32_t(kk));
+  const uint32_t base = h->cap_per_query ? h->cap_per_query
+                                         : AutoCap(L, kk, std::min(h->seed_leaves, L));
+  const uint32_t cap = std::max<uint32_t>(base, 2u * uint32_t(kk));
   if (nq <= w.nq && L <= w.L && kk <= w.kk && width <= w.width && cap == w.cap &&
       ix.dim == w.dim)
     return SMX_OK;
@@ -1093,8 +1110,9 @@ int smx_set_tuning(smx_index* h, int32_t candidates_per_query, int32_t seed_leav
                 "scan_variant is 0 (scan), 4 (timing ablation) or 8 (diagnostic stamps)");
   if (chunk_tiles != 0 && (chunk_tiles < 16 || chunk_tiles > 65535))
     return Fail(SMX_INVALID_ARGUMENT, "chunk_tiles must be 0 (default) or in [16, 65535]");
-  if (candidates_per_query < 32 || candidates_per_query > 8192)
-    return Fail(SMX_INVALID_ARGUMENT, "candidates_per_query must be in [32, 8192]");
+  if (candidates_per_query != 0 && (candidates_per_query < 32 || candidates_per_query > 8192))
+    return Fail(SMX_INVALID_ARGUMENT,
+                "candidates_per_query must be 0 (sized per call) or in [32, 8192]");
   if (seed_leaves < 0) return Fail(SMX_INVALID_ARGUMENT, "seed_leaves must be >= 0");
   std::lock_guard<std::mutex> lock(h->mu);
   h->cap_per_query = uint32_t(candidates_per_query);

@@ -131,6 +131,9 @@ def _tokens(ds: GeneratedDataset, c0: int, c1: int, c: torch.Tensor, cn: torch.T
                     leaves.append(t)
                     rows.append(rid)
     if keep:
+        if not leaves:   # a rank without chunks (n < world chunks)
+            e = torch.zeros(0, dtype=torch.int64, device=ds.device)
+            return counts, e, e.clone()
         return counts, torch.cat(leaves), torch.cat(rows)
     return counts, None, None
 
@@ -227,7 +230,8 @@ def build_generated_shard(ds: GeneratedDataset, num_leaves: int, rank: int = 0, 
         codes[s:s + step] = d.argmin(-1).to(torch.uint8).cpu().numpy()
         member_rows[s:s + step] = x.cpu().numpy()
     del x_all
-    say(f"codes: {m} members encoded")
+    say(f"codes: {m} members encoded; largest leaf {int(total.max())} (whole index"
+        f"{', estimated' if world > 1 and not counts_from_all_ranks else ''}), shift {shift}")
     members = rows.to(torch.int64).cpu().numpy().astype(np.uint32)
     if world == 1:
         dataset = np.empty((ds.n, dim), np.float32)
@@ -237,6 +241,13 @@ def build_generated_shard(ds: GeneratedDataset, num_leaves: int, rank: int = 0, 
                            codebook=codebook, leaf_offsets=offsets, leaf_members=members,
                            member_codes=codes, num_datapoints=ds.n, dataset=dataset,
                            spilling_overretrieve_factor=float(overretrieve_factor))
+    if shift == 0 and ds.n * dim * 4 > (16 << 30):
+        # without the global top-N path ties are global ids and the reorder
+        # reads rows by global id: every rank would need the whole dataset
+        raise ValueError(
+            f"generated shard: a leaf exceeds {1 << inner} members (the global top-N limit "
+            f"for {L} leaves), so the shard would need the whole {ds.n}-row dataset; use "
+            f"more leaves or a more uniform mixture")
     return TreeAHIndex(metric=metric, dim=dim, num_blocks=num_blocks,
                        dims_per_block=dims_per_block, residual=residual, centers=centers,
                        codebook=codebook, leaf_offsets=offsets, leaf_members=members,

@@ -47,3 +47,11 @@ def test_rank_shards_are_the_range_split_of_the_whole_index(soar):
     # the shard carries its members' float rows for the reorder
     sh = shards[1]
     np.testing.assert_array_equal(sh.member_rows, whole.dataset[sh.leaf_members])
+
+
+def test_rank_without_chunks_is_an_empty_shard():
+    ds = _ds(n=100_000)   # 2 chunks, 3 ranks
+    sh = generate.build_generated_shard(ds, 8, 0, 3, training_sample_size=5000,
+                                        training_iterations=2, ah_training_sample_size=5000,
+                                        ah_training_iterations=2)
+    assert sh.num_members == 0 and sh.is_shard

@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 def test_generated_shards_merge_to_the_whole_index(oracle, soar, leaves, world):
     from scann_amd import _native, generate
     from scann_amd.distributed import NativeShardEngine
-    ds = generate.GeneratedDataset(400_000, 96, 4, device=torch.device("cuda"))
+    ds = generate.GeneratedDataset(500_000, 96, 4, device=torch.device("cuda"))
     kw = dict(soar_lambda=soar, training_sample_size=60_000, training_iterations=4,
               ah_training_sample_size=40_000, ah_training_iterations=4, seed=4)
     whole = generate.build_generated_shard(ds, leaves, 0, 1, **kw)
