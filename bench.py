@@ -92,7 +92,7 @@ SWEEP_LEAVES = (10, 20, 30, 40, 50, 60, 70, 80, 100, 150)
 def scan_k(num_blocks):
     """MFMA steps of the compiled scan instantiation (EffectiveKSteps in smx_searcher.hip)."""
     k = (num_blocks + 1) // 2
-    return next(v for v in (4, 8, 12, 16, 20, 24, 25, 28, 32) if v >= k)
+    return next(v for v in (4, 8, 12, 16, 20, 24, 26, 28, 32) if v >= k)
 
 
 def queries_for_rank(dim, rank):

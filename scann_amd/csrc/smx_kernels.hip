@@ -37,6 +37,7 @@ namespace smx {
 namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v8i __attribute__((ext_vector_type(8)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
 // sqrtf(FLT_EPSILON) as the reference computes it on the host
@@ -1244,6 +1245,52 @@ __device__ __forceinline__ v16i TileMfma(const uint32_t* codes, const v4i (&b)[K
   return acc;
 }
 
+// The same tile on the 2:4 structured-sparse MFMA (v_smfmac_i32_32x32x64_i8:
+// K = 64 at the cycles of the dense K = 32 form, measured by
+// tools/smfmac_probe.hip).  A one-hot row is exactly 2:4 sparse -- at most
+// one non-zero in every group of 4 centers -- so the sparse instruction
+// computes the whole dense product.  Operand layout (tools/smfmac_probe2/3):
+// lane (r, hA) of A holds 16 compressed values, j < 8 for B lanes (c, 0) and
+// j >= 8 for B lanes (c, 1), two per group of 4, value j selecting B byte
+// 16*hA + 4*((j % 8) / 2) + idx_j (idx_j = bits [2j, 2j+2) of the index
+// VGPR).  Step s covers blocks 4s + 2*hB + hA: lane (r, hA) needs the
+// codes of blocks 4s + hA and 4s + 2 + hA = nibbles 2s and 2s + 1 of its
+// stream (byte s of the unchanged tile layout), and B lane (c, hB) the LUT
+// rows 4s + 2hB and 4s + 2hB + 1 (32 contiguous bytes).  Per step: one
+// ds_read_b128 of a 256-entry table (byte -> compressed values, a 1 in the
+// group of each nibble) and the index word (each nibble's low two bits in
+// its eight fields) from two VALU ops.
+__device__ __forceinline__ int SparseIndex(uint32_t by) {
+  return int(__umul24((by & 3u) | ((by & 0x30u) << 12), 0x5555u));
+}
+
+template <int K, int R>
+__device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)[K / 2],
+                                           const v4i* oh2_tab) {
+  constexpr int KS = K / 2;
+  auto byte_at = [&](int t) { return (codes[t >> 2] >> ((t & 3) * 8)) & 0xFFu; };
+  v4i o[R];
+#pragma unroll
+  for (int p = 0; p < R; ++p)
+    if (p < KS) o[p] = oh2_tab[byte_at(p)];
+  v16i acc = v16i{0};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    // the index word just in time (two VALU ops from the live code words)
+    acc = __builtin_amdgcn_smfmac_i32_32x32x64_i8(o[s % R], b[s], acc,
+                                                  SparseIndex(byte_at(s)), 0, 0);
+    if (s + R < KS) o[s % R] = oh2_tab[byte_at(s + R)];
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if (s == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    if (s + R < KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+  }
+  return acc;
+}
+
 // ---------------------------------------------------------------------------
 // The scan kernel: one workgroup of kScanWaves waves per CU (3 per SIMD), the
 // CU's waves sharing a static share of the work and balancing it among
@@ -1286,13 +1333,13 @@ constexpr int kItemKeys = 256;     // survivors one segment stages in LDS
 constexpr int kMaxSegs = 512;      // share segments listed per round
 constexpr uint32_t kStealMin = 3;  // tiles left for a second wave to join a segment
 
-// Waves per scan workgroup: 3 per SIMD (168 VGPRs) up to K = 25; 2 per SIMD
+// Waves per scan workgroup: 3 per SIMD (168 VGPRs) up to K = 26; 2 per SIMD
 // above (the K B-fragment registers).
 #ifndef SMX_SCAN_WAVES
 #define SMX_SCAN_WAVES 12
 #endif
 template <int K>
-constexpr int ScanWaves() { return K <= 25 ? SMX_SCAN_WAVES : 8; }
+constexpr int ScanWaves() { return K <= 26 ? SMX_SCAN_WAVES : 8; }
 
 // Diagnostic stamps (ABL & 8; a separate buffer that nothing else reads):
 // per segment {hw_id | worker << 32, xcc_id << 32 | item, realtime, memtime at
@@ -1403,8 +1450,9 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   constexpr int W = 4 * NW;
   constexpr int Q = 32, KB = kItemKeys, NWAVES = ScanWaves<K>();
   constexpr int R = 3;   // one-hot reads in flight ahead of their MFMA
+  static_assert(K % 2 == 0, "the sparse scan takes two code nibbles per step");
   __shared__ ScanWaveLds wl_[NWAVES];
-  __shared__ v4i oh_tab[16];
+  __shared__ v4i oh2_tab[256];
   __shared__ uint32_t s_item[kMaxSegs], s_end[kMaxSegs], s_next[kMaxSegs];
   __shared__ SegDesc s_desc[kMaxSegs];
   __shared__ uint32_t s_nseg, s_claim, s_sw, s_su;
@@ -1414,10 +1462,12 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   const int c = lane & 31;
   const int h = lane >> 5;
   ScanWaveLds& wl = wl_[wv];
-  if (threadIdx.x < 16) {
+  if (threadIdx.x < 256) {   // byte (x0 | x1 << 4) -> a 1 at value 2*(x0>>2), 8 + 2*(x1>>2)
+    const uint32_t x0 = threadIdx.x & 15u, x1 = threadIdx.x >> 4;
     v4i t = {0, 0, 0, 0};
-    t[threadIdx.x >> 2] = int(1u << (8 * (threadIdx.x & 3)));
-    oh_tab[threadIdx.x] = t;
+    t[(x0 >> 2) >> 1] = int(1u << (16 * ((x0 >> 2) & 1u)));
+    t[2 + ((x1 >> 2) >> 1)] = int(1u << (16 * ((x1 >> 2) & 1u)));
+    oh2_tab[threadIdx.x] = t;
   }
   const uint32_t worker = blockIdx.x * NWAVES + wv;
   const WorkItem* __restrict__ work = a.work;
@@ -1539,13 +1589,14 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       const uint32_t n = __builtin_amdgcn_readfirstlane(sd.n);
       const int leaf = int(__builtin_amdgcn_readfirstlane(sd.leaf));
       // this segment's B fragments (LUT rows 2s+h of query c) and first tile
-      v4i b[K];
+      v8i b[K / 2];
       uint32_t codes[NW] = {};
       const uint8_t* tb = a.tiles + toff * 64ull * W + size_t(lane) * W;
-      const v4i* bsrc = reinterpret_cast<const v4i*>(a.lut) + size_t(lq) * 2 * K + h;
+      // LUT rows 4s + 2h, 4s + 2h + 1 of query c (32 bytes) per sparse step
+      const v8i* bsrc = reinterpret_cast<const v8i*>(a.lut) + size_t(lq) * K + h;
       auto load_b = [&]() {
 #pragma unroll
-        for (int s2 = 0; s2 < K; ++s2) b[s2] = bsrc[2 * s2];
+        for (int s2 = 0; s2 < K / 2; ++s2) b[s2] = bsrc[2 * s2];
       };
       load_b();
       LoadCodes<K>(tb + size_t(j) * 64 * W, codes);
@@ -1625,7 +1676,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
 
       // one tile: K MFMAs, then the hit test
       auto tile = [&](const uint32_t (&cd)[NW], uint32_t jt) {
-        v16i acc = TileMfma<K, R>(cd, b, oh_tab);
+        v16i acc = TileSmfmac<K, R>(cd, b, oh2_tab);
         if (ABL & 4) {
           int x = acc[0];
 #pragma unroll
@@ -2679,7 +2730,7 @@ hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int va
     SMX_SCAN_CASE(16)
     SMX_SCAN_CASE(20)
     SMX_SCAN_CASE(24)
-    SMX_SCAN_CASE(25)
+    SMX_SCAN_CASE(26)
     SMX_SCAN_CASE(28)
     SMX_SCAN_CASE(32)
     default:
@@ -2702,7 +2753,7 @@ hipError_t ScanBlocksPerCU(const DeviceIndex& ix, int* blocks) {
     SMX_OCC_CASE(16)
     SMX_OCC_CASE(20)
     SMX_OCC_CASE(24)
-    SMX_OCC_CASE(25)
+    SMX_OCC_CASE(26)
     SMX_OCC_CASE(28)
     SMX_OCC_CASE(32)
     default:
@@ -2734,7 +2785,7 @@ hipError_t LaunchLeafScores(const DeviceIndex& ix, int leaf, const int8_t* lut, 
     SMX_LEAF_CASE(16)
     SMX_LEAF_CASE(20)
     SMX_LEAF_CASE(24)
-    SMX_LEAF_CASE(25)
+    SMX_LEAF_CASE(26)
     SMX_LEAF_CASE(28)
     SMX_LEAF_CASE(32)
     default:
@@ -2757,7 +2808,7 @@ hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStrea
     SMX_SEED_CASE(16)
     SMX_SEED_CASE(20)
     SMX_SEED_CASE(24)
-    SMX_SEED_CASE(25)
+    SMX_SEED_CASE(26)
     SMX_SEED_CASE(28)
     SMX_SEED_CASE(32)
     default:

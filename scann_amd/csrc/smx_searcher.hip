@@ -66,7 +66,8 @@ int Log2Ceil(uint32_t n) {
 
 // K values with a compiled scan kernel; others round up (zero padding).
 int EffectiveKSteps(int nb) {
-  static const int kList[] = {4, 8, 12, 16, 20, 24, 25, 28, 32};
+  // even: the sparse scan takes two code nibbles (four blocks) per step
+  static const int kList[] = {4, 8, 12, 16, 20, 24, 26, 28, 32};
   const int k = (nb + 1) / 2;
   for (int v : kList)
     if (v >= k) return v;
