@@ -25,6 +25,22 @@ constexpr uint32_t kCounterStride = 32;
 // the nibbles of datapoint r for blocks h, h+2, h+4, ... (K = ceil(B/2)).
 inline int LaneBytes(int ksteps) { return 4 * ((((ksteps + 1) / 2) + 3) / 4); }
 
+// Code byte j of a lane holds the nibbles of its blocks x0 = 4j + h and
+// x1 = 4j + 2 + h (one sparse MFMA step), encoded for the sparse operand:
+// low nibble = the codes' groups of four, (x0 >> 2) | (x1 >> 2) << 2 (which
+// compressed A values are 1), high nibble = their positions in the group,
+// (x0 & 3) | (x1 & 3) << 2 (the index fields).  Every consumer decodes
+// through these (the pair tables are indexed by the encoded byte).
+__host__ __device__ inline uint32_t EncodeCodePair(uint32_t x0, uint32_t x1) {
+  return ((x0 >> 2) | ((x1 >> 2) << 2)) | (((x0 & 3u) | ((x1 & 3u) << 2)) << 4);
+}
+__host__ __device__ inline uint32_t CodePairLo(uint32_t by) {   // x0
+  return ((by & 3u) << 2) | ((by >> 4) & 3u);
+}
+__host__ __device__ inline uint32_t CodePairHi(uint32_t by) {   // x1
+  return (by & 0xCu) | ((by >> 6) & 3u);
+}
+
 // Index resident in HBM (owned by the handle).
 struct DeviceIndex {
   int metric = 0, dim = 0, nl = 0, nb = 0, dpb = 0, residual = 0;

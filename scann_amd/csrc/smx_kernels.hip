@@ -956,10 +956,9 @@ __device__ __forceinline__ v16i TileSums(const uint32_t* codes, const v4i* frag)
   v16i acc = {0};
 #pragma unroll
   for (int s = 0; s < K; ++s) {
-    const int sh = (s & 7) * 4;
-    const uint32_t w = codes[s >> 3];
-    const uint32_t e8 = sh >= 3 ? ((w >> (sh - 3)) & 0x78u) : ((w << 3) & 0x78u);
-    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(OneHot16(e8), frag[s], acc, 0, 0, 0);
+    const uint32_t by = (codes[s >> 3] >> (8 * ((s >> 1) & 3))) & 0xFFu;
+    const uint32_t x = (s & 1) ? CodePairHi(by) : CodePairLo(by);
+    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(OneHot16(8u * x), frag[s], acc, 0, 0, 0);
   }
   return acc;
 }
@@ -1048,8 +1047,8 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
 #pragma unroll
   for (int i = 0; i < 2 * NB; ++i) {
     const int h = i / NB, j = i % NB, s0 = 2 * j, s1 = 2 * j + 1;
-    int v = lut[(2 * s0 + h) * 16 + (tid & 15)];
-    if (s1 < K) v += lut[(2 * s1 + h) * 16 + (tid >> 4)];
+    int v = lut[(2 * s0 + h) * 16 + CodePairLo(uint32_t(tid))];
+    if (s1 < K) v += lut[(2 * s1 + h) * 16 + CodePairHi(uint32_t(tid))];
     ptab[i * 256 + tid] = int16_t(v);
   }
   if (tid == 0) s_cnt = 0;
@@ -1206,46 +1205,9 @@ __global__ void __launch_bounds__(256) pair_scatter_kernel(SeedArgs a, int nq) {
 }
 
 
-// K MFMAs of one tile with the item's B fragments (LUT rows) held in
-// registers.  The one-hot A fragments come from a 16-entry LDS table
-// (oh_tab[t] = 16 bytes with byte t = 1): per MFMA one nibble extraction and
-// one ds_read_b128 (conflict-free: the table spans the 64 banks exactly, and
-// equal entries broadcast), read R steps ahead of their MFMA; a scheduling
-// barrier closes each step so the compiler cannot collapse the ring.
-template <int K, int R>
-__device__ __forceinline__ v16i TileMfma(const uint32_t* codes, const v4i (&b)[K],
-                                         const v4i* oh_tab) {
-  v4i o[R];
-#pragma unroll
-  for (int p = 0; p < R; ++p)
-    if (p < K) o[p] = oh_tab[(codes[p >> 3] >> ((p & 7) * 4)) & 15u];
-  v16i acc = v16i{0};
-#pragma unroll
-  for (int s = 0; s < K; ++s) {
-    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(o[s % R], b[s], acc, 0, 0, 0);
-    if (s + R < K) {
-      const int t = s + R;
-      o[s % R] = oh_tab[(codes[t >> 3] >> ((t & 7) * 4)) & 15u];
-    }
-  }
-  // the order the machine scheduler must keep: the ring's first R reads,
-  // then MFMA s followed by the read of step s + R (the DAG builder would
-  // otherwise issue every read first and sink the MFMAs to their use); the
-  // next tile's code load (issued by the caller just before) goes right
-  // after the first MFMA -- after this tile's address arithmetic, so no wait
-  // for it is placed in front of that, and before the rest of the MFMAs, so
-  // that its latency hides behind them
-  __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
-#pragma unroll
-  for (int s = 0; s < K; ++s) {
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    if (s == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-    if (s + R < K) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-  }
-  return acc;
-}
-
-// The same tile on the 2:4 structured-sparse MFMA (v_smfmac_i32_32x32x64_i8:
+// One tile: S[dp][q] for 32 datapoints x 32 queries with the item's B
+// fragments (LUT rows) held in registers, on the 2:4 structured-sparse MFMA
+// (v_smfmac_i32_32x32x64_i8:
 // K = 64 at the cycles of the dense K = 32 form, measured by
 // tools/smfmac_probe.hip).  A one-hot row is exactly 2:4 sparse -- at most
 // one non-zero in every group of 4 centers -- so the sparse instruction
@@ -1255,38 +1217,43 @@ __device__ __forceinline__ v16i TileMfma(const uint32_t* codes, const v4i (&b)[K
 // 16*hA + 4*((j % 8) / 2) + idx_j (idx_j = bits [2j, 2j+2) of the index
 // VGPR).  Step s covers blocks 4s + 2*hB + hA: lane (r, hA) needs the
 // codes of blocks 4s + hA and 4s + 2 + hA = nibbles 2s and 2s + 1 of its
-// stream (byte s of the unchanged tile layout), and B lane (c, hB) the LUT
-// rows 4s + 2hB and 4s + 2hB + 1 (32 contiguous bytes).  Per step: one
-// ds_read_b128 of a 256-entry table (byte -> compressed values, a 1 in the
-// group of each nibble) and the index word (each nibble's low two bits in
-// its eight fields) from two VALU ops.
-__device__ __forceinline__ int SparseIndex(uint32_t by) {
-  return int(__umul24((by & 3u) | ((by & 0x30u) << 12), 0x5555u));
-}
-
+// stream (code byte s, EncodeCodePair), and B lane (c, hB) the LUT rows
+// 4s + 2hB and 4s + 2hB + 1 (32 contiguous bytes).  Per step two
+// conflict-free LDS reads (16-entry tables spanning distinct banks; equal
+// entries broadcast): the compressed values from the byte's group nibble
+// (a 1 at value 2*(x0 >> 2) and 8 + 2*(x1 >> 2)) and the index word from its
+// position nibble (x0 & 3 in fields 0..7, x1 & 3 in fields 8..15), each
+// address two VALU ops; a 256-entry table of both spent 60% of the LDS
+// cycles in bank conflicts.
 template <int K, int R>
 __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)[K / 2],
-                                           const v4i* oh2_tab) {
+                                           const v4i* grp_tab, const int* pos_tab) {
   constexpr int KS = K / 2;
-  auto byte_at = [&](int t) { return (codes[t >> 2] >> ((t & 3) * 8)) & 0xFFu; };
+  auto grp = [&](int t) { return (codes[t >> 2] >> ((t & 3) * 8)) & 0xFu; };
+  auto pos = [&](int t) { return (codes[t >> 2] >> ((t & 3) * 8 + 4)) & 0xFu; };
   v4i o[R];
+  int ix[R];
 #pragma unroll
   for (int p = 0; p < R; ++p)
-    if (p < KS) o[p] = oh2_tab[byte_at(p)];
+    if (p < KS) {
+      o[p] = grp_tab[grp(p)];
+      ix[p] = pos_tab[pos(p)];
+    }
   v16i acc = v16i{0};
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    // the index word just in time (two VALU ops from the live code words)
-    acc = __builtin_amdgcn_smfmac_i32_32x32x64_i8(o[s % R], b[s], acc,
-                                                  SparseIndex(byte_at(s)), 0, 0);
-    if (s + R < KS) o[s % R] = oh2_tab[byte_at(s + R)];
+    acc = __builtin_amdgcn_smfmac_i32_32x32x64_i8(o[s % R], b[s], acc, ix[s % R], 0, 0);
+    if (s + R < KS) {
+      o[s % R] = grp_tab[grp(s + R)];
+      ix[s % R] = pos_tab[pos(s + R)];
+    }
   }
-  __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
+  __builtin_amdgcn_sched_group_barrier(0x100, 2 * R, 0);
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
     if (s == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-    if (s + R < KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    if (s + R < KS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
   }
   return acc;
 }
@@ -1452,7 +1419,8 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   constexpr int R = 3;   // one-hot reads in flight ahead of their MFMA
   static_assert(K % 2 == 0, "the sparse scan takes two code nibbles per step");
   __shared__ ScanWaveLds wl_[NWAVES];
-  __shared__ v4i oh2_tab[256];
+  __shared__ v4i grp_tab[16];
+  __shared__ int pos_tab[16];
   __shared__ uint32_t s_item[kMaxSegs], s_end[kMaxSegs], s_next[kMaxSegs];
   __shared__ SegDesc s_desc[kMaxSegs];
   __shared__ uint32_t s_nseg, s_claim, s_sw, s_su;
@@ -1462,12 +1430,14 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   const int c = lane & 31;
   const int h = lane >> 5;
   ScanWaveLds& wl = wl_[wv];
-  if (threadIdx.x < 256) {   // byte (x0 | x1 << 4) -> a 1 at value 2*(x0>>2), 8 + 2*(x1>>2)
-    const uint32_t x0 = threadIdx.x & 15u, x1 = threadIdx.x >> 4;
+  if (threadIdx.x < 16) {   // group nibble g0 | g1 << 2: a 1 at values 2*g0, 8 + 2*g1
+    const uint32_t g0 = threadIdx.x & 3u, g1 = threadIdx.x >> 2;
     v4i t = {0, 0, 0, 0};
-    t[(x0 >> 2) >> 1] = int(1u << (16 * ((x0 >> 2) & 1u)));
-    t[2 + ((x1 >> 2) >> 1)] = int(1u << (16 * ((x1 >> 2) & 1u)));
-    oh2_tab[threadIdx.x] = t;
+    t[g0 >> 1] = int(1u << (16 * (g0 & 1u)));
+    t[2 + (g1 >> 1)] = int(1u << (16 * (g1 & 1u)));
+    grp_tab[threadIdx.x] = t;
+    // position nibble p0 | p1 << 2: p0 in index fields 0..7, p1 in 8..15
+    pos_tab[threadIdx.x] = int((threadIdx.x & 3u) * 0x5555u | ((threadIdx.x >> 2) * 0x5555u) << 16);
   }
   const uint32_t worker = blockIdx.x * NWAVES + wv;
   const WorkItem* __restrict__ work = a.work;
@@ -1676,7 +1646,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
 
       // one tile: K MFMAs, then the hit test
       auto tile = [&](const uint32_t (&cd)[NW], uint32_t jt) {
-        v16i acc = TileSmfmac<K, R>(cd, b, oh2_tab);
+        v16i acc = TileSmfmac<K, R>(cd, b, grp_tab, pos_tab);
         if (ABL & 4) {
           int x = acc[0];
 #pragma unroll
@@ -1894,8 +1864,8 @@ __device__ __forceinline__ uint32_t RescanQuery(const RescanArgs& a, int qi, uin
   __syncthreads();
   for (int i = 0; i < 2 * NB; ++i) {
     const int h = i / NB, j = i % NB, s0 = 2 * j, s1 = 2 * j + 1;
-    int v = lut[(2 * s0 + h) * 16 + (tid & 15)];
-    if (s1 < K) v += lut[(2 * s1 + h) * 16 + (tid >> 4)];
+    int v = lut[(2 * s0 + h) * 16 + CodePairLo(uint32_t(tid))];
+    if (s1 < K) v += lut[(2 * s1 + h) * 16 + CodePairHi(uint32_t(tid))];
     ptab[i * 256 + tid] = int16_t(v);
   }
   const float inv = a.inv[qi];

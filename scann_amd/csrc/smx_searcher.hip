@@ -216,9 +216,9 @@ int UploadIndex(const smx_index_desc* d, smx_index* h) {
   }
 
   // Code tiles: lane l = h*32 + r of tile j of a leaf holds, as nibbles
-  // s = 0..K-1 (low nibble first), the codes of datapoint 32j + r for blocks
-  // 2s + h.  Missing datapoints / blocks are code 0 against a zero LUT row or
-  // are masked in the epilogue.
+  // s = 0..K-1 (two per byte, then EncodeCodePair), the codes of datapoint
+  // 32j + r for blocks 2s + h.  Missing datapoints / blocks are code 0
+  // against a zero LUT row or are masked in the epilogue.
   std::vector<uint8_t> tiles(size_t(ix.num_tiles) * 64 * W, 0);
   for (int l = 0; l < nl; ++l) {
     const uint64_t beg = d->leaf_offsets[l];
@@ -234,6 +234,7 @@ int UploadIndex(const smx_index_desc* d, smx_index* h) {
       }
     }
   }
+  for (auto& by : tiles) by = uint8_t(smx::EncodeCodePair(by & 15u, by >> 4));
   (void)K;
 
   // Transposed centers and squared norms (A.10 database side).

@@ -47,7 +47,7 @@ def main():
         torch.cuda.synchronize()
         wall_ms = (time.perf_counter() - tw) * 1000.0 / 50
         nat.set_profiling(True)
-        mfma_tops = acc["scan_item_tiles"] * 25 * 65536 / (acc["scan_ms"] * 1e-3) / 1e12
+        mfma_tops = acc["scan_item_tiles"] * 26 * 65536 / (acc["scan_ms"] * 1e-3) / 1e12
         print(f"var={variant} chunk={chunk:3d} cap={cap:5d} seed={seed:2d} total={acc['total_ms']:.3f} part={acc['partition_ms']:.3f} "
               f"lut={acc['lut_ms']:.3f} inv={acc['invert_ms']:.3f} seed={acc['seed_scan_ms']:.3f} "
               f"scan={acc['scan_ms']:.3f} sel={acc['select_ms']:.3f} retries={acc['overflow_retries']:.1f} "
