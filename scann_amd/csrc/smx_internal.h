@@ -250,7 +250,7 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count,
                           ItemLane* lanes /*[max items][32]*/, uint4* wave_start /*[grid]*/,
                           int grid, uint32_t* totals /*[3]*/,
                           unsigned long long* code_bytes /*[1]*/, uint32_t chunk_tiles,
-                          hipStream_t s);
+                          unsigned long long* part /*[4 * ceil(nl / 256)]*/, hipStream_t s);
 // variant 0: the LUT16 scan (lut16_scan_kernel); 4: the same without its
 // threshold epilogue (timing ablation, results invalid).
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,

@@ -337,15 +337,18 @@ struct LutParams {
 // them at once (clamped indices, no guarded loads: a guarded load waits on its
 // own), then accumulated in the reference's order.
 __device__ void BuildLut(int qi, const LutParams& p) {
-  __shared__ float red[4];
+  __shared__ float red[16];
   constexpr int kPer = (kMaxBlocks * 16) / 256;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  // the table's entries belong to the first 256 threads; a larger block's
+  // other threads only take part in the reduction's barrier
+  const bool act = t < 256;
   const float* q = p.queries + size_t(qi) * p.dim;
   const int nb = p.nb, dpb = p.dpb;
   const int nent = nb * 16;
   const int last = p.dim - dpb * (nb - 1);
   float raw[kPer];
-  for (int i = 0; i < dpb; ++i) {
+  for (int i = 0; act && i < dpb; ++i) {
     float qv[kPer], cv[kPer];
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
@@ -374,20 +377,21 @@ __device__ void BuildLut(int qi, const LutParams& p) {
   for (int u = 0; u < kPer; ++u) {
     const int e = t + 256 * u;
     float v = 0.0f;
-    if (e < nent) v = p.metric == 0 ? -raw[u] : raw[u];
+    if (act && e < nent) v = p.metric == 0 ? -raw[u] : raw[u];
     raw[u] = v;
     local_max = fmaxf(local_max, fabsf(v));
   }
   for (int off = 32; off > 0; off >>= 1) local_max = fmaxf(local_max, __shfl_xor(local_max, off));
   if (lane == 0) red[wid] = local_max;
   __syncthreads();
-  local_max = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  local_max = red[0];
+  for (int w = 1; w < int(blockDim.x >> 6); ++w) local_max = fmaxf(local_max, red[w]);
   const float m = __fdiv_rn(127.0f, fmaxf(SqrtFltEps(), local_max));
   const int tot = p.padded_blocks * 16;
 #pragma unroll
   for (int u = 0; u < kPer; ++u) {
     const int e = t + 256 * u;
-    if (e < tot) {
+    if (act && e < tot) {
       int8_t v8 = 0;
       if (e < nent) {
         const float r = roundf(__fmul_rn(raw[u], m));
@@ -429,156 +433,175 @@ __device__ void TopLFinish(int qi, int L, uint32_t m, const uint64_t* sel, int32
   }
 }
 
-// Exact top-L by (score, center index) with one 256-thread block per query,
-// the row in registers (VPT scores per thread, nl <= 256 * VPT; a block per
-// query, not a wave: 1000 queries must fill 1024 SIMDs several waves deep).
-// Linear 256-bin histograms of the ordered score bits between the row's
-// current [lo, hi] (radix digits of nearby floats would all hit one bin)
-// narrow down to the bin holding the L-th score until at most 256 keys are
-// left; every key below that bin and the keys inside it are compacted in LDS
-// and ordered by a counting rank over (score, leaf) (keys are unique), of
-// which the first L are kept.  Then the pairs' ranks in their leaves' lists
-// and the query's LUT (the front end's tail, as TopLFinish).
-constexpr int kWaveTopL = 256;         // L limit of the register top-L kernel
+// Exact top-L by (score, center index) with one NT-thread block per query,
+// the row in registers (VPT scores per thread, nl <= NT * VPT; a block per
+// query, not a wave: 1000 queries must fill 1024 SIMDs several waves deep;
+// NT = 1024 for 10^4 - 6.5 * 10^4 leaves).  Linear 256-bin histograms of the
+// ordered score bits between the boundary set's [LO, HI] (radix digits of
+// nearby floats would all hit one bin) narrow down to the bin holding the
+// L-th score until at most 256 keys are left.  The boundary set is always a
+// value range, so a score's state needs no register: below LO = taken,
+// inside [LO, HI] = boundary, above HI = out.  Every taken key and the
+// boundary keys are compacted in LDS and ordered by a counting rank over
+// (score, leaf) (keys are unique), of which the first L are kept.  Then the
+// pairs' ranks in their leaves' lists and the query's LUT (TopLFinish's
+// tail).
+constexpr int kWaveTopL = 512;         // L limit of the register top-L kernel
 constexpr int kBlockTopCand = 1024;    // compacted keys one block orders
 constexpr uint32_t kTopNarrow = 256;   // histogram rounds until this many keys
 
-template <int VPT>
-__global__ void __launch_bounds__(256) topl_block_kernel(const float* __restrict__ scores, int nl,
-                                                         int L, int32_t* __restrict__ out_leaf,
-                                                         float* __restrict__ out_dist, TopLTail tail) {
+template <int VPT, int NT>
+__global__ void __launch_bounds__(NT) topl_block_kernel(const float* __restrict__ scores, int nl,
+                                                        int L, int32_t* __restrict__ out_leaf,
+                                                        float* __restrict__ out_dist, TopLTail tail) {
+  constexpr int NWV = NT / 64;
   __shared__ uint32_t hist[256];
   __shared__ uint64_t sel[kBlockTopCand];
   __shared__ uint64_t srt[kWaveTopL];
-  __shared__ uint32_t wsum[4], s_lo[4], s_hi[4], s_wave[4], s_bin, s_cum, s_hb, s_cnt, s_cnt2;
+  __shared__ uint32_t s_lo[NWV], s_hi[NWV], s_wave[NWV], s_bin, s_cum, s_hb, s_cnt, s_cnt2;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int qi = blockIdx.x;
   SMX_PHASE(0, qi, 0);
   const float* row = scores + size_t(qi) * nl;
   const uint64_t lanes_below = (1ull << lane) - 1ull;
   // every load issued before the first use (clamped index, no guarded load)
-  float f[VPT];
-#pragma unroll
-  for (int u = 0; u < VPT; ++u) f[u] = row[min(tid + 256 * u, nl - 1)];
-  // per score: its ordered bits and its state: 0 = taken (below the
-  // boundary bin), 1 = boundary candidate, 2 = out
   uint32_t v[VPT];
-  uint8_t st[VPT];
 #pragma unroll
-  for (int u = 0; u < VPT; ++u) {
-    const int cix = tid + 256 * u;
-    v[u] = cix < nl ? OrderedBits(f[u]) : 0xFFFFFFFFu;
-    st[u] = cix < nl ? 1 : 2;
-  }
+  for (int u = 0; u < VPT; ++u) v[u] = __float_as_uint(row[min(tid + NT * u, nl - 1)]);
+#pragma unroll
+  for (int u = 0; u < VPT; ++u) v[u] = OrderedBits(__uint_as_float(v[u]));
+  auto valid = [&](int u) { return tid + NT * u < nl; };
   if (tid == 0) { s_cnt = 0; s_cnt2 = 0; }
-  __syncthreads();   // the counters are zero before any wave's compaction
+  // block-wide min / max of the boundary keys in [lo, hi] with bin `b` under
+  // (lo, scale) (b < 0: every key in [lo, hi])
+  auto minmax = [&](uint32_t lo, uint32_t hi, uint64_t scale, int b, uint32_t& mn, uint32_t& mx) {
+    mn = 0xFFFFFFFFu;
+    mx = 0;
+#pragma unroll
+    for (int u = 0; u < VPT; ++u)
+      if (valid(u) && v[u] >= lo && v[u] <= hi &&
+          (b < 0 || int((uint64_t(v[u] - lo) * scale) >> 32) == b)) {
+        mn = min(mn, v[u]);
+        mx = max(mx, v[u]);
+      }
+    for (int off = 32; off > 0; off >>= 1) {
+      mn = min(mn, uint32_t(__shfl_xor(int(mn), off)));
+      mx = max(mx, uint32_t(__shfl_xor(int(mx), off)));
+    }
+    if (lane == 0) { s_lo[wid] = mn; s_hi[wid] = mx; }
+    __syncthreads();
+    mn = s_lo[0];
+    mx = s_hi[0];
+#pragma unroll
+    for (int w = 1; w < NWV; ++w) {
+      mn = min(mn, s_lo[w]);
+      mx = max(mx, s_hi[w]);
+    }
+    __syncthreads();   // s_lo / s_hi are rewritten by the next call
+  };
   SMX_PHASE(0, qi, 1);
   const uint32_t m = min(uint32_t(L), uint32_t(nl));
   uint32_t below = 0, incnt = uint32_t(nl);
-  uint32_t lo = 0, hi = 0;
-  for (int round = 0; round < 8 && m > 0 && below + incnt > kTopNarrow; ++round) {
-    lo = 0xFFFFFFFFu;
-    hi = 0;
+  uint32_t LO = 0, HI = 0xFFFFFFFFu;
+  minmax(LO, HI, 0, -1, LO, HI);
+  for (int round = 0; round < 8 && m > 0 && below + incnt > kTopNarrow && LO < HI; ++round) {
+    // bin = floor((v - LO) * scale / 2^32), scale = floor(255.99 * 2^32 / span):
+    // monotone in v, 0 at LO, <= 255 at HI (no division per value)
+    const uint64_t scale = ((uint64_t(255) << 32) + 0xFFFFFFFFull) / (uint64_t(HI - LO));
+    for (int i = tid; i < 256; i += NT) hist[i] = 0;
+    __syncthreads();
 #pragma unroll
     for (int u = 0; u < VPT; ++u)
-      if (st[u] == 1) {
-        lo = min(lo, v[u]);
-        hi = max(hi, v[u]);
+      if (valid(u) && v[u] >= LO && v[u] <= HI)
+        atomicAdd(&hist[uint32_t((uint64_t(v[u] - LO) * scale) >> 32)], 1u);
+    __syncthreads();
+    if (wid == 0) {   // wave 0: inclusive scan of 4 bins per lane, the bin of the m-th key
+      const uint32_t h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2],
+                     h3 = hist[4 * lane + 3];
+      uint32_t incl = h0 + h1 + h2 + h3;
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = uint32_t(__shfl_up(int(incl), off));
+        if (lane >= off) incl += t;
       }
-    for (int off = 32; off > 0; off >>= 1) {
-      lo = min(lo, uint32_t(__shfl_xor(int(lo), off)));
-      hi = max(hi, uint32_t(__shfl_xor(int(hi), off)));
+      const uint32_t excl = incl - (h0 + h1 + h2 + h3);
+      const uint32_t need = m - below;
+      if (excl < need && incl >= need) {
+        const uint32_t h[4] = {h0, h1, h2, h3};
+        uint32_t cum = excl;
+        int u = 0;
+        while (cum + h[u] < need) { cum += h[u]; ++u; }
+        s_bin = uint32_t(4 * lane + u);
+        s_cum = cum;
+        s_hb = h[u];
+      }
     }
-    if (lane == 0) { s_lo[wid] = lo; s_hi[wid] = hi; }
-    hist[tid] = 0;
     __syncthreads();
-    lo = min(min(s_lo[0], s_lo[1]), min(s_lo[2], s_lo[3]));
-    hi = max(max(s_hi[0], s_hi[1]), max(s_hi[2], s_hi[3]));
-    if (lo == hi) break;   // block-uniform: one value left in the boundary set
-    // bin = floor((v - lo) * scale / 2^32), scale = floor(255.99 * 2^32 / span):
-    // monotone in v, 0 at lo, <= 255 at hi (no division per value)
-    const uint64_t scale = ((uint64_t(255) << 32) + 0xFFFFFFFFull) / (uint64_t(hi - lo));
-#pragma unroll
-    for (int u = 0; u < VPT; ++u)
-      if (st[u] == 1) atomicAdd(&hist[uint32_t((uint64_t(v[u] - lo) * scale) >> 32)], 1u);
-    __syncthreads();
-    const uint32_t hv = hist[tid];
-    const uint32_t inc = BlockInclusiveScan256(hv, wsum);
-    const uint32_t need = m - below;
-    if (inc - hv < need && inc >= need) { s_bin = uint32_t(tid); s_cum = inc - hv; s_hb = hv; }
-    __syncthreads();
-    const uint32_t bsel = s_bin;
+    const int bsel = int(s_bin);
     below += s_cum;
     incnt = s_hb;
-#pragma unroll
-    for (int u = 0; u < VPT; ++u)
-      if (st[u] == 1) {
-        const uint32_t bn = uint32_t((uint64_t(v[u] - lo) * scale) >> 32);
-        st[u] = bn < bsel ? 0 : bn > bsel ? 2 : 1;
-      }
-    __syncthreads();   // hist, wsum, s_lo and s_bin are rewritten by the next round
+    minmax(LO, HI, scale, bsel, LO, HI);   // the selected bin's value range
   }
   SMX_PHASE(0, qi, 2);
-  // the taken keys and the boundary candidates, in LDS (one LDS atomic per wave)
+  // the taken keys and the boundary keys, in LDS (one LDS atomic per wave)
 #pragma unroll
   for (int u = 0; u < VPT; ++u) {
-    const bool in = st[u] <= 1;
+    const bool in = valid(u) && v[u] <= HI;
     const uint64_t bal = __ballot(in);
     uint32_t base = 0;
     if (lane == 0 && bal) base = atomicAdd(&s_cnt, uint32_t(__popcll(bal)));
     base = uint32_t(__shfl(int(base), 0));
     if (in) {
       const uint32_t pos = base + uint32_t(__popcll(bal & lanes_below));
-      if (pos < uint32_t(kBlockTopCand)) sel[pos] = (uint64_t(v[u]) << 32) | uint32_t(tid + 256 * u);
+      if (pos < uint32_t(kBlockTopCand)) sel[pos] = (uint64_t(v[u]) << 32) | uint32_t(tid + NT * u);
     }
   }
   __syncthreads();
   const uint32_t cnt = s_cnt;
   if (cnt <= uint32_t(kBlockTopCand)) {
     // counting rank over (score, leaf), keys unique; keep the first m
-    for (uint32_t i = tid; i < cnt; i += 256) {
+    for (uint32_t i = tid; i < cnt; i += NT) {
       const uint64_t key = sel[i];
       const uint32_t r = CountLess(sel, cnt, key);
       if (r < m) srt[r] = key;
     }
   } else {
-    // more than kBlockTopCand keys on one boundary value (lo == hi, e.g. an
+    // more than kBlockTopCand keys on one boundary value (LO == HI, e.g. an
     // all-equal row): the keys below it by rank, then the lowest-index ties
-    // in index order (index c = tid + 256 u: u-major, then thread order)
-    const uint32_t T = lo;
+    // in index order (index c = tid + NT u: u-major, then thread order)
+    const uint32_t T = LO;
     __syncthreads();   // every thread has read s_cnt; sel is rewritten
 #pragma unroll
     for (int u = 0; u < VPT; ++u) {
-      const bool in = st[u] == 0;
+      const bool in = valid(u) && v[u] < T;
       const uint64_t bal = __ballot(in);
       uint32_t base = 0;
       if (lane == 0 && bal) base = atomicAdd(&s_cnt2, uint32_t(__popcll(bal)));
       base = uint32_t(__shfl(int(base), 0));
-      if (in) sel[base + uint32_t(__popcll(bal & lanes_below))] = (uint64_t(v[u]) << 32) | uint32_t(tid + 256 * u);
+      if (in) sel[base + uint32_t(__popcll(bal & lanes_below))] = (uint64_t(v[u]) << 32) | uint32_t(tid + NT * u);
     }
     __syncthreads();
     const uint32_t c2 = s_cnt2;   // == below < m
-    for (uint32_t i = tid; i < c2; i += 256) {
+    for (uint32_t i = tid; i < c2; i += NT) {
       const uint64_t key = sel[i];
       srt[CountLess(sel, c2, key)] = key;
     }
     uint32_t ties = 0;
 #pragma unroll
     for (int u = 0; u < VPT; ++u) {
-      const bool te = st[u] == 1;
+      const bool te = valid(u) && v[u] == T;
       const uint64_t bal = __ballot(te);
       if (lane == 0) s_wave[wid] = uint32_t(__popcll(bal));
       __syncthreads();
       uint32_t before = ties + uint32_t(__popcll(bal & lanes_below));
       for (int w = 0; w < wid; ++w) before += s_wave[w];
-      if (te && c2 + before < m) srt[c2 + before] = (uint64_t(T) << 32) | uint32_t(tid + 256 * u);
-      ties += s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+      if (te && c2 + before < m) srt[c2 + before] = (uint64_t(T) << 32) | uint32_t(tid + NT * u);
+      for (int w = 0; w < NWV; ++w) ties += s_wave[w];
       __syncthreads();   // s_wave is rewritten by the next u
     }
   }
   __syncthreads();
   SMX_PHASE(0, qi, 3);
-  for (int i = tid; i < L; i += 256) {
+  for (int i = tid; i < L; i += NT) {
     const bool has = uint32_t(i) < m;
     const int32_t leaf = has ? int32_t(srt[i] & 0xFFFFFFFFu) : -1;
     out_leaf[size_t(qi) * L + i] = leaf;
@@ -738,104 +761,129 @@ __device__ __forceinline__ uint32_t LeafUnits(uint32_t c, uint32_t n, uint32_t c
   return qt * ((n + 31u) / 32u);
 }
 
-// Phase 1 (one block): prefixes over the leaves in work order -- each leaf's
-// first item (leaf_item0) and first unit (pos_unit0, by position), the 8
-// groups' unit boundaries (gunits[0..8]; gunits[8] = all units) -- and the
-// totals.
-__global__ void __launch_bounds__(1024) worklist_kernel(
-    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ order,
-    const uint32_t* __restrict__ leaf_size, int nl, int nb, uint32_t chunk_tiles,
-    uint32_t* __restrict__ leaf_item0, uint32_t* __restrict__ pos_unit0,
-    uint32_t* __restrict__ gunits, uint32_t* __restrict__ totals,
-    unsigned long long* __restrict__ code_bytes, int grid, uint4* __restrict__ wave_start) {
-  __shared__ uint32_t s_items[1024], s_wt[1024], s_pairs[1024];
-  __shared__ unsigned long long s_bytes[1024];
-  const int tid = threadIdx.x;
-  const int nt = blockDim.x;
-  const int per = (nl + nt - 1) / nt;
-  const int beg = tid * per;
-  const int end = min(nl, beg + per);
-  uint32_t sp = 0, st = 0, sw = 0;
-  unsigned long long sb = 0;
-  for (int p = beg; p < end; ++p) {
+// Phase 1 in two multi-block passes over the leaf positions in work order
+// (256 positions per block; one single-block pass over 10^4 - 5 * 10^4
+// leaves took 0.1 ms of dependent loads): per block the sums of its
+// positions' items, units, pairs and code bytes; then every block adds the
+// sums of the blocks before it to its own block scan -- each leaf's first
+// item (leaf_item0) and first unit (pos_unit0, by position), the 8 groups'
+// unit boundaries (gunits[0..8]; gunits[8] = all units) and the totals.
+struct WorklistPart {
+  unsigned long long items, units, pairs, bytes;
+};
+
+__device__ __forceinline__ void PositionWork(const uint32_t* __restrict__ cnt,
+                                             const uint32_t* __restrict__ order,
+                                             const uint32_t* __restrict__ leaf_size, int nl,
+                                             int nb, uint32_t chunk_tiles, int p, uint32_t& items,
+                                             uint32_t& units, uint32_t& pairs, uint64_t& bytes) {
+  items = units = pairs = 0;
+  bytes = 0;
+  if (p < nl) {
     const uint32_t leaf = order[p];
     const uint32_t c = cnt[size_t(leaf) * kCounterStride], n = leaf_size[leaf];
-    uint32_t items;
-    sw += LeafUnits(c, n, chunk_tiles, items);
-    st += items;
-    sp += c;
+    units = LeafUnits(c, n, chunk_tiles, items);
+    pairs = c;
     // algorithmic code bytes: 16 * B * ceil(n / 32) per (query, leaf) pair
-    sb += 16ull * nb * ((n + 31u) / 32u) * c;
+    bytes = 16ull * nb * ((n + 31u) / 32u) * c;
   }
-  s_items[tid] = st;
-  s_wt[tid] = sw;
-  s_pairs[tid] = sp;
-  s_bytes[tid] = sb;
+}
+
+__global__ void __launch_bounds__(256) worklist_part_kernel(
+    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ order,
+    const uint32_t* __restrict__ leaf_size, int nl, int nb, uint32_t chunk_tiles,
+    WorklistPart* __restrict__ part) {
+  __shared__ unsigned long long red[4][4];
+  uint32_t items, units, pairs;
+  uint64_t bytes;
+  PositionWork(cnt, order, leaf_size, nl, nb, chunk_tiles, int(blockIdx.x * 256 + threadIdx.x),
+               items, units, pairs, bytes);
+  unsigned long long v[4] = {items, units, pairs, bytes};
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
+    if (lane == 0) red[wid][k] = v[k];
+  }
   __syncthreads();
-  for (int off = nt / 2; off > 0; off >>= 1) {
-    if (tid < off) {
-      s_bytes[tid] += s_bytes[tid + off];
-      s_pairs[tid] += s_pairs[tid + off];
-    }
-    __syncthreads();
+  if (threadIdx.x == 0) {
+    WorklistPart w;
+    w.items = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+    w.units = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+    w.pairs = red[0][2] + red[1][2] + red[2][2] + red[3][2];
+    w.bytes = red[0][3] + red[1][3] + red[2][3] + red[3][3];
+    part[blockIdx.x] = w;
   }
-  if (tid == 0) {
-    code_bytes[0] = s_bytes[0];
-    totals[0] = s_pairs[0];
+}
+
+__global__ void __launch_bounds__(256) worklist_kernel(
+    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ order,
+    const uint32_t* __restrict__ leaf_size, int nl, int nb, uint32_t chunk_tiles,
+    const WorklistPart* __restrict__ part, uint32_t* __restrict__ leaf_item0,
+    uint32_t* __restrict__ pos_unit0, uint32_t* __restrict__ gunits, uint32_t* __restrict__ totals,
+    unsigned long long* __restrict__ code_bytes) {
+  __shared__ unsigned long long red[4][6];
+  __shared__ uint32_t wsum[4], s_units[256];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nblk = int(gridDim.x), blk = int(blockIdx.x);
+  // the blocks before this one and all blocks (nblk <= 256 for nl <= 65536)
+  unsigned long long bi = 0, bu = 0, ti = 0, tu = 0, tp = 0, tb = 0;
+  for (int b = tid; b < nblk; b += 256) {
+    const WorklistPart w = part[b];
+    if (b < blk) { bi += w.items; bu += w.units; }
+    ti += w.items; tu += w.units; tp += w.pairs; tb += w.bytes;
   }
-  for (int off = 1; off < nt; off <<= 1) {
-    uint32_t y = 0, z = 0;
-    if (tid >= off) {
-      y = s_items[tid - off];
-      z = s_wt[tid - off];
-    }
-    __syncthreads();
-    s_items[tid] += y;
-    s_wt[tid] += z;
-    __syncthreads();
+  unsigned long long v[6] = {bi, bu, ti, tu, tp, tb};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
+    if (lane == 0) red[wid][k] = v[k];
   }
-  const uint32_t total_w = s_wt[nt - 1];
-  const uint64_t wdiv = max(1u, total_w);
-  uint32_t rt = tid ? s_items[tid - 1] : 0;
-  uint32_t rw = tid ? s_wt[tid - 1] : 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 6; ++k) v[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+  const uint32_t total_w = uint32_t(v[3]);
+  if (blk == 0 && tid == 0) {
+    totals[0] = uint32_t(v[4]);
+    totals[1] = uint32_t(v[2]);
+    totals[2] = total_w;
+    code_bytes[0] = v[5];
+  }
+  const int p = blk * 256 + tid;
+  uint32_t items, units, pairs;
+  uint64_t bytes;
+  PositionWork(cnt, order, leaf_size, nl, nb, chunk_tiles, p, items, units, pairs, bytes);
+  const uint32_t inc_i = BlockInclusiveScan256(items, wsum);
+  __syncthreads();   // wsum is reused
+  const uint32_t inc_u = BlockInclusiveScan256(units, wsum);
+  s_units[tid] = units;
+  __syncthreads();
+  if (p >= nl) return;
+  const uint32_t ex_i = uint32_t(v[0]) + inc_i - items;
+  const uint32_t ex_u = uint32_t(v[1]) + inc_u - units;
+  leaf_item0[order[p]] = ex_i;
+  pos_unit0[p] = ex_u;
   // group boundaries: the first position whose exclusive unit prefix puts it
   // in group g (g = 8 * prefix / total); the groups are contiguous ranges
+  const uint64_t wdiv = max(1u, total_w);
   auto group_of = [&](uint32_t excl_w) {
     return int(min<uint64_t>(kGroups - 1, (uint64_t(kGroups) * excl_w) / wdiv));
   };
-  int prev = tid == 0 ? -1 : (beg < end ? group_of(rw) : kGroups);
-  if (tid > 0 && beg < end) {
-    // group of the previous thread's last position
-    const int pp = beg - 1;
-    const uint32_t leaf = order[pp];
-    uint32_t items;
-    prev = group_of(rw - LeafUnits(cnt[size_t(leaf) * kCounterStride], leaf_size[leaf], chunk_tiles, items));
+  const int gp = group_of(ex_u);
+  int prev = -1;
+  if (p > 0) {
+    const uint32_t prev_units = tid > 0 ? s_units[tid - 1] : [&] {
+      uint32_t it, un, pa;
+      uint64_t by;
+      PositionWork(cnt, order, leaf_size, nl, nb, chunk_tiles, p - 1, it, un, pa, by);
+      return un;
+    }();
+    prev = group_of(ex_u - prev_units);
   }
-  for (int p = beg; p < end; ++p) {
-    const uint32_t leaf = order[p];
-    const int gp = group_of(rw);
-    for (int gg = prev + 1; gg <= gp; ++gg) gunits[gg] = rw;
-    prev = gp;
-    leaf_item0[leaf] = rt;
-    pos_unit0[p] = rw;
-    uint32_t items;
-    rw += LeafUnits(cnt[size_t(leaf) * kCounterStride], leaf_size[leaf], chunk_tiles, items);
-    rt += items;
-  }
-  if (beg < end && end == nl) {
-    for (int gg = prev + 1; gg <= kGroups; ++gg) gunits[gg] = total_w;
+  for (int gg = prev + 1; gg <= gp; ++gg) gunits[gg] = ex_u;
+  if (p == nl - 1) {
+    for (int gg = gp + 1; gg <= kGroups; ++gg) gunits[gg] = total_w;
     pos_unit0[nl] = total_w;
-  }
-  if (tid == 0) {
-    totals[1] = s_items[nt - 1];
-    totals[2] = total_w;
-  }
-  // the waves of groups without units get an empty share (the items kernel
-  // writes every other wave's share)
-  __syncthreads();
-  for (int i = tid; i < grid; i += nt) {
-    const int g = i & (kGroups - 1);
-    if (gunits[g + 1] == gunits[g]) wave_start[i] = make_uint4(0, 0, 0, 0);
   }
 }
 
@@ -852,6 +900,14 @@ __global__ void __launch_bounds__(64) items_kernel(
     const uint32_t* __restrict__ gunits, WorkItem* __restrict__ work,
     ItemLane* __restrict__ lanes, uint4* __restrict__ wave_start) {
   const int p = blockIdx.x, lane = threadIdx.x;
+  if (p == 0) {
+    // the waves of groups without units get an empty share (the blocks below
+    // write every other wave's share)
+    for (int i = lane; i < grid; i += 64) {
+      const int g = i & (kGroups - 1);
+      if (gunits[g + 1] == gunits[g]) wave_start[i] = make_uint4(0, 0, 0, 0);
+    }
+  }
   const uint32_t leaf = order[p];
   const uint32_t c = cnt[size_t(leaf) * kCounterStride], n = leaf_size[leaf];
   const uint32_t chunks = LeafChunks(n, chunk_tiles);
@@ -2638,11 +2694,17 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   // raw table and reduction (~5 KB) and the selection's words
   constexpr size_t kStaticLds = 6 * 1024;
   if (L <= kWaveTopL && ix.nl <= 256 * 4) {
-    hipLaunchKernelGGL(topl_block_kernel<4>, dim3(nq), dim3(256), 0, s, scores, ix.nl, L, out_leaf,
-                       out_dist, tail);
+    hipLaunchKernelGGL((topl_block_kernel<4, 256>), dim3(nq), dim3(256), 0, s, scores, ix.nl, L,
+                       out_leaf, out_dist, tail);
   } else if (L <= kWaveTopL && ix.nl <= 256 * 8) {
-    hipLaunchKernelGGL(topl_block_kernel<8>, dim3(nq), dim3(256), 0, s, scores, ix.nl, L, out_leaf,
-                       out_dist, tail);
+    hipLaunchKernelGGL((topl_block_kernel<8, 256>), dim3(nq), dim3(256), 0, s, scores, ix.nl, L,
+                       out_leaf, out_dist, tail);
+  } else if (L <= kWaveTopL && ix.nl <= 1024 * 16) {
+    hipLaunchKernelGGL((topl_block_kernel<16, 1024>), dim3(nq), dim3(1024), 0, s, scores, ix.nl,
+                       L, out_leaf, out_dist, tail);
+  } else if (L <= kWaveTopL && ix.nl <= 1024 * 52) {
+    hipLaunchKernelGGL((topl_block_kernel<52, 1024>), dim3(nq), dim3(1024), 0, s, scores, ix.nl,
+                       L, out_leaf, out_dist, tail);
   } else if (ix.nl <= kLdsSelectLeaves && lds + kStaticLds <= 160 * 1024) {
     hipLaunchKernelGGL(topl_select_kernel, dim3(nq), dim3(256), lds, s, scores, ix.nl, L, kcap,
                        out_leaf, out_dist, tail);
@@ -2668,10 +2730,16 @@ hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq, i
 hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, WorkItem* work,
                           uint32_t* leaf_item0, uint32_t* pos_unit0, uint32_t* gunits,
                           ItemLane* lanes, uint4* wave_start, int grid, uint32_t* totals,
-                          unsigned long long* code_bytes, uint32_t chunk_tiles, hipStream_t s) {
-  hipLaunchKernelGGL(worklist_kernel, dim3(1), dim3(1024), 0, s, leaf_count, ix.leaf_order,
-                     ix.leaf_size, ix.nl, ix.nb, chunk_tiles, leaf_item0, pos_unit0, gunits, totals,
-                     code_bytes, grid, wave_start);
+                          unsigned long long* code_bytes, uint32_t chunk_tiles,
+                          unsigned long long* part, hipStream_t s) {
+  const int nblk = (ix.nl + 255) / 256;
+  if (nblk > 256) return hipErrorInvalidValue;   // more than 65536 leaves
+  WorklistPart* wp = reinterpret_cast<WorklistPart*>(part);
+  hipLaunchKernelGGL(worklist_part_kernel, dim3(nblk), dim3(256), 0, s, leaf_count, ix.leaf_order,
+                     ix.leaf_size, ix.nl, ix.nb, chunk_tiles, wp);
+  hipLaunchKernelGGL(worklist_kernel, dim3(nblk), dim3(256), 0, s, leaf_count, ix.leaf_order,
+                     ix.leaf_size, ix.nl, ix.nb, chunk_tiles, wp, leaf_item0, pos_unit0, gunits,
+                     totals, code_bytes);
   hipLaunchKernelGGL(items_kernel, dim3(ix.nl), dim3(64), 0, s, leaf_count, ix.leaf_order,
                      ix.leaf_size, ix.tile_off, ix.member_off, chunk_tiles, grid, leaf_item0,
                      pos_unit0, gunits, work, lanes, wave_start);

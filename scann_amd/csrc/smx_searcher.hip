@@ -104,6 +104,7 @@ struct Workspace {
   uint4* wave_start = nullptr;      // [grid] each scan wave's static share
   uint32_t* pos_unit0 = nullptr;    // [nl+1] work units before each leaf (work order)
   uint32_t* gunits = nullptr;       // [16] the XCD groups' unit boundaries
+  unsigned long long* wl_part = nullptr;   // [4 * ceil(nl / 256)] work-list block sums
   uint64_t* tau = nullptr;          // [nq]
   uint64_t* cand = nullptr;         // [nq][cap]
   uint32_t* cand_count = nullptr;   // [nq] strided (kCounterStride)
@@ -115,7 +116,7 @@ struct Workspace {
     DFree(queries); DFree(topl_leaf); DFree(topl_dist); DFree(scores); DFree(lut); DFree(mult);
     DFree(inv);
     DFree(counters); DFree(rank); DFree(leaf_item0); DFree(lanes); DFree(wave_start);
-    DFree(pos_unit0); DFree(gunits);
+    DFree(pos_unit0); DFree(gunits); DFree(wl_part);
     DFree(work); DFree(tau); DFree(cand); DFree(cand_count); DFree(out_idx);
     DFree(out_dist);
     DFree(out_count);
@@ -379,6 +380,7 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
       (rc = DAlloc(&w.lanes, size_t(max_items) * smx::kQueriesPerTile)) ||
       (rc = DAlloc(&w.wave_start, size_t(std::max(h->grid, 1)))) ||
       (rc = DAlloc(&w.pos_unit0, size_t(nl + 1))) || (rc = DAlloc(&w.gunits, 16)) ||
+      (rc = DAlloc(&w.wl_part, size_t(4) * ((nl + 255) / 256))) ||
       (rc = DAlloc(&w.work, max_items)) || (rc = DAlloc(&w.tau, nq)) ||
       (rc = DAlloc(&w.cand, size_t(nq) * cap)) || (rc = DAlloc(&w.cand_count, size_t(nq) * smx::kCounterStride)) ||
       (rc = DAlloc(&w.out_idx, size_t(nq) * width)) ||
@@ -560,7 +562,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     SMX_HIP(hipStreamWaitEvent(h->side, h->fork_ev, 0));
     SMX_HIP(smx::LaunchWorklist(ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes,
                                 w.wave_start, h->grid, stats + 3, code_bytes, h->chunk_tiles,
-                                h->side));
+                                w.wl_part, h->side));
     SMX_HIP(smx::LaunchPairScatter(ix, sa, nq, h->side));
     Mark(h, 3, h->side);
     SMX_HIP(hipEventRecord(h->join_ev, h->side));
@@ -734,6 +736,8 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
   if (rc) return rc;
   if (EffectiveKSteps(desc->num_blocks) < 0)
     return Fail(SMX_INVALID_ARGUMENT, "unsupported number of AH blocks");
+  if (desc->num_leaves > 65536)
+    return Fail(SMX_INVALID_ARGUMENT, "at most 65536 leaves (work-list block sums)");
   int ndev = 0;
   SMX_HIP(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return Fail(SMX_INVALID_ARGUMENT, "no such HIP device");
