@@ -1496,7 +1496,6 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
     pos_tab[threadIdx.x] = int((threadIdx.x & 3u) * 0x5555u | ((threadIdx.x >> 2) * 0x5555u) << 16);
   }
   const uint32_t worker = blockIdx.x * NWAVES + wv;
-  const WorkItem* __restrict__ work = a.work;
   // this workgroup's share: `units` tiles from tile jfirst of item w on
   const uint4 ws = a.wave_start[blockIdx.x];
   if (threadIdx.x == 0) {
@@ -1792,7 +1791,10 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         uint32_t t = j, tn = 0;
         for (;;) {
           bool more = next_tile(t, tn);
-          if (more) LoadCodes<K>(tb + size_t(tn) * 64 * W, cb);
+          // unconditional (the current tile again when none follows): one
+          // load per tile on every path, so the wait for this tile's codes
+          // leaves the next tile's load in flight (vmcnt(1), not vmcnt(0))
+          LoadCodes<K>(tb + size_t(more ? tn : t) * 64 * W, cb);
           tile(codes, t);
           ++tiles_done;
           if (pending) copy_prev();   // after the segment's first tile: the atomic has returned
@@ -1801,7 +1803,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
           advance(t, tn);
           t = tn;
           more = next_tile(t, tn);
-          if (more) LoadCodes<K>(tb + size_t(tn) * 64 * W, codes);
+          LoadCodes<K>(tb + size_t(more ? tn : t) * 64 * W, codes);
           tile(cb, t);
           ++tiles_done;
           if (!more) break;

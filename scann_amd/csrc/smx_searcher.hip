@@ -136,7 +136,7 @@ struct smx_index {
   uint32_t cap_per_query = 0;      // candidate list capacity; 0 = sized per call (AutoCap)
   int seed_leaves = 4;
   int scan_variant = 0;            // see smx::LaunchScan
-  uint32_t chunk_tiles = 32;       // tiles per work item
+  uint32_t chunk_tiles = 16;       // tiles per work item (tools/tune.py: 16-20 best at glove)
   int grid = 0;                    // scan grid: resident one-wave workgroups (occupancy API)
   bool profiling = false;
   bool use_graph = true;           // replay the first pass as a hipGraph
@@ -369,7 +369,7 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
   w.Release();
   const int nl = ix.nl;
   const size_t pairs = size_t(nq) * L;
-  const uint32_t chunks = (uint32_t((ix.max_leaf + 31) / 32) + 15) / 16 + 1;  // chunk >= 16
+  const uint32_t chunks = (uint32_t((ix.max_leaf + 31) / 32) + 7) / 8 + 1;  // chunk >= 8
   const uint32_t max_items = uint32_t((pairs / smx::kQueriesPerTile + nl + 1) * chunks);
   int rc;
   if ((rc = DAlloc(&w.queries, size_t(nq) * ix.dim)) || (rc = DAlloc(&w.topl_leaf, pairs)) ||
@@ -1114,8 +1114,8 @@ int smx_set_tuning(smx_index* h, int32_t candidates_per_query, int32_t seed_leav
   if (scan_variant != 0 && scan_variant != 4 && scan_variant != 8)
     return Fail(SMX_INVALID_ARGUMENT,
                 "scan_variant is 0 (scan), 4 (timing ablation) or 8 (diagnostic stamps)");
-  if (chunk_tiles != 0 && (chunk_tiles < 16 || chunk_tiles > 65535))
-    return Fail(SMX_INVALID_ARGUMENT, "chunk_tiles must be 0 (default) or in [16, 65535]");
+  if (chunk_tiles != 0 && (chunk_tiles < 8 || chunk_tiles > 65535))
+    return Fail(SMX_INVALID_ARGUMENT, "chunk_tiles must be 0 (default) or in [8, 65535]");
   if (candidates_per_query != 0 && (candidates_per_query < 32 || candidates_per_query > 8192))
     return Fail(SMX_INVALID_ARGUMENT,
                 "candidates_per_query must be 0 (sized per call) or in [32, 8192]");
