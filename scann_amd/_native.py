@@ -88,6 +88,29 @@ def load(path: str = LIB_PATH):
     return lib
 
 
+_pybind = None
+
+
+def load_pybind():
+    """The C++ pybind11 module (ScannNumpyCore, scann_amd/csrc/smx_pybind.cc);
+    raises ImportError (loudly) if it was not built."""
+    global _pybind
+    if _pybind is not None:
+        return _pybind
+    import importlib.machinery
+    import importlib.util
+    import sysconfig
+    path = os.path.join(_HERE, "lib", "_smx_pybind" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if not os.path.exists(path):
+        raise ImportError(f"{path} not found: build it with `python -m scann_amd.build`")
+    loader = importlib.machinery.ExtensionFileLoader("_smx_pybind", path)
+    spec = importlib.util.spec_from_file_location("_smx_pybind", path, loader=loader)
+    mod = importlib.util.module_from_spec(spec)
+    loader.exec_module(mod)
+    _pybind = mod
+    return mod
+
+
 class SmxError(RuntimeError):
     pass
 

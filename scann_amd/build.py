@@ -49,5 +49,36 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str = OUT
     return out
 
 
+PYBIND_SRC = os.path.join(CSRC, "smx_pybind.cc")
+
+
+def pybind_path() -> str:
+    import sysconfig
+    return os.path.join(os.path.dirname(OUT), "_smx_pybind" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_pybind(force: bool = False, verbose: bool = False) -> str:
+    """The C++ pybind11 module (scann_amd/csrc/smx_pybind.cc) over the C ABI,
+    next to the library it links (rpath $ORIGIN)."""
+    import sysconfig
+
+    import pybind11
+    out = pybind_path()
+    deps = [PYBIND_SRC, OUT, os.path.join(ROOT, "include", "scann_mi355x.h")]
+    if not force and os.path.exists(out) and all(
+            os.path.getmtime(out) >= os.path.getmtime(d) for d in deps if os.path.exists(d)):
+        return out
+    tmp = out + f".tmp{os.getpid()}"
+    cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall", "-fvisibility=hidden",
+           f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", PYBIND_SRC,
+           f"-L{os.path.dirname(OUT)}", "-l:libscann_mi355x.so", "-Wl,-rpath,$ORIGIN", "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, out)
+    return out
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_pybind(force="--force" in sys.argv, verbose=True))

@@ -94,7 +94,7 @@ struct ItemLane {
   uint32_t qid;
   float bias;
   float inv;
-  uint32_t pad;
+  int32_t amax;   // the slot's sum limit (pair scatter, after the seed)
 };
 constexpr uint32_t kNoQuery = 0xFFFFFFFFu;     // ItemLane::qid of an empty slot
 constexpr int32_t kNoSum = -2147483647 - 1;   // the sum limit of an empty slot
@@ -141,6 +141,31 @@ struct SeedArgs {
   int residual;
   int nb;
 };
+
+// The work list's inputs and outputs (LaunchWorklist / the fused block of
+// LaunchSeed).
+struct WorklistArgs {
+  const uint32_t* cnt;         // per-leaf query counts (kCounterStride apart)
+  const uint32_t* order;       // leaf positions in work order
+  const uint32_t* leaf_size;
+  const uint64_t* tile_off;
+  const uint64_t* member_off;
+  int nl;
+  int nb;
+  uint32_t chunk_tiles;
+  int grid;                    // scan workgroups
+  uint32_t* leaf_item0;        // [nl]
+  uint32_t* pos_unit0;         // [nl + 1]
+  uint32_t* gunits;            // [9]
+  uint32_t* totals;            // [3] pairs, items, units
+  unsigned long long* code_bytes;
+  WorkItem* work;
+  ItemLane* lanes;
+  uint4* wave_start;           // [grid]
+};
+// Up to this many leaves the work list is built by one extra block of the
+// seed launch (no second stream, no fork/join); above it by three launches.
+constexpr int kFusedWorklistLeaves = 4096;
 
 // An overflowed query's rescan (RescanQuery, inside the select kernels):
 // the query's leaves, LUT and lists, and the code layout of the index.
@@ -258,9 +283,16 @@ hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int va
 // Resident scan workgroups per CU (occupancy of the index's instantiation).
 hipError_t ScanBlocksPerCU(const DeviceIndex& ix, int* blocks);
 // The per-query thresholds (tau_key) from the seed leaves.
-hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s);
+WorklistArgs MakeWorklistArgs(const DeviceIndex& ix, const uint32_t* leaf_count, WorkItem* work,
+                              uint32_t* leaf_item0, uint32_t* pos_unit0, uint32_t* gunits,
+                              ItemLane* lanes, uint4* wave_start, int grid, uint32_t* totals,
+                              unsigned long long* code_bytes, uint32_t chunk_tiles);
+// The seed thresholds (one block per query); with `wl`, one more block
+// builds the whole work list (ix.nl <= kFusedWorklistLeaves).
+hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s,
+                      const WorklistArgs* wl = nullptr);
 // Every (query, leaf) pair's lane record into its leaf's work items (after
-// LaunchWorklist; independent of LaunchSeed).
+// LaunchWorklist and the seed thresholds: each record carries its sum limit).
 hipError_t LaunchPairScatter(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s);
 // The rank kernel (one block per query, <= kSelMax keys in LDS) for k' <=
 // kSelMax, the block kernel otherwise; both rescan overflowed lists first.

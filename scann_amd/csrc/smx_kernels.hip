@@ -887,33 +887,29 @@ __global__ void __launch_bounds__(256) worklist_kernel(
   }
 }
 
-// Phase 2 (one 64-thread block per leaf position): the leaf's work items,
-// the empty query slots of its last query tile, and the start of every scan
-// wave whose share begins inside this leaf.  Wave i of group g (i % 8 == g)
-// takes the units [U0 + span * k / n, U0 + span * (k + 1) / n) of its
-// group, k = i / 8 of the group's n waves.
-__global__ void __launch_bounds__(64) items_kernel(
-    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ order,
-    const uint32_t* __restrict__ leaf_size, const uint64_t* __restrict__ tile_off,
-    const uint64_t* __restrict__ member_off, uint32_t chunk_tiles, int grid,
-    const uint32_t* __restrict__ leaf_item0, const uint32_t* __restrict__ pos_unit0,
-    const uint32_t* __restrict__ gunits, WorkItem* __restrict__ work,
-    ItemLane* __restrict__ lanes, uint4* __restrict__ wave_start) {
-  const int p = blockIdx.x, lane = threadIdx.x;
+// Phase 2 (64 lanes per leaf position): the leaf's work items, the empty
+// query slots of its last query tile, and the start of every scan wave whose
+// share begins inside this leaf.  Wave i of group g (i % 8 == g) takes the
+// units [U0 + span * k / n, U0 + span * (k + 1) / n) of its group, k = i / 8
+// of the group's n waves.
+// (item0 = the leaf's first item, [ua, ub) = its units, gunits = the 8
+// groups' unit boundaries)
+__device__ void ItemsCore(const WorklistArgs& w, int p, int lane, const uint32_t* gunits,
+                          uint32_t item0, uint32_t ua, uint32_t ub) {
   if (p == 0) {
-    // the waves of groups without units get an empty share (the blocks below
-    // write every other wave's share)
-    for (int i = lane; i < grid; i += 64) {
+    // the waves of groups without units get an empty share (the other
+    // positions write every other wave's share)
+    for (int i = lane; i < w.grid; i += 64) {
       const int g = i & (kGroups - 1);
-      if (gunits[g + 1] == gunits[g]) wave_start[i] = make_uint4(0, 0, 0, 0);
+      if (gunits[g + 1] == gunits[g]) w.wave_start[i] = make_uint4(0, 0, 0, 0);
     }
   }
-  const uint32_t leaf = order[p];
-  const uint32_t c = cnt[size_t(leaf) * kCounterStride], n = leaf_size[leaf];
+  const uint32_t chunk_tiles = w.chunk_tiles;
+  const uint32_t leaf = w.order[p];
+  const uint32_t c = w.cnt[size_t(leaf) * kCounterStride], n = w.leaf_size[leaf];
   const uint32_t chunks = LeafChunks(n, chunk_tiles);
   const uint32_t qt = (c + kQueriesPerTile - 1) / kQueriesPerTile;
-  const uint32_t item0 = leaf_item0[leaf];
-  const uint64_t toff = tile_off[leaf], moff = member_off[leaf];
+  const uint64_t toff = w.tile_off[leaf], moff = w.member_off[leaf];
   for (uint32_t u = lane; u < qt * chunks; u += 64) {
     const uint2 cr = ChunkTiles(n, chunk_tiles, u % chunks);
     WorkItem it;
@@ -923,7 +919,7 @@ __global__ void __launch_bounds__(64) items_kernel(
     it.jend = cr.y;
     it.tile_off = toff;
     it.member_off = moff;
-    work[item0 + u] = it;
+    w.work[item0 + u] = it;
   }
   if (qt) {
     const uint32_t first = c - (qt - 1) * kQueriesPerTile;   // empty slots [first, 32)
@@ -933,16 +929,15 @@ __global__ void __launch_bounds__(64) items_kernel(
       v.qid = kNoQuery;
       v.bias = 0.0f;
       v.inv = 0.0f;
-      v.pad = 0;
-      lanes[size_t(item0 + (qt - 1) * chunks + e / ne) * kQueriesPerTile + first + e % ne] = v;
+      v.amax = kNoSum;   // never passes
+      w.lanes[size_t(item0 + (qt - 1) * chunks + e / ne) * kQueriesPerTile + first + e % ne] = v;
     }
   }
   // the waves whose share starts in this leaf's units [ua, ub)
-  const uint32_t ua = pos_unit0[p], ub = pos_unit0[p + 1];
   if (ua >= ub) return;
   const uint32_t wdiv = max(1u, gunits[kGroups]);
   const int g = int(min<uint64_t>(kGroups - 1, (uint64_t(kGroups) * ua) / wdiv));
-  const uint32_t nw = uint32_t(grid - g + kGroups - 1) / kGroups;
+  const uint32_t nw = uint32_t(w.grid - g + kGroups - 1) / kGroups;
   const uint32_t U0 = gunits[g], span = gunits[g + 1] - U0;
   // the first k with U0 + span*k/nw >= ua
   uint32_t k = uint32_t((uint64_t(ua - U0) * nw + span - 1) / span);
@@ -955,10 +950,113 @@ __global__ void __launch_bounds__(64) items_kernel(
     const uint32_t off = us - ua, tq = off / tiles, rem = off % tiles;
     uint32_t ch = 0;
     while (ChunkTiles(n, chunk_tiles, ch).y <= rem) ++ch;
-    wave_start[kGroups * k + g] = make_uint4(item0 + tq * chunks + ch, rem, ue - us, 0);
+    w.wave_start[kGroups * k + g] = make_uint4(item0 + tq * chunks + ch, rem, ue - us, 0);
   }
 }
 
+__global__ void __launch_bounds__(64) items_kernel(WorklistArgs w) {
+  const int p = int(blockIdx.x);
+  ItemsCore(w, p, int(threadIdx.x), w.gunits, w.leaf_item0[w.order[p]], w.pos_unit0[p],
+            w.pos_unit0[p + 1]);
+}
+
+// The work list without extra launches (nl <= kFusedWorklistLeaves): extra
+// blocks of the seed launch, each of which scans ALL positions redundantly
+// (16 per thread: two rounds of independent loads, then block scans) and
+// builds the items of its own kWlPosPerBlock positions, one wave each.  No
+// block waits for another; block 0 also writes the global prefixes (the pair
+// scatter reads leaf_item0) and totals.  The seed blocks neither read nor
+// write anything these touch.
+constexpr int kWlPerThread = kFusedWorklistLeaves / 256;
+constexpr int kWlPosPerBlock = 4;
+
+__device__ void WorklistFusedBlock(const WorklistArgs& w, int b) {
+  __shared__ uint32_t wsum[4], s_gunits[kGroups + 1], s_last_un[256];
+  __shared__ uint32_t s_ex_i[kWlPosPerBlock], s_ex_u[kWlPosPerBlock + 1];
+  __shared__ unsigned long long red[4][2];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nl = w.nl, p0 = tid * kWlPerThread;
+  const int pb = b * kWlPosPerBlock, pe = min(nl, pb + kWlPosPerBlock);
+  uint32_t leafv[kWlPerThread], itv[kWlPerThread], unv[kWlPerThread];
+#pragma unroll
+  for (int k = 0; k < kWlPerThread; ++k) leafv[k] = p0 + k < nl ? w.order[p0 + k] : 0u;
+  uint32_t ti = 0, tu = 0;
+  unsigned long long tp = 0, tb = 0;
+#pragma unroll
+  for (int k = 0; k < kWlPerThread; ++k) {
+    itv[k] = unv[k] = 0;
+    if (p0 + k < nl) {
+      const uint32_t leaf = leafv[k];
+      const uint32_t c = w.cnt[size_t(leaf) * kCounterStride], n = w.leaf_size[leaf];
+      unv[k] = LeafUnits(c, n, w.chunk_tiles, itv[k]);
+      tp += c;
+      tb += 16ull * w.nb * ((n + 31u) / 32u) * c;   // algorithmic code bytes
+    }
+    ti += itv[k];
+    tu += unv[k];
+  }
+  s_last_un[tid] = unv[kWlPerThread - 1];
+  const uint32_t inc_i = BlockInclusiveScan256(ti, wsum);
+  __syncthreads();   // wsum is reused
+  const uint32_t inc_u = BlockInclusiveScan256(tu, wsum);
+  const uint32_t total_w = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  if (b == 0) {
+    unsigned long long v[2] = {tp, tb};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
+      if (lane == 0) red[wid][k] = v[k];
+    }
+  }
+  __syncthreads();   // s_last_un, red
+  if (b == 0 && tid == 255) {
+    w.totals[0] = uint32_t(red[0][0] + red[1][0] + red[2][0] + red[3][0]);
+    w.totals[1] = inc_i;   // thread 255's inclusive item prefix = all items
+    w.totals[2] = total_w;
+    w.code_bytes[0] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+  }
+  const uint64_t wdiv = max(1u, total_w);
+  auto group_of = [&](uint32_t excl_w) {
+    return int(min<uint64_t>(kGroups - 1, (uint64_t(kGroups) * excl_w) / wdiv));
+  };
+  uint32_t ei = inc_i - ti, eu = inc_u - tu;
+  uint32_t prev_un = tid > 0 ? s_last_un[tid - 1] : 0u;
+#pragma unroll
+  for (int k = 0; k < kWlPerThread; ++k) {
+    const int p = p0 + k;
+    if (p < nl) {
+      if (b == 0) {
+        w.leaf_item0[leafv[k]] = ei;
+        w.pos_unit0[p] = eu;
+      }
+      if (p >= pb && p < pe) {
+        s_ex_i[p - pb] = ei;
+        s_ex_u[p - pb] = eu;
+      }
+      if (p == pe) s_ex_u[pe - pb] = eu;
+      const int gp = group_of(eu);
+      const int prev = p > 0 ? group_of(eu - prev_un) : -1;
+      for (int gg = prev + 1; gg <= gp; ++gg) {
+        s_gunits[gg] = eu;
+        if (b == 0) w.gunits[gg] = eu;
+      }
+      if (p == nl - 1) {
+        for (int gg = gp + 1; gg <= kGroups; ++gg) {
+          s_gunits[gg] = total_w;
+          if (b == 0) w.gunits[gg] = total_w;
+        }
+        if (b == 0) w.pos_unit0[nl] = total_w;
+        if (pe == nl && pb < nl) s_ex_u[pe - pb] = total_w;
+      }
+    }
+    ei += itv[k];
+    eu += unv[k];
+    prev_un = unv[k];
+  }
+  __syncthreads();
+  for (int p = pb + wid; p < pe; p += 4)
+    ItemsCore(w, p, lane, s_gunits, s_ex_i[p - pb], s_ex_u[p - pb], s_ex_u[p - pb + 1]);
+}
 
 // ---------------------------------------------------------------------------
 // LUT16 scan on MFMA.
@@ -1229,9 +1327,15 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
 }
 
 // Per query: its threshold key (SeedTau).
+// Per query: its threshold key (SeedTau); blocks from nq on build the work
+// list (WorklistFusedBlock).
 template <int K>
-__global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
+__global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a, WorklistArgs w, int nq) {
   const int qi = blockIdx.x;
+  if (qi >= nq) {   // the fused work-list blocks
+    WorklistFusedBlock(w, qi - nq);
+    return;
+  }
   const uint64_t T = SeedTau<K>(a, qi);
   if (threadIdx.x == 0) a.tau_key[qi] = T;
 }
@@ -1239,8 +1343,9 @@ __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a) {
 // Every (query, leaf) pair into the scan's work-item lanes -- slot rank % 32
 // of query tile rank / 32, in every chunk of the leaf -- with the pair's bias
 // and the query's 1/multiplier: the scatter half of InvertCentersToSearch
-// (tree_ah_hybrid_residual.cc:610-622).  One thread per pair; runs beside
-// the seed pass (they share no buffer).
+// (tree_ah_hybrid_residual.cc:610-622), with the slot's sum limit from the
+// query's seed threshold.  One thread per pair; runs after the seed pass and
+// the work list.
 __global__ void __launch_bounds__(256) pair_scatter_kernel(SeedArgs a, int nq) {
   const size_t p = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (p >= size_t(nq) * a.L) return;
@@ -1254,7 +1359,13 @@ __global__ void __launch_bounds__(256) pair_scatter_kernel(SeedArgs a, int nq) {
   v.qid = qi;
   v.bias = a.residual ? a.topl_dist[p] : 0.0f;
   v.inv = a.inv[qi];
-  v.pad = 0;
+  // the slot's sum limit: the largest LUT16 sum whose distance can pass the
+  // query's threshold (d is monotone in the sum), so the scan's setup needs
+  // neither the threshold nor a search
+  const uint64_t tau = a.tau_key[qi];
+  v.amax = tau == kNoThreshold ? 128 * a.nb
+                               : SumLimit(FromOrdered(uint32_t(tau >> 32)), v.inv, v.bias,
+                                          -128 * a.nb, 128 * a.nb);
   const uint32_t w0 = a.leaf_item0[leaf] + (r / kQueriesPerTile) * chunks;
   for (uint32_t ch = 0; ch < chunks; ++ch)
     a.lanes[size_t(w0 + ch) * kQueriesPerTile + (r % kQueriesPerTile)] = v;
@@ -1363,6 +1474,9 @@ constexpr uint32_t kStealMin = 3;  // tiles left for a second wave to join a seg
 #endif
 template <int K>
 constexpr int ScanWaves() { return K <= 26 ? SMX_SCAN_WAVES : 8; }
+#ifndef SMX_SCAN_R
+#define SMX_SCAN_R 3
+#endif
 
 // Diagnostic stamps (ABL & 8; a separate buffer that nothing else reads):
 // per segment {hw_id | worker << 32, xcc_id << 32 | item, realtime, memtime at
@@ -1393,7 +1507,6 @@ struct QParam {
   int32_t amax;
   float bias;
   float inv;
-  uint64_t tau;
 };
 
 // A wave's own LDS: hit list, survivor stage (double buffered: a segment's
@@ -1472,7 +1585,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
   constexpr int W = 4 * NW;
   constexpr int Q = 32, KB = kItemKeys, NWAVES = ScanWaves<K>();
-  constexpr int R = 3;   // one-hot reads in flight ahead of their MFMA
+  constexpr int R = SMX_SCAN_R;   // one-hot reads in flight ahead of their MFMA
   static_assert(K % 2 == 0, "the sparse scan takes two code nibbles per step");
   __shared__ ScanWaveLds wl_[NWAVES];
   __shared__ v4i grp_tab[16];
@@ -1560,7 +1673,8 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
     // the claimed-ahead segment's item and query ids, loaded during the
     // segment before it: the B-fragment addresses need the query id, so
     // without this a segment's setup is two dependent global latencies
-    uint32_t pf_seg = ~0u, pf_item = 0, pf_qid = 0;
+    uint32_t pf_seg = ~0u, pf_item = 0;
+    ItemLane pf_rec = {};
     for (;;) {
       uint32_t sg = __builtin_amdgcn_readfirstlane(sg_next);
       if (sg >= nseg) {
@@ -1591,21 +1705,21 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         st_rt = __builtin_amdgcn_s_memrealtime();
         st_t0 = __builtin_amdgcn_s_memtime();
       }
-      uint32_t item, qid;
+      // the slot's lane record {query, bias, 1/multiplier, sum limit}:
+      // prefetched during the segment before (the claimed-ahead one), so
+      // the B-fragment loads issue at once
+      uint32_t item;
+      ItemLane cl;
       if (sg == pf_seg) {
         item = pf_item;
-        qid = pf_qid;
+        cl = pf_rec;
       } else {
         item = __builtin_amdgcn_readfirstlane(s_item[sg]);
-        qid = a.lanes[size_t(item) * Q + c].qid;
+        cl = a.lanes[size_t(item) * Q + c];
       }
-      // the segment's lane records first (their wait then leaves the B loads
-      // in flight), then the B fragments and the first code tile
+      const uint32_t qid = cl.qid;
       // an empty slot (kNoQuery) loads query 0's rows and never passes (amax)
       const uint32_t lq = qid == kNoQuery ? 0u : qid;
-      const ItemLane cl = a.lanes[size_t(item) * Q + c];
-      const uint64_t tau = a.tau_key[lq];
-      __builtin_amdgcn_sched_barrier(0);
       const SegDesc& sd = s_desc[sg];
       const uint64_t toff = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(sd.tile_off >> 32))) << 32) |
                             __builtin_amdgcn_readfirstlane(uint32_t(sd.tile_off));
@@ -1616,34 +1730,37 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       // this segment's B fragments (LUT rows 2s+h of query c) and first tile
       v8i b[K / 2];
       uint32_t codes[NW] = {};
-      const uint8_t* tb = a.tiles + toff * 64ull * W + size_t(lane) * W;
+      // addresses as a wave-uniform base + a 32-bit lane offset (saddr
+      // loads: no 64-bit per-lane pointers live across the tile loop)
+      const uint8_t* tseg = a.tiles + toff * 64ull * W;
+      auto tile_ptr = [&](uint32_t t) {
+        return tseg + size_t(t * uint32_t(64 * W) + uint32_t(lane) * uint32_t(W));
+      };
       // LUT rows 4s + 2h, 4s + 2h + 1 of query c (32 bytes) per sparse step
-      const v8i* bsrc = reinterpret_cast<const v8i*>(a.lut) + size_t(lq) * K + h;
+      const uint32_t boff = (lq * uint32_t(K) + uint32_t(h)) * 32u;
+      const uint8_t* lutb = reinterpret_cast<const uint8_t*>(a.lut);
       auto load_b = [&]() {
 #pragma unroll
-        for (int s2 = 0; s2 < K / 2; ++s2) b[s2] = bsrc[2 * s2];
+        for (int s2 = 0; s2 < K / 2; ++s2)
+          b[s2] = *reinterpret_cast<const v8i*>(lutb + size_t(boff + uint32_t(s2) * 64u));
       };
       load_b();
-      LoadCodes<K>(tb + size_t(j) * 64 * W, codes);
+      LoadCodes<K>(tile_ptr(j), codes);
       // the claimed-ahead segment's item and query ids, for its setup
       {
         const uint32_t sn = __builtin_amdgcn_readfirstlane(sg_next);
         if (sn < nseg) {
           pf_seg = sn;
           pf_item = __builtin_amdgcn_readfirstlane(s_item[sn]);
-          pf_qid = a.lanes[size_t(pf_item) * Q + c].qid;
+          pf_rec = a.lanes[size_t(pf_item) * Q + c];
         } else {
           pf_seg = ~0u;
         }
       }
 
-      // the slot's sum limit: the largest LUT16 sum whose distance can pass
-      // the query's threshold (d is monotone in the sum)
-      int amax = kNoSum;
-      if (qid != kNoQuery)
-        amax = tau == kNoThreshold ? 128 * a.nb
-                                   : SumLimit(FromOrdered(uint32_t(tau >> 32)), cl.inv, cl.bias,
-                                              -128 * a.nb, 128 * a.nb);
+      // the slot's sum limit (written with the record by the pair scatter:
+      // the largest LUT16 sum whose distance can pass the query's threshold)
+      const int amax = cl.amax;
       if (flush) flush_prev();
       if (lane < Q) {
         QParam v;
@@ -1651,7 +1768,6 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         v.amax = amax;
         v.bias = cl.bias;
         v.inv = cl.inv;
-        v.tau = tau;
         wl.qp[lane] = v;
         wl.qcnt[lane] = 0;
       }
@@ -1659,8 +1775,10 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       WaveLdsSync();
       uint32_t whits = 0;   // wave-uniform
 
-      // lane k of the wave takes hits k, k+64: per-element test, key, exact
-      // threshold compare, append to the query's LDS stage
+      // lane k of the wave takes hits k, k+64: per-element test, key, append
+      // to the query's LDS stage.  sum <= amax implies key <= the threshold
+      // key: the scan's thresholds are the seed's (ordered(d_k') << 32 |
+      // 0xFFFFFFFF) or none, and d is monotone in the sum
       auto drain = [&]() {
         for (uint32_t hidx = uint32_t(lane); hidx < whits; hidx += 64) {
           const uint32_t meta = wl.hmeta[hidx];
@@ -1671,7 +1789,6 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
           const QParam pq = wl.qp[cc];
           const int am = pq.amax;
           const float iv = pq.inv, bs = pq.bias;
-          const uint64_t TT = pq.tau;
           const uint32_t qq = pq.qid;
 #pragma unroll 1
           for (int i = 0; i < 16; ++i) {
@@ -1682,16 +1799,14 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
               const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp)
                                                : a.members[moff + dp];
               const uint64_t key = (uint64_t(OrderedBits(d)) << 32) | tie;
-              if (key <= TT) {
-                const uint32_t p = atomicAdd(&wl.s_kn[par], 1u);
-                if (p < uint32_t(KB)) {
-                  wl.kbuf[par][p] = key;
-                  wl.kslot[par][p] = uint8_t(cc);
-                  atomicAdd(&wl.qcnt[cc], 1u);
-                } else {  // stage full (rare): straight to the global list
-                  const uint32_t gs = atomicAdd(&a.cand_count[size_t(qq) * kCounterStride], 1u);
-                  if (gs < a.cap) a.cand[size_t(qq) * a.cap + gs] = key;
-                }
+              const uint32_t p = atomicAdd(&wl.s_kn[par], 1u);
+              if (p < uint32_t(KB)) {
+                wl.kbuf[par][p] = key;
+                wl.kslot[par][p] = uint8_t(cc);
+                atomicAdd(&wl.qcnt[cc], 1u);
+              } else {  // stage full (rare): straight to the global list
+                const uint32_t gs = atomicAdd(&a.cand_count[size_t(qq) * kCounterStride], 1u);
+                if (gs < a.cap) a.cand[size_t(qq) * a.cap + gs] = key;
               }
             }
           }
@@ -1794,7 +1909,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
           // unconditional (the current tile again when none follows): one
           // load per tile on every path, so the wait for this tile's codes
           // leaves the next tile's load in flight (vmcnt(1), not vmcnt(0))
-          LoadCodes<K>(tb + size_t(more ? tn : t) * 64 * W, cb);
+          LoadCodes<K>(tile_ptr(more ? tn : t), cb);
           tile(codes, t);
           ++tiles_done;
           if (pending) copy_prev();   // after the segment's first tile: the atomic has returned
@@ -1803,7 +1918,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
           advance(t, tn);
           t = tn;
           more = next_tile(t, tn);
-          LoadCodes<K>(tb + size_t(more ? tn : t) * 64 * W, codes);
+          LoadCodes<K>(tile_ptr(more ? tn : t), codes);
           tile(cb, t);
           ++tiles_done;
           if (!more) break;
@@ -2729,6 +2844,31 @@ hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq, i
   return hipGetLastError();
 }
 
+WorklistArgs MakeWorklistArgs(const DeviceIndex& ix, const uint32_t* leaf_count, WorkItem* work,
+                              uint32_t* leaf_item0, uint32_t* pos_unit0, uint32_t* gunits,
+                              ItemLane* lanes, uint4* wave_start, int grid, uint32_t* totals,
+                              unsigned long long* code_bytes, uint32_t chunk_tiles) {
+  WorklistArgs w;
+  w.cnt = leaf_count;
+  w.order = ix.leaf_order;
+  w.leaf_size = ix.leaf_size;
+  w.tile_off = ix.tile_off;
+  w.member_off = ix.member_off;
+  w.nl = ix.nl;
+  w.nb = ix.nb;
+  w.chunk_tiles = chunk_tiles;
+  w.grid = grid;
+  w.leaf_item0 = leaf_item0;
+  w.pos_unit0 = pos_unit0;
+  w.gunits = gunits;
+  w.totals = totals;
+  w.code_bytes = code_bytes;
+  w.work = work;
+  w.lanes = lanes;
+  w.wave_start = wave_start;
+  return w;
+}
+
 hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, WorkItem* work,
                           uint32_t* leaf_item0, uint32_t* pos_unit0, uint32_t* gunits,
                           ItemLane* lanes, uint4* wave_start, int grid, uint32_t* totals,
@@ -2742,9 +2882,9 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
   hipLaunchKernelGGL(worklist_kernel, dim3(nblk), dim3(256), 0, s, leaf_count, ix.leaf_order,
                      ix.leaf_size, ix.nl, ix.nb, chunk_tiles, wp, leaf_item0, pos_unit0, gunits,
                      totals, code_bytes);
-  hipLaunchKernelGGL(items_kernel, dim3(ix.nl), dim3(64), 0, s, leaf_count, ix.leaf_order,
-                     ix.leaf_size, ix.tile_off, ix.member_off, chunk_tiles, grid, leaf_item0,
-                     pos_unit0, gunits, work, lanes, wave_start);
+  const WorklistArgs w = MakeWorklistArgs(ix, leaf_count, work, leaf_item0, pos_unit0, gunits,
+                                          lanes, wave_start, grid, totals, code_bytes, chunk_tiles);
+  hipLaunchKernelGGL(items_kernel, dim3(ix.nl), dim3(64), 0, s, w);
   return hipGetLastError();
 }
 
@@ -2836,11 +2976,15 @@ hipError_t LaunchLeafScores(const DeviceIndex& ix, int leaf, const int8_t* lut, 
 
 #define SMX_SEED_CASE(KV)                                                        \
   case KV:                                                                       \
-    hipLaunchKernelGGL(seed_tau_kernel<KV>, dim3(nq), dim3(256), 0, s, a);       \
+    hipLaunchKernelGGL(seed_tau_kernel<KV>, dim3(nq + nwl), dim3(256), 0, s, a,            \
+                       wl ? *wl : WorklistArgs{}, nq);                                      \
     break;
 
-hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s) {
-  if (nq == 0) return hipSuccess;   // (seed <= 0 still scatters the pairs)
+hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s,
+                      const WorklistArgs* wl) {
+  if (wl && wl->nl > kFusedWorklistLeaves) return hipErrorInvalidValue;
+  const int nwl = wl ? (wl->nl + kWlPosPerBlock - 1) / kWlPosPerBlock : 0;
+  if (nq + nwl == 0) return hipSuccess;
   switch (ix.ksteps) {
     SMX_SEED_CASE(4)
     SMX_SEED_CASE(8)

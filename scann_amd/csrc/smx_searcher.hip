@@ -136,6 +136,7 @@ struct smx_index {
   uint32_t cap_per_query = 0;      // candidate list capacity; 0 = sized per call (AutoCap)
   int seed_leaves = 4;
   int scan_variant = 0;            // see smx::LaunchScan
+  int fused_worklist_leaves = smx::kFusedWorklistLeaves;   // 0: always the side stream
   uint32_t chunk_tiles = 16;       // tiles per work item (tools/tune.py: 16-20 best at glove)
   int grid = 0;                    // scan grid: resident one-wave workgroups (occupancy API)
   bool profiling = false;
@@ -552,23 +553,39 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     f.one_to_many = single ? 1 : 0;
     SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s, &f));
     Mark(h, 1, s);
-    // Fork.  Side stream: the work list and the pairs' lane records; this
-    // stream: the seed thresholds.  Write sets ("Two streams"):
-    // side = leaf_item0, pos_unit0, gunits, work, lanes, wave_start,
-    // stats[3..7]; seed = tau.  Both only read the front end's outputs,
-    // written before the fork; the per-call state reset happens in the
-    // partition kernel, before the fork as well.
-    SMX_HIP(hipEventRecord(h->fork_ev, s));
-    SMX_HIP(hipStreamWaitEvent(h->side, h->fork_ev, 0));
-    SMX_HIP(smx::LaunchWorklist(ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes,
-                                w.wave_start, h->grid, stats + 3, code_bytes, h->chunk_tiles,
-                                w.wl_part, h->side));
-    SMX_HIP(smx::LaunchPairScatter(ix, sa, nq, h->side));
-    Mark(h, 3, h->side);
-    SMX_HIP(hipEventRecord(h->join_ev, h->side));
-    SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
-    Mark(h, 4, s);
-    SMX_HIP(hipStreamWaitEvent(s, h->join_ev, 0));   // join
+    if (ix.nl <= h->fused_worklist_leaves) {
+      // the work list is built by extra blocks of the seed launch (one
+      // stream: a fork/join costs 5-10 us per cross-queue edge)
+      const smx::WorklistArgs wla = smx::MakeWorklistArgs(
+          ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes, w.wave_start, h->grid,
+          stats + 3, code_bytes, h->chunk_tiles);
+      Mark(h, 3, s);
+      SMX_HIP(smx::LaunchSeed(ix, sa, nq, s, &wla));
+      Mark(h, 4, s);
+    } else {
+      // Fork.  Side stream: the work list (and the empty slots' records);
+      // this stream: the seed thresholds.  Write sets ("Two
+      // streams"): side = leaf_item0, pos_unit0, gunits, work, lanes (empty
+      // slots), wave_start, stats[3..7]; seed = tau.  Both only read the
+      // front end's outputs, written before the fork; the per-call state
+      // reset happens in the partition kernel, before the fork as well.
+      // The seed (the longer branch) is captured first, so that a replayed
+      // graph keeps it on the launch queue with the kernels before and after
+      // it; the shorter work-list branch pays the cross-queue edges.
+      SMX_HIP(hipEventRecord(h->fork_ev, s));
+      SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
+      Mark(h, 4, s);
+      SMX_HIP(hipStreamWaitEvent(h->side, h->fork_ev, 0));
+      SMX_HIP(smx::LaunchWorklist(ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes,
+                                  w.wave_start, h->grid, stats + 3, code_bytes, h->chunk_tiles,
+                                  w.wl_part, h->side));
+      Mark(h, 3, h->side);
+      SMX_HIP(hipEventRecord(h->join_ev, h->side));
+      SMX_HIP(hipStreamWaitEvent(s, h->join_ev, 0));   // join
+    }
+    // every pair's lane record with its sum limit (needs the work list and
+    // the seed thresholds)
+    SMX_HIP(smx::LaunchPairScatter(ix, sa, nq, s));
     Mark(h, 5, s);
     SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s));
     Mark(h, 6, s);
@@ -776,6 +793,7 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
     smx_index_destroy(h);
     return Fail(SMX_OUT_OF_MEMORY, "hipHostMalloc failed");
   }
+  if (const char* fw = std::getenv("SMX_FUSED_WORKLIST")) h->fused_worklist_leaves = std::atoi(fw);
   const char* ng = std::getenv("SMX_NO_GRAPH");
   h->use_graph = !(ng && ng[0] == '1');
 

@@ -17,14 +17,23 @@ tree-AH LUT16 path:
   2-D check, the (0, NaN) padding and the x(-1) of dot-product distances
   (scann.h:162-180, scann.cc:364-369).  Errors surface as RuntimeError with
   the reference's "Error during search: " prefix (scann_npy.cc:41-55).
+  The search calls run in C++ (``ScannNumpyCore``, scann_amd/csrc/
+  smx_pybind.cc, a pybind11 module over the C ABI).
 """
 from __future__ import annotations
+
+import ctypes
 
 import numpy as np
 
 from . import _native, assets
 from .config import SearchConfig, search_config_from_text
 from .index import METRIC_NAMES, TreeAHIndex
+
+
+def _arg(v) -> int:
+    """None means "config default", as -1 does (scann.cc:384-430)."""
+    return -1 if v is None else int(v)
 
 
 class ScannNumpy:
@@ -51,9 +60,17 @@ class ScannNumpy:
                 seed=seed, noise_shaping_threshold=cfg.noise_shaping_threshold)
         self._config_text = config
         self._index = index
-        self._native = _native.NativeIndex(index, device=device)
-        # ScannInterface::Initialize: dot-family distances are negated on output
-        self._result_multiplier = -1.0 if self._cfg.metric == "dot_product" else 1.0
+        self._device = device
+        self._native = None
+        # the search surface in C++ (scann_amd/csrc/smx_pybind.cc): parameter
+        # resolution, GIL release, result arrays, x(-1) of dot-product
+        # distances (ScannInterface::Initialize) and the error mapping
+        cfg = self._cfg
+        desc = index.desc()
+        self._core = _native.load_pybind().ScannNumpyCore(
+            ctypes.addressof(desc), device, cfg.num_neighbors,
+            cfg.reorder_num_neighbors if cfg.has_reordering else cfg.num_neighbors,
+            cfg.leaves_to_search, cfg.has_reordering, cfg.metric == "dot_product")
 
     # -- parameter resolution (ScannInterface::GetSearchParameters[Batched]) --
     def _resolve(self, final_nn: int, pre_reorder_nn: int, leaves: int):
@@ -67,38 +84,18 @@ class ScannNumpy:
         leaves = cfg.leaves_to_search if leaves is None or leaves <= 0 else int(leaves)
         return final_nn, pre, leaves
 
-    def _run(self, queries: np.ndarray, final_nn, pre_reorder_nn, leaves):
-        final_nn, pre, leaves = self._resolve(final_nn, pre_reorder_nn, leaves)
-        try:
-            idx, dist, _ = self._native.search_batched(queries, leaves, pre, final_nn,
-                                                       self._cfg.has_reordering)
-        except _native.SmxError as e:
-            raise RuntimeError(f"Error during search: {e}") from None
-        return idx, dist * np.float32(self._result_multiplier)
-
     def search(self, query, final_nn=-1, pre_reorder_nn=-1, leaves=-1):
         """ScannNumpy::Search: one query through the single-query path's
         numerics (one-to-many partition scores, smx_search)."""
-        q = np.ascontiguousarray(query, dtype=np.float32)
-        if q.ndim != 1:
-            raise ValueError("Query must be one-dimensional")
-        final_nn, pre, leaves = self._resolve(final_nn, pre_reorder_nn, leaves)
-        try:
-            idx, dist, n = self._native.search(q, leaves, pre, final_nn, self._cfg.has_reordering)
-        except _native.SmxError as e:
-            raise RuntimeError(f"Error during search: {e}") from None
-        return idx[:n], dist[:n] * np.float32(self._result_multiplier)
+        return self._core.search(query, _arg(final_nn), _arg(pre_reorder_nn), _arg(leaves))
 
     def search_batched(self, queries, final_nn=-1, pre_reorder_nn=-1, leaves=-1,
-                       parallel=False, batch_size=0):
-        q = np.ascontiguousarray(queries, dtype=np.float32)
-        if q.ndim != 2:
-            raise ValueError("Queries must be in two-dimensional array")
+                       parallel=False, batch_size=256):
         # parallel mode (SearchBatchedParallel) exists to spread a batch over
         # CPU threads; the GPU batch is already parallel, so both modes run
         # the same device pipeline (results identical by construction).
-        del parallel, batch_size
-        return self._run(q, final_nn, pre_reorder_nn, leaves)
+        return self._core.search_batched(queries, _arg(final_nn), _arg(pre_reorder_nn),
+                                         _arg(leaves), bool(parallel), int(batch_size or 0))
 
     def serialize(self, path: str, relative_path: bool = False) -> None:
         try:
@@ -116,6 +113,10 @@ class ScannNumpy:
         del num_threads  # host threads do not drive the GPU pipeline
 
     def native(self) -> _native.NativeIndex:
+        """A ctypes handle on its own device copy of the index (stage entry
+        points, tuning); created on first use."""
+        if self._native is None:
+            self._native = _native.NativeIndex(self._index, device=self._device)
         return self._native
 
     @property

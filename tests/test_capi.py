@@ -111,3 +111,18 @@ def test_struct_layout_matches_header(tmp_path):
         for fname, _ in py._fields_:
             assert int(got[f"{cname}.{fname}"]) == getattr(py, fname).offset, (cname, fname)
     assert int(got["smx_shard_entry"]) == 16
+
+
+def test_pybind_module_surface():
+    """The C++ pybind11 module (scann_amd/csrc/smx_pybind.cc) loads and has the
+    reference's ScannNumpy search surface (scann_pybind.cc:24-54); no GPU
+    call is made here."""
+    from scann_amd import _native
+    mod = _native.load_pybind()
+    core = mod.ScannNumpyCore
+    for name in ("search", "search_batched", "size", "dim"):
+        assert callable(getattr(core, name))
+    doc = core.search_batched.__doc__
+    assert "queries" in doc and "parallel" in doc and "batch_size" in doc
+    with pytest.raises(ValueError, match="null index description"):
+        core(0, 0, 10, 100, 100, True, True)

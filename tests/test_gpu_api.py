@@ -110,3 +110,20 @@ def test_soar_serialization_in_reference_layout(data, tmp_path):
     np.testing.assert_array_equal(a[0], b[0])
     np.testing.assert_array_equal(a[1], b[1])
     assert "INT8_LUT16" in s2.config()
+
+
+def test_cpp_core_defaults_and_errors(searcher, data):
+    """ScannNumpyCore (C++, scann_amd/csrc/smx_pybind.cc) resolves -1 to the
+    config defaults as ScannInterface::GetSearchParametersBatched does
+    (scann.cc:406-430) and maps a failed search to RuntimeError with the
+    reference's prefix (scann_npy.cc:41-47)."""
+    _, q = data
+    core = searcher.searcher._core
+    a = core.search_batched(q[:16])
+    b = core.search_batched(q[:16], 10, 100, 20)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    with pytest.raises(ValueError, match="two-dimensional"):
+        core.search_batched(q[0])
+    with pytest.raises(RuntimeError, match="Error during search: "):
+        core.search_batched(q[:4, :10])   # wrong dimensionality
