@@ -147,7 +147,7 @@ struct smx_index {
   uint32_t* host_stats = nullptr;  // pinned copy of the stats words
   smx_timings timings{};
   hipEvent_t ev[16] = {};
-  hipEvent_t done_ev = nullptr;      // the last call's end (cross-stream ordering)
+  hipEvent_t done_ev = nullptr;      // cross-stream ordering (recorded at a stream switch)
   hipStream_t side = nullptr;        // the fork/join branch of every call
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   hipStream_t last_stream = nullptr;
@@ -595,7 +595,11 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   };
   // The workspace is shared by every stream: a call on another stream than
   // the last one waits for that one's work (stream-ordered, no host sync).
+  // The event is recorded on the last stream only at such a switch (it then
+  // covers all of that stream's calls so far): a record per call put a
+  // barrier packet between consecutive graph replays (~4 us per call).
   if (h->last_stream != s) {
+    SMX_HIP(hipEventRecord(h->done_ev, h->last_stream));
     SMX_HIP(hipStreamWaitEvent(s, h->done_ev, 0));
     h->last_stream = s;
   }
@@ -633,7 +637,6 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     }
   }
   if (!ran && (rc = first_pass())) return rc;
-  SMX_HIP(hipEventRecord(h->done_ev, s));
   // No host round trip: overflow and the select's fallback queries are
   // handled on the device, so the call returns with the work enqueued
   // (search_batched_device is stream-ordered; the host-buffer entry points
@@ -793,7 +796,8 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
     smx_index_destroy(h);
     return Fail(SMX_OUT_OF_MEMORY, "hipHostMalloc failed");
   }
-  if (const char* fw = std::getenv("SMX_FUSED_WORKLIST")) h->fused_worklist_leaves = std::atoi(fw);
+  if (const char* fw = std::getenv("SMX_FUSED_WORKLIST"))
+    h->fused_worklist_leaves = std::min(std::atoi(fw), smx::kFusedWorklistLeaves);
   const char* ng = std::getenv("SMX_NO_GRAPH");
   h->use_graph = !(ng && ng[0] == '1');
 
