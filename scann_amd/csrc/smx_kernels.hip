@@ -1459,7 +1459,8 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
 // over the hits, and stages the segment's survivors in LDS: one global atomic
 // per query per segment reserves their list slots (issued at the segment's
 // end, its result consumed after the next segment's first tile).
-// ABL = 4: timing ablation without the epilogue (results invalid).
+// ABL = 4: timing ablation without the epilogue; ABL = 2: with the hit test
+// but no hit list (results invalid for both).
 // ---------------------------------------------------------------------------
 
 constexpr int kHitsPerWave = 64;   // a tile adds at most one hit per lane
@@ -1775,42 +1776,57 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       WaveLdsSync();
       uint32_t whits = 0;   // wave-uniform
 
-      // lane k of the wave takes hits k, k+64: per-element test, key, append
-      // to the query's LDS stage.  sum <= amax implies key <= the threshold
-      // key: the scan's thresholds are the seed's (ordered(d_k') << 32 |
-      // 0xFFFFFFFF) or none, and d is monotone in the sum
+      // the hit list's elements (16 sums per hit) spread over the lanes,
+      // element e = 16 * hit + i on lane e % 64: per-element test, key, and
+      // a ballot-ranked append to the LDS stage (no returning atomic; the 16
+      // lanes of one hit read its meta and parameters as broadcasts).
+      // sum <= amax implies key <= the threshold key: the scan's thresholds
+      // are the seed's (ordered(d_k') << 32 | 0xFFFFFFFF) or none, and d is
+      // monotone in the sum
       auto drain = [&]() {
-        for (uint32_t hidx = uint32_t(lane); hidx < whits; hidx += 64) {
-          const uint32_t meta = wl.hmeta[hidx];
-          const uint32_t jj = meta >> 6;
-          const int cc = int(meta & 31u), hh = int((meta >> 5) & 1u);
-          const uint4 s0 = wl.hsum[hidx][0], s1 = wl.hsum[hidx][1];
-          const uint32_t sw8[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-          const QParam pq = wl.qp[cc];
-          const int am = pq.amax;
-          const float iv = pq.inv, bs = pq.bias;
-          const uint32_t qq = pq.qid;
-#pragma unroll 1
-          for (int i = 0; i < 16; ++i) {
-            const int sum = int(int16_t(uint16_t(sw8[i >> 1] >> (16 * (i & 1)))));
-            if (sum <= am) {
-              const uint32_t dp = jj * kDpPerTile + (i & 3) + 8 * (i >> 2) + 4 * hh;
-              const float d = DistOf(sum, iv, bs);
+        const uint32_t total = whits * 16u;
+        uint32_t kn = __builtin_amdgcn_readfirstlane(wl.s_kn[par]);
+        for (uint32_t e0 = 0; e0 < total; e0 += 64) {
+          const uint32_t e = e0 + uint32_t(lane);
+          bool pass = false;
+          uint64_t key = 0;
+          int cc = 0;
+          if (e < total) {
+            const uint32_t hidx = e >> 4, i = e & 15u;
+            const uint32_t meta = wl.hmeta[hidx];
+            cc = int(meta & 31u);
+            const uint32_t hh = (meta >> 5) & 1u, jj = meta >> 6;
+            const uint32_t word = reinterpret_cast<const uint32_t*>(&wl.hsum[hidx][0])[i >> 1];
+            const int sum = int(int16_t(uint16_t(word >> (16u * (i & 1u)))));
+            const QParam pq = wl.qp[cc];
+            if (sum <= pq.amax) {
+              pass = true;
+              const uint32_t dp = jj * kDpPerTile + (i & 3u) + 8u * (i >> 2) + 4u * hh;
+              const float d = DistOf(sum, pq.inv, pq.bias);
               const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp)
                                                : a.members[moff + dp];
-              const uint64_t key = (uint64_t(OrderedBits(d)) << 32) | tie;
-              const uint32_t p = atomicAdd(&wl.s_kn[par], 1u);
+              key = (uint64_t(OrderedBits(d)) << 32) | tie;
+            }
+          }
+          const uint64_t bm = __builtin_amdgcn_ballot_w64(pass);
+          if (bm) {
+            if (pass) {
+              const uint32_t p = kn + __builtin_amdgcn_mbcnt_hi(
+                                          uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u));
               if (p < uint32_t(KB)) {
                 wl.kbuf[par][p] = key;
                 wl.kslot[par][p] = uint8_t(cc);
                 atomicAdd(&wl.qcnt[cc], 1u);
               } else {  // stage full (rare): straight to the global list
+                const uint32_t qq = wl.qp[cc].qid;
                 const uint32_t gs = atomicAdd(&a.cand_count[size_t(qq) * kCounterStride], 1u);
                 if (gs < a.cap) a.cand[size_t(qq) * a.cap + gs] = key;
               }
             }
+            kn += uint32_t(__popcll(bm));
           }
         }
+        if (lane == 0) wl.s_kn[par] = kn;
         WaveLdsSync();   // the hit list is rewritten next
       };
 
@@ -1839,6 +1855,10 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         m = min(m, acc[15]);
         const bool hit = m <= amax;
         const uint64_t hb = __builtin_amdgcn_ballot_w64(hit);
+        if (ABL & 2) {   // timing ablation: the hit test without its list
+          if (hb == 0x1234567ull) a.cand_count[0] = 1u;
+          return;
+        }
         if (hb) {
           // whits <= 64 here and a tile adds at most 64: the list (128)
           // always has room, so the sums are dead before any drain
@@ -1857,7 +1877,9 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
           }
           whits += nh;
           if (ABL & 8) st_hits += nh;
-          WaveLdsSync();
+          // no wait for the writes: a wave's LDS instructions execute in
+          // order, so the drain's later reads see them (compiler barrier only)
+          asm volatile("" ::: "memory");
         }
       };
       // a hit list over half full is drained between tiles with the B
@@ -2890,7 +2912,10 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
 
 #define SMX_SCAN_CASE(KV)                                                                  \
   case KV:                                                                                 \
-    if (variant == 4)                                                                      \
+    if (variant == 2)                                                                      \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 2>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
+                         0, s, a);                                                         \
+    else if (variant == 4)                                                                 \
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 4>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
                          0, s, a);                                                         \
     else if (variant == 8)                                                                 \
