@@ -1460,7 +1460,8 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
 // per query per segment reserves their list slots (issued at the segment's
 // end, its result consumed after the next segment's first tile).
 // ABL = 4: timing ablation without the epilogue; ABL = 2: with the hit test
-// but no hit list (results invalid for both).
+// but no hit list; ABL = 16: with hit lists and drains but no copy to the
+// candidate lists (results invalid for all three).
 // ---------------------------------------------------------------------------
 
 constexpr int kHitsPerWave = 64;   // a tile adds at most one hit per lane
@@ -1626,6 +1627,10 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   // place = its query's reserved first slot (the returned value of the
   // segment-end atomic, waited for only here) + a running count
   auto copy_prev = [&]() {
+    if (ABL & 16) {
+      pending = false;
+      return;
+    }
     const uint32_t pp = par ^ 1u;
     if (lane < Q) {
       wl.q_slot[lane] = slot;
@@ -1646,7 +1651,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   // those loads would otherwise wait for these atomics too), consumed by
   // copy_prev after that segment's first tile
   auto flush_prev = [&]() {
-    if (lane < Q) {
+    if ((ABL & 16) == 0 && lane < Q) {   // (16: timing ablation without the lists)
       const uint32_t m = wl.qcnt[lane];
       slot = m ? atomicAdd(&a.cand_count[size_t(fqid) * kCounterStride], m) : 0u;
       wl.prev_qid[lane] = fqid;
@@ -1741,9 +1746,10 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       const uint32_t boff = (lq * uint32_t(K) + uint32_t(h)) * 32u;
       const uint8_t* lutb = reinterpret_cast<const uint8_t*>(a.lut);
       auto load_b = [&]() {
+        // one per-lane address, the steps as immediate offsets
+        const v8i* bp = reinterpret_cast<const v8i*>(lutb + size_t(boff));
 #pragma unroll
-        for (int s2 = 0; s2 < K / 2; ++s2)
-          b[s2] = *reinterpret_cast<const v8i*>(lutb + size_t(boff + uint32_t(s2) * 64u));
+        for (int s2 = 0; s2 < K / 2; ++s2) b[s2] = bp[2 * s2];
       };
       load_b();
       LoadCodes<K>(tile_ptr(j), codes);
@@ -2912,7 +2918,10 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
 
 #define SMX_SCAN_CASE(KV)                                                                  \
   case KV:                                                                                 \
-    if (variant == 2)                                                                      \
+    if (variant == 16)                                                                     \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 16>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
+                         0, s, a);                                                         \
+    else if (variant == 2)                                                                 \
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 2>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
                          0, s, a);                                                         \
     else if (variant == 4)                                                                 \

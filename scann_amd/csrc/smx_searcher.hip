@@ -1133,9 +1133,10 @@ int smx_get_timings(const smx_index* h, smx_timings* out) {
 int smx_set_tuning(smx_index* h, int32_t candidates_per_query, int32_t seed_leaves,
                    int32_t scan_variant, int32_t chunk_tiles) {
   if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
-  if (scan_variant != 0 && scan_variant != 2 && scan_variant != 4 && scan_variant != 8)
+  if (scan_variant != 0 && scan_variant != 2 && scan_variant != 4 && scan_variant != 8 &&
+      scan_variant != 16)
     return Fail(SMX_INVALID_ARGUMENT,
-                "scan_variant is 0 (scan), 2 / 4 (timing ablations) or 8 (diagnostic stamps)");
+                "scan_variant is 0 (scan), 2 / 4 / 16 (timing ablations) or 8 (diagnostic stamps)");
   if (chunk_tiles != 0 && (chunk_tiles < 8 || chunk_tiles > 65535))
     return Fail(SMX_INVALID_ARGUMENT, "chunk_tiles must be 0 (default) or in [8, 65535]");
   if (candidates_per_query != 0 && (candidates_per_query < 32 || candidates_per_query > 8192))
