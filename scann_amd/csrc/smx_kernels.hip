@@ -1406,7 +1406,17 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
       o[p] = grp_tab[grp(p)];
       ix[p] = pos_tab[pos(p)];
     }
-  v16i acc = v16i{0};
+  // zeroed as 8 x v_mov_b64 (the plain v16i{0} became 16 v_mov_b32 plus a
+  // chain of 8 register-shifting v_mov_b64 copies per tile)
+  typedef long long v8l __attribute__((ext_vector_type(8)));
+  v8l z;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    long long t;
+    asm volatile("v_mov_b64 %0, 0" : "=v"(t));
+    z[k] = t;
+  }
+  v16i acc = __builtin_bit_cast(v16i, z);
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     acc = __builtin_amdgcn_smfmac_i32_32x32x64_i8(o[s % R], b[s], acc, ix[s % R], 0, 0);

@@ -137,7 +137,7 @@ struct smx_index {
   int seed_leaves = 4;
   int scan_variant = 0;            // see smx::LaunchScan
   int fused_worklist_leaves = smx::kFusedWorklistLeaves;   // 0: always the side stream
-  uint32_t chunk_tiles = 16;       // tiles per work item (tools/tune.py: 16-20 best at glove)
+  uint32_t chunk_tiles = 20;       // tiles per work item (tools/tune.py: 16-20 best at glove)
   int grid = 0;                    // scan grid: resident one-wave workgroups (occupancy API)
   bool profiling = false;
   bool use_graph = true;           // replay the first pass as a hipGraph
