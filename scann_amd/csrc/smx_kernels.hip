@@ -1600,7 +1600,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   constexpr int R = SMX_SCAN_R;   // one-hot reads in flight ahead of their MFMA
   static_assert(K % 2 == 0, "the sparse scan takes two code nibbles per step");
   __shared__ ScanWaveLds wl_[NWAVES];
-  __shared__ v4i grp_tab[16];
+  __shared__ __align__(256) v4i grp_tab[16];   // 256-aligned: base | (x & 0xF0)
   __shared__ int pos_tab[16];
   __shared__ uint32_t s_item[kMaxSegs], s_end[kMaxSegs], s_next[kMaxSegs];
   __shared__ SegDesc s_desc[kMaxSegs];
