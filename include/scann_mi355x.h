@@ -235,14 +235,30 @@ int smx_exact_distances(smx_index* index, const float* queries, int32_t nq,
 int smx_lut16_leaf_scores(smx_index* index, int32_t leaf, const uint8_t* lut,
                           int32_t* out_scores);
 
+/* ---- index build (device buffers, enqueued on `stream`) ----------------- */
+
+/* Nearest center of every row: out[i] = argmin_j ||x_i - c_j||^2 (ties to the
+ * lowest j) — the assignment step of k-means training, GmmUtils::KMeansImpl
+ * (scann/utils/gmm_utils.cc:539-1318).  With `primary` (one center per row,
+ * device int32) the SOAR secondary assignment instead
+ * (kmeans_tree_partitioner.cc:926-997): argmin over j != primary_i of
+ * ||x_i - c_j||^2 + lambda <r_i, x_i - c_j>^2 / ||r_i||^2, r_i = x_i -
+ * c_primary_i.  x: [n][d], centers: [k][d] float32; out: [n] int32;
+ * out_loss: [n] float32 (the winning loss; the k-means form omits ||x_i||^2)
+ * or NULL. */
+int smx_nearest_centers(const float* d_x, int64_t n, int32_t d, const float* d_centers,
+                        int32_t k, const int32_t* d_primary, float lambda, int32_t* d_out,
+                        float* d_out_loss, void* stream);
+
 /* ---- diagnostics ---------------------------------------------------------- */
 int smx_set_profiling(smx_index* index, int32_t enabled);
 int smx_get_timings(const smx_index* index, smx_timings* out);
 /* Tuning knobs: candidate buffer capacity per query (0, the default: sized
  * per call from k', leaves_to_search and the seed leaves), seed leaves used for the
- * per-query threshold, scan kernel variant (0 = the scan, 4 = the scan
- * without its threshold epilogue: a timing ablation whose results are
- * invalid) and tiles per work item (0 keeps the default, 32). */
+ * per-query threshold, scan kernel variant (0 = the scan; 2, 4, 16 = timing
+ * ablations whose results are invalid: without the hit list, without the
+ * epilogue, without the copy to the candidate lists; 8 = diagnostic stamps)
+ * and tiles per work item (0 keeps the default, 20; at least 8). */
 int smx_set_tuning(smx_index* index, int32_t candidates_per_query, int32_t seed_leaves,
                    int32_t scan_variant, int32_t chunk_tiles);
 

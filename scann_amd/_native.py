@@ -63,6 +63,8 @@ SIGNATURES = {
     "smx_shard_width": (ctypes.c_int, [_vp, ctypes.POINTER(SearchParams), ctypes.POINTER(_i32)]),
     "smx_search_shard_device": (ctypes.c_int, [_vp, _vp, _i32, _i32, ctypes.POINTER(SearchParams), _vp, _vp]),
     "smx_merge_shards_device": (ctypes.c_int, [_vp, _i32, _i32, ctypes.POINTER(SearchParams), _vp, _vp, _vp, _vp, _vp]),
+    "smx_nearest_centers": (ctypes.c_int, [_vp, ctypes.c_int64, _i32, _vp, _i32, _vp,
+                                           ctypes.c_float, _vp, _vp, _vp]),
     "smx_last_error": (ctypes.c_char_p, []),
     "smx_version": (ctypes.c_char_p, []),
 }
@@ -136,6 +138,14 @@ def _current_stream(stream):
     if torch is not None and torch.cuda.is_available() and torch.cuda.is_initialized():
         return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     return None
+
+
+def nearest_centers_device(x_ptr, n, d, c_ptr, k, out_ptr, primary_ptr=None, lam=0.0,
+                           loss_ptr=None, stream=None):
+    """smx_nearest_centers on device buffers (k-means / SOAR assignment)."""
+    check(load().smx_nearest_centers(x_ptr, int(n), int(d), c_ptr, int(k), primary_ptr,
+                                     float(lam), out_ptr, loss_ptr, _current_stream(stream)),
+          "smx_nearest_centers")
 
 
 class NativeIndex:

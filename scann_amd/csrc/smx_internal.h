@@ -297,6 +297,11 @@ hipError_t LaunchPairScatter(const DeviceIndex& ix, const SeedArgs& a, int nq, h
 // The rank kernel (one block per query, <= kSelMax keys in LDS) for k' <=
 // kSelMax, the block kernel otherwise; both rescan overflowed lists first.
 hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s);
+// Nearest center per row, or the SOAR secondary center with `primary`
+// (smx_builder.hip).
+hipError_t LaunchNearestCenters(const float* x, int64_t n, int d, const float* centers, int k,
+                                const int32_t* primary, float lambda, int32_t* out,
+                                float* out_loss, hipStream_t s);
 hipError_t LaunchMergeShards(const MergeArgs& a, hipStream_t s);
 hipError_t LaunchExactDistances(const DeviceIndex& ix, const float* queries, int nq,
                                 const uint32_t* ids, int k, float* out, hipStream_t s);

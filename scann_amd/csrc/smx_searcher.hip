@@ -893,6 +893,19 @@ int SearchHost(smx_index* h, const float* queries, int32_t nq, int32_t dim,
 
 extern "C" {
 
+int smx_nearest_centers(const float* x, int64_t n, int32_t d, const float* centers, int32_t k,
+                        const int32_t* primary, float lambda, int32_t* out, float* out_loss,
+                        void* stream) {
+  if (n < 0 || d <= 0 || k <= 0) return Fail(SMX_INVALID_ARGUMENT, "need n >= 0, d > 0, k > 0");
+  if (primary && k < 2) return Fail(SMX_INVALID_ARGUMENT, "SOAR assignment needs k >= 2");
+  if (n == 0) return SMX_OK;
+  if (!x || !centers || !out) return Fail(SMX_INVALID_ARGUMENT, "null input or output buffer");
+  if (!(lambda >= 0.0f)) return Fail(SMX_INVALID_ARGUMENT, "lambda must be >= 0");
+  SMX_HIP(smx::LaunchNearestCenters(x, n, d, centers, k, primary, lambda, out, out_loss,
+                                    static_cast<hipStream_t>(stream)));
+  return SMX_OK;
+}
+
 int smx_search_batched(smx_index* h, const float* queries, int32_t nq, int32_t dim,
                        const smx_search_params* p, uint32_t* out_idx, float* out_dist,
                        int32_t* out_count) {

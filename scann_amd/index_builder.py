@@ -22,9 +22,12 @@ builder API:
   (SOAR's orthogonality-amplified loss, kmeans_tree_partitioner.cc:926-997),
   encoded against that leaf's center.
 
-Uses torch on the GPU when one is visible (dense distance blocks), numpy
-otherwise; results differ only in training floating-point noise, which no
-parity claim depends on.
+On a GPU the row-to-center assignments (k-means steps, partitioning, SOAR)
+run in the hand-written HIP kernel smx_nearest_centers
+(scann_amd/csrc/smx_builder.hip) and the AVQ encoder and codebook encoding
+in torch; numpy otherwise.  Results differ only in training floating-point
+noise, which no parity claim depends on (the built index is the input of
+both the GPU path and the oracle).
 """
 from __future__ import annotations
 
@@ -46,20 +49,38 @@ def _torch_device():
     return None, None
 
 
+def _hip_nearest(x: np.ndarray, centers: np.ndarray, primary: Optional[np.ndarray] = None,
+                 lam: float = 0.0, chunk: int = 1 << 20) -> np.ndarray:
+    """The hand-written HIP assignment kernel (smx_nearest_centers,
+    scann_amd/csrc/smx_builder.hip) on rows streamed to the device in chunks."""
+    import torch
+    from . import _native
+    dev = torch.device("cuda")
+    c = torch.from_numpy(np.ascontiguousarray(centers, dtype=np.float32)).to(dev)
+    k, d = c.shape
+    out = np.empty(x.shape[0], dtype=np.int64)
+    res = torch.empty(min(chunk, max(1, x.shape[0])), dtype=torch.int32, device=dev)
+    for s in range(0, x.shape[0], chunk):
+        xb = torch.from_numpy(np.ascontiguousarray(x[s:s + chunk], dtype=np.float32)).to(dev)
+        m = xb.shape[0]
+        pb = None
+        if primary is not None:
+            pb = torch.from_numpy(np.ascontiguousarray(primary[s:s + chunk], dtype=np.int32)).to(dev)
+        _native.nearest_centers_device(xb.data_ptr(), m, d, c.data_ptr(), k, res.data_ptr(),
+                                       None if pb is None else pb.data_ptr(), lam)
+        out[s:s + m] = res[:m].cpu().numpy()
+    return out
+
+
 def _assign_l2(x: np.ndarray, centers: np.ndarray, chunk: int = 1 << 16) -> np.ndarray:
-    """argmin_c ||x - c||^2 for every row of x (ties -> lowest index)."""
+    """argmin_c ||x - c||^2 for every row of x (ties -> lowest index): the
+    HIP kernel when a GPU is visible, numpy otherwise."""
     torch, dev = _torch_device()
+    if torch is not None:
+        return _hip_nearest(x, centers)
     out = np.empty(x.shape[0], dtype=np.int64)
     # bound one distance block to ~2^28 entries (50000 centers: 5k rows)
     chunk = max(1024, min(chunk, (1 << 28) // max(1, centers.shape[0])))
-    if torch is not None:
-        c = torch.from_numpy(centers).to(dev)
-        cn = (c * c).sum(1)
-        for s in range(0, x.shape[0], chunk):
-            xb = torch.from_numpy(x[s:s + chunk]).to(dev)
-            d = cn[None, :] - 2.0 * (xb @ c.T)
-            out[s:s + chunk] = d.argmin(1).cpu().numpy()
-        return out
     cn = (centers * centers).sum(1)
     for s in range(0, x.shape[0], chunk):
         d = cn[None, :] - 2.0 * (x[s:s + chunk] @ centers.T)
@@ -252,24 +273,13 @@ def encode_avq(residuals: np.ndarray, originals: np.ndarray, codebook: np.ndarra
 
 def soar_assign(x: np.ndarray, centers: np.ndarray, primary: np.ndarray, lam: float,
                 chunk: int = 1 << 15) -> np.ndarray:
-    """Secondary leaf per row with the SOAR loss (never the primary leaf)."""
-    out = np.empty(x.shape[0], dtype=np.int64)
-    chunk = max(1024, min(chunk, (1 << 27) // max(1, centers.shape[0])))
+    """Secondary leaf per row with the SOAR loss (never the primary leaf): the
+    HIP kernel when a GPU is visible, numpy otherwise."""
     torch, dev = _torch_device()
     if torch is not None:
-        c = torch.from_numpy(centers).to(dev)
-        cn = (c * c).sum(1)
-        for s in range(0, x.shape[0], chunk):
-            xb = torch.from_numpy(x[s:s + chunk]).to(dev)
-            p = torch.from_numpy(primary[s:s + chunk]).to(dev)
-            r = xb - c[p]
-            rn = (r * r).sum(1).clamp_min(1e-30)
-            d2 = (xb * xb).sum(1, keepdim=True) - 2.0 * (xb @ c.T) + cn[None, :]
-            proj = (r * xb).sum(1, keepdim=True) - r @ c.T
-            loss = d2 + lam * proj * proj / rn[:, None]
-            loss[torch.arange(xb.shape[0], device=dev), p] = float("inf")
-            out[s:s + chunk] = loss.argmin(1).cpu().numpy()
-        return out
+        return _hip_nearest(x, centers, primary=primary, lam=float(lam))
+    out = np.empty(x.shape[0], dtype=np.int64)
+    chunk = max(1024, min(chunk, (1 << 27) // max(1, centers.shape[0])))
     cn = (centers * centers).sum(1)
     for s in range(0, x.shape[0], chunk):
         xb, p = x[s:s + chunk], primary[s:s + chunk]
