@@ -140,7 +140,7 @@ struct smx_index {
   uint32_t chunk_tiles = 20;       // tiles per work item (tools/tune.py: 16-20 best at glove)
   int grid = 0;                    // scan grid: resident one-wave workgroups (occupancy API)
   bool profiling = false;
-  bool use_graph = true;           // replay the first pass as a hipGraph
+  bool use_graph = false;          // SMX_GRAPH=1: replay the pipeline as a hipGraph
   hipGraphExec_t graph_exec = nullptr;
   uint64_t graph_key[16] = {};
   uint64_t ws_generation = 0;
@@ -799,7 +799,11 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
   if (const char* fw = std::getenv("SMX_FUSED_WORKLIST"))
     h->fused_worklist_leaves = std::min(std::atoi(fw), smx::kFusedWorklistLeaves);
   const char* ng = std::getenv("SMX_NO_GRAPH");
-  h->use_graph = !(ng && ng[0] == '1');
+  // Eager launches by default: six kernels a call queue back to back on the
+  // stream, while consecutive replays of a captured graph left ~13 us
+  // between graphs (0.165 vs 0.158 ms/step, bench A/B on one box).
+  const char* gr = std::getenv("SMX_GRAPH");
+  h->use_graph = gr && gr[0] == '1' && !(ng && ng[0] == '1');
 
   *out = h;
   return SMX_OK;

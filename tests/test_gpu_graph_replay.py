@@ -18,14 +18,14 @@ def medium():
     return make_index(n=60000, d=32, leaves=120, seed=21, components=200)
 
 
-# graph replay, eager; the work list from the fused seed-launch blocks (the
+# eager (the default), graph replay; the work list from the fused seed-launch blocks (the
 # default at <= 4096 leaves) and from the side-stream fork/join path
-@pytest.mark.parametrize("env", [{}, {"SMX_NO_GRAPH": "1"}, {"SMX_FUSED_WORKLIST": "0"},
-                                 {"SMX_FUSED_WORKLIST": "0", "SMX_NO_GRAPH": "1"}])
+@pytest.mark.parametrize("env", [{}, {"SMX_GRAPH": "1"}, {"SMX_FUSED_WORKLIST": "0"},
+                                 {"SMX_FUSED_WORKLIST": "0", "SMX_GRAPH": "1"}])
 def test_replays_see_new_queries(oracle, medium, env):
     from scann_amd import _native, synthetic
     ix, db, _ = medium
-    old = {k: os.environ.get(k) for k in ("SMX_NO_GRAPH", "SMX_FUSED_WORKLIST")}
+    old = {k: os.environ.get(k) for k in ("SMX_GRAPH", "SMX_NO_GRAPH", "SMX_FUSED_WORKLIST")}
     try:
         for k in old:
             os.environ.pop(k, None)
