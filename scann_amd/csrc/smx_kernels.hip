@@ -963,12 +963,12 @@ __global__ void __launch_bounds__(64) items_kernel(WorklistArgs w) {
 // The work list without extra launches (nl <= kFusedWorklistLeaves): extra
 // blocks of the seed launch, each of which scans ALL positions redundantly
 // (16 per thread: two rounds of independent loads, then block scans) and
-// builds the items of its own kWlPosPerBlock positions, one wave at a time.  No
+// builds the items of its own kWlPosPerBlock positions, one wave each.  No
 // block waits for another; block 0 also writes the global prefixes (the pair
 // scatter reads leaf_item0) and totals.  The seed blocks neither read nor
 // write anything these touch.
 constexpr int kWlPerThread = kFusedWorklistLeaves / 256;
-constexpr int kWlPosPerBlock = 8;
+constexpr int kWlPosPerBlock = 4;
 
 __device__ void WorklistFusedBlock(const WorklistArgs& w, int b) {
   __shared__ uint32_t wsum[4], s_gunits[kGroups + 1], s_last_un[256];
@@ -1327,17 +1327,15 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
 }
 
 // Per query: its threshold key (SeedTau).
-// Per query: its threshold key (SeedTau); blocks [0, nwl) build the work list
-// (WorklistFusedBlock), block nwl + q takes query q.
+// Per query: its threshold key (SeedTau); blocks from nq on build the work
+// list (WorklistFusedBlock).
 template <int K>
-__global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a, WorklistArgs w, int nwl) {
-  // the fused work-list blocks first: they are short, and dispatched ahead
-  // of the seed blocks they never wait for a seed block's slot
-  if (int(blockIdx.x) < nwl) {
-    WorklistFusedBlock(w, int(blockIdx.x));
+__global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a, WorklistArgs w, int nq) {
+  const int qi = blockIdx.x;
+  if (qi >= nq) {   // the fused work-list blocks
+    WorklistFusedBlock(w, qi - nq);
     return;
   }
-  const int qi = int(blockIdx.x) - nwl;
   const uint64_t T = SeedTau<K>(a, qi);
   if (threadIdx.x == 0) a.tau_key[qi] = T;
 }
@@ -3023,7 +3021,7 @@ hipError_t LaunchLeafScores(const DeviceIndex& ix, int leaf, const int8_t* lut, 
 #define SMX_SEED_CASE(KV)                                                        \
   case KV:                                                                       \
     hipLaunchKernelGGL(seed_tau_kernel<KV>, dim3(nq + nwl), dim3(256), 0, s, a,            \
-                       wl ? *wl : WorklistArgs{}, nwl);                                     \
+                       wl ? *wl : WorklistArgs{}, nq);                                      \
     break;
 
 hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s,
