@@ -1145,7 +1145,13 @@ __device__ __forceinline__ void LoadCodes(const uint8_t* p, uint32_t* codes) {
 // a 256-bin histogram over the order-preserving bits narrow down to the
 // exact k'-th value.
 // ---------------------------------------------------------------------------
-constexpr int kSeedPerThread = 32;
+#ifndef SMX_SEED_U
+#define SMX_SEED_U 8
+#endif
+#ifndef SMX_SEED_PER_THREAD
+#define SMX_SEED_PER_THREAD 32
+#endif
+constexpr int kSeedPerThread = SMX_SEED_PER_THREAD;
 constexpr uint32_t kSeedCap = 256u * kSeedPerThread;
 constexpr int kSeedMaxLeaves = 64;   // one wave of leaf slots
 constexpr int kSeedSel = 1024;       // values under the minima bound ranked exactly
@@ -1156,7 +1162,7 @@ template <int K>
 __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
   constexpr int W = 4 * NW;
-  constexpr int U = 8;   // datapoints whose code loads are in flight together
+  constexpr int U = SMX_SEED_U;   // datapoints whose code loads are in flight together
   constexpr int NB = (K + 1) / 2;   // code bytes per half holding steps < K
   __shared__ __align__(16) int8_t lut[2 * K * 16];
   // pair tables: ptab[h][j][byte] = the LUT sum of the two nibbles of code
