@@ -255,9 +255,9 @@ int smx_set_profiling(smx_index* index, int32_t enabled);
 int smx_get_timings(const smx_index* index, smx_timings* out);
 /* Tuning knobs: candidate buffer capacity per query (0, the default: sized
  * per call from k', leaves_to_search and the seed leaves), seed leaves used for the
- * per-query threshold, scan kernel variant (0 = the scan; 2, 4, 16 = timing
- * ablations whose results are invalid: without the hit list, without the
- * epilogue, without the copy to the candidate lists; 8 = diagnostic stamps)
+ * per-query threshold, scan kernel variant (must be 0 in this library; the
+ * timing ablations 2, 4, 16 -- whose results are invalid -- and the stamps
+ * of variant 8 exist only in the diagnostic build, -DSMX_SCAN_DIAGNOSTICS)
  * and tiles per work item (0 keeps the default, 20; at least 8). */
 int smx_set_tuning(smx_index* index, int32_t candidates_per_query, int32_t seed_leaves,
                    int32_t scan_variant, int32_t chunk_tiles);

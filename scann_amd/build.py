@@ -79,6 +79,29 @@ def build_pybind(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
+DIAG_OUT = os.path.join(ROOT, "scann_amd", "lib", "libscann_mi355x_diag.so")
+# The diagnostic library (loaded through $SMX_LIB by tools/ and by the
+# debug-check test run only): device index checks on every computed index
+# (a violation fails the call with SMX_INTERNAL), the scan's timing
+# ablations and per-segment stamps, and the front-end/select phase stamps.
+DIAG_DEFINES = ("SMX_DEBUG_CHECKS", "SMX_SCAN_DIAGNOSTICS", "SMX_PHASE_STAMPS")
+
+
+def build_diag(force: bool = False, verbose: bool = False) -> str:
+    if not force and os.path.exists(DIAG_OUT) and not needs_build_for(DIAG_OUT):
+        return DIAG_OUT
+    return build(force=True, verbose=verbose, defines=DIAG_DEFINES, out=DIAG_OUT)
+
+
+def needs_build_for(out: str) -> bool:
+    t = os.path.getmtime(out)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.abspath(__file__)]
+    return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
+
+
 if __name__ == "__main__":
+    if "--diag" in sys.argv:
+        print(build_diag(force="--force" in sys.argv, verbose=True))
+        sys.exit(0)
     print(build(force="--force" in sys.argv, verbose=True))
     print(build_pybind(force="--force" in sys.argv, verbose=True))

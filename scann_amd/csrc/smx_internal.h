@@ -75,6 +75,21 @@ struct ShardEntry {
   float exact;
 };
 
+// Sizes of the per-call buffers and of the index, for the index checks of
+// the debug build (-DSMX_DEBUG_CHECKS: every computed index into them is
+// verified before the access, a violation is counted and reported by the
+// host as SMX_INTERNAL; the product library compiles the checks out).
+struct Bounds {
+  uint32_t nq = 0;          // queries of the call
+  uint32_t items = 0;       // work items the workspace holds
+  uint32_t grid = 0;        // scan workgroups (wave_start entries)
+  uint32_t nl = 0;          // leaves
+  uint32_t datapoints = 0;  // dataset rows
+  uint32_t pad = 0;
+  uint64_t members = 0;     // leaf members (members[], member_rows)
+  uint64_t tiles = 0;       // code tiles
+};
+
 // One work item of the scan: a chunk [j0, jend) of the 32-datapoint tiles of
 // a leaf, for one 32-query tile of that leaf's query list.
 struct WorkItem {
@@ -118,6 +133,7 @@ struct ScanArgs {
   int nl;
   int nb;
   int shift;
+  Bounds bd;                  // debug-build index checks
 };
 
 struct SeedArgs {
@@ -140,6 +156,7 @@ struct SeedArgs {
   int kk;
   int residual;
   int nb;
+  Bounds bd;                  // debug-build index checks
 };
 
 // The work list's inputs and outputs (LaunchWorklist / the fused block of
@@ -162,6 +179,7 @@ struct WorklistArgs {
   WorkItem* work;
   ItemLane* lanes;
   uint4* wave_start;           // [grid]
+  Bounds bd;                  // debug-build index checks
 };
 // Up to this many leaves the work list is built by one extra block of the
 // seed launch (no second stream, no fork/join); above it by three launches.
@@ -189,6 +207,7 @@ struct RescanArgs {
   uint32_t cap;
   int kk;
   uint32_t* stats;            // [10] queries rescanned [11] rescan rounds
+  Bounds bd;                  // debug-build index checks
 };
 
 struct SelectArgs {
@@ -218,6 +237,7 @@ struct SelectArgs {
   ShardEntry* shard_out;      // shard mode: [nq][kk] local top-k' entries (or NULL)
   const uint32_t* row_base;   // shard: whole-leaf row of each leaf's first shard row
   const float* member_rows;   // shard: [members][dim] rows for the exact distances
+  Bounds bd;                  // debug-build index checks
 };
 
 struct MergeArgs {
@@ -275,7 +295,8 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count,
                           ItemLane* lanes /*[max items][32]*/, uint4* wave_start /*[grid]*/,
                           int grid, uint32_t* totals /*[3]*/,
                           unsigned long long* code_bytes /*[1]*/, uint32_t chunk_tiles,
-                          unsigned long long* part /*[4 * ceil(nl / 256)]*/, hipStream_t s);
+                          unsigned long long* part /*[4 * ceil(nl / 256)]*/, const Bounds& bd,
+                          hipStream_t s);
 // variant 0: the LUT16 scan (lut16_scan_kernel); 4: the same without its
 // threshold epilogue (timing ablation, results invalid).
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,
@@ -286,7 +307,8 @@ hipError_t ScanBlocksPerCU(const DeviceIndex& ix, int* blocks);
 WorklistArgs MakeWorklistArgs(const DeviceIndex& ix, const uint32_t* leaf_count, WorkItem* work,
                               uint32_t* leaf_item0, uint32_t* pos_unit0, uint32_t* gunits,
                               ItemLane* lanes, uint4* wave_start, int grid, uint32_t* totals,
-                              unsigned long long* code_bytes, uint32_t chunk_tiles);
+                              unsigned long long* code_bytes, uint32_t chunk_tiles,
+                              const Bounds& bd);
 // The seed thresholds (one block per query); with `wl`, one more block
 // builds the whole work list (ix.nl <= kFusedWorklistLeaves).
 hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s,
@@ -297,6 +319,9 @@ hipError_t LaunchPairScatter(const DeviceIndex& ix, const SeedArgs& a, int nq, h
 // The rank kernel (one block per query, <= kSelMax keys in LDS) for k' <=
 // kSelMax, the block kernel otherwise; both rescan overflowed lists first.
 hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s);
+// Whether the final selection of these arguments fits the CU's 160 KiB LDS
+// (static + dynamic; the block kernel for k' > kSelMax holds the whole list).
+bool FinalSelectFits(const SelectArgs& a);
 // Nearest center per row, or the SOAR secondary center with `primary`
 // (smx_builder.hip).
 hipError_t LaunchNearestCenters(const float* x, int64_t n, int d, const float* centers, int k,
@@ -311,6 +336,9 @@ hipError_t LaunchLeafScores(const DeviceIndex& ix, int leaf, const int8_t* lut,
 // ([3 kernels][kPhaseQueries][8] u64, or NULL).
 constexpr int kPhaseQueries = 4096;
 hipError_t SetPhaseStamps(unsigned long long* p);
+// Debug build only (-DSMX_DEBUG_CHECKS): index-check violations counted on
+// the device since the last call (reset to 0); always 0 in the product build.
+hipError_t TakeCheckFailures(unsigned int* out);
 hipError_t LaunchFill64(uint64_t* p, uint64_t v, size_t n, hipStream_t s);
 
 }  // namespace smx

@@ -63,13 +63,36 @@ __device__ __forceinline__ float FromOrdered(uint32_t o) {
 __device__ unsigned long long* g_phase_stamps;
 #define SMX_PHASE(kid, qi, ph)                                                             \
   do {                                                                                     \
-    if (g_phase_stamps && (threadIdx.x & 63) == 0)                                         \
+    if (g_phase_stamps && (threadIdx.x & 63) == 0 && (qi) < kPhaseQueries)                 \
       g_phase_stamps[((size_t(kid) * kPhaseQueries) + (qi)) * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
 #define SMX_PHASE(kid, qi, ph) \
   do {                         \
   } while (0)
+#endif
+
+// Debug build only (-DSMX_DEBUG_CHECKS): SMX_GUARD(v, bound, tag) stmt; runs
+// stmt only when v < bound and otherwise counts and prints the violation
+// (the host turns a non-zero count into SMX_INTERNAL after the call);
+// SMX_CHECK(v, bound, tag) only counts.  Both vanish from the product library.
+#ifdef SMX_DEBUG_CHECKS
+__device__ unsigned int g_check_failures;
+__device__ __noinline__ bool SmxCheckFailed(const char* tag, int line, unsigned long long v,
+                                            unsigned long long bound) {
+  if (atomicAdd(&g_check_failures, 1u) < 32u)
+    printf("SMX_CHECK %s (line %d): value %llu bound %llu, block %u thread %u\n", tag, line, v,
+           bound, blockIdx.x, threadIdx.x);
+  return false;
+}
+#define SMX_LT(v, b, tag) \
+  (((unsigned long long)(v) < (unsigned long long)(b)) || \
+   SmxCheckFailed(tag, __LINE__, (unsigned long long)(v), (unsigned long long)(b)))
+#define SMX_GUARD(v, b, tag) if (SMX_LT(v, b, tag))
+#define SMX_CHECK(v, b, tag) ((void)SMX_LT(v, b, tag))
+#else
+#define SMX_GUARD(v, b, tag)
+#define SMX_CHECK(v, b, tag) ((void)0)
 #endif
 
 __device__ __forceinline__ uint32_t NextPow2(uint32_t x) {
@@ -110,6 +133,17 @@ __device__ __forceinline__ uint32_t CountLess(const uint64_t* keys, uint32_t n, 
   }
   if (j < n) r += keys[j] < key ? 1u : 0u;
   return r;
+}
+
+// Stable rank of keys[i] == key among keys[0..n): the keys below it plus
+// the equal keys at lower positions.  Distinct keys rank as CountLess; equal
+// keys (the two copies of a SOAR-spilled datapoint in an index without the
+// global top-N tie, whose keys coincide) get consecutive ranks.
+__device__ __forceinline__ uint32_t RankStable(const uint64_t* keys, uint32_t n, uint64_t key,
+                                               uint32_t i) {
+  uint32_t r = 0;
+  for (uint32_t j = 0; j < i; ++j) r += keys[j] <= key ? 1u : 0u;
+  return r + CountLess(keys + i + 1, n - i - 1, key);
 }
 
 // Block-wide bitonic sort (ascending) of n (power of two) keys in LDS.
@@ -826,7 +860,7 @@ __global__ void __launch_bounds__(256) worklist_kernel(
   __shared__ uint32_t wsum[4], s_units[256];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nblk = int(gridDim.x), blk = int(blockIdx.x);
-  // the blocks before this one and all blocks (nblk <= 256 for nl <= 65536)
+  // the blocks before this one and all blocks (256 per round)
   unsigned long long bi = 0, bu = 0, ti = 0, tu = 0, tp = 0, tb = 0;
   for (int b = tid; b < nblk; b += 256) {
     const WorklistPart w = part[b];
@@ -901,7 +935,9 @@ __device__ void ItemsCore(const WorklistArgs& w, int p, int lane, const uint32_t
     // positions write every other wave's share)
     for (int i = lane; i < w.grid; i += 64) {
       const int g = i & (kGroups - 1);
-      if (gunits[g + 1] == gunits[g]) w.wave_start[i] = make_uint4(0, 0, 0, 0);
+      if (gunits[g + 1] == gunits[g]) {
+        SMX_GUARD(i, w.bd.grid, "empty wave start") w.wave_start[i] = make_uint4(0, 0, 0, 0);
+      }
     }
   }
   const uint32_t chunk_tiles = w.chunk_tiles;
@@ -919,7 +955,7 @@ __device__ void ItemsCore(const WorklistArgs& w, int p, int lane, const uint32_t
     it.jend = cr.y;
     it.tile_off = toff;
     it.member_off = moff;
-    w.work[item0 + u] = it;
+    SMX_GUARD(item0 + u, w.bd.items, "work item") w.work[item0 + u] = it;
   }
   if (qt) {
     const uint32_t first = c - (qt - 1) * kQueriesPerTile;   // empty slots [first, 32)
@@ -930,6 +966,7 @@ __device__ void ItemsCore(const WorklistArgs& w, int p, int lane, const uint32_t
       v.bias = 0.0f;
       v.inv = 0.0f;
       v.amax = kNoSum;   // never passes
+      SMX_GUARD(item0 + (qt - 1) * chunks + e / ne, w.bd.items, "empty-slot lane")
       w.lanes[size_t(item0 + (qt - 1) * chunks + e / ne) * kQueriesPerTile + first + e % ne] = v;
     }
   }
@@ -950,6 +987,8 @@ __device__ void ItemsCore(const WorklistArgs& w, int p, int lane, const uint32_t
     const uint32_t off = us - ua, tq = off / tiles, rem = off % tiles;
     uint32_t ch = 0;
     while (ChunkTiles(n, chunk_tiles, ch).y <= rem) ++ch;
+    SMX_CHECK(item0 + tq * chunks + ch, w.bd.items, "wave start item");
+    SMX_GUARD(kGroups * k + g, w.bd.grid, "wave start")
     w.wave_start[kGroups * k + g] = make_uint4(item0 + tq * chunks + ch, rem, ue - us, 0);
   }
 }
@@ -1227,6 +1266,7 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
         while (g >= s_start[r + 1]) ++r;
         ru[u] = r;
         const uint32_t dp = g - s_start[r];
+        SMX_CHECK(s_tile0[r] + (dp >> 5), a.bd.tiles, "seed tile");
         const uint8_t* t0 = a.tiles + ((s_tile0[r] + (dp >> 5)) * 64 + (dp & 31)) * W;
         LoadCodes<K>(t0, c0[u]);
         LoadCodes<K>(t0 + 32 * W, c1[u]);
@@ -1372,9 +1412,12 @@ __global__ void __launch_bounds__(256) pair_scatter_kernel(SeedArgs a, int nq) {
   v.amax = tau == kNoThreshold ? 128 * a.nb
                                : SumLimit(FromOrdered(uint32_t(tau >> 32)), v.inv, v.bias,
                                           -128 * a.nb, 128 * a.nb);
+  SMX_CHECK(leaf, a.bd.nl, "pair leaf");
   const uint32_t w0 = a.leaf_item0[leaf] + (r / kQueriesPerTile) * chunks;
-  for (uint32_t ch = 0; ch < chunks; ++ch)
+  for (uint32_t ch = 0; ch < chunks; ++ch) {
+    SMX_GUARD(w0 + ch, a.bd.items, "pair lane")
     a.lanes[size_t(w0 + ch) * kQueriesPerTile + (r % kQueriesPerTile)] = v;
+  }
 }
 
 
@@ -1562,6 +1605,7 @@ __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32
     const WorkItem it = a.work[min(idx, a.num_items - 1)];
     const uint32_t j0 = (lane == 0 && sj) ? sj : it.j0;
     const uint32_t t = it.jend > j0 ? min(it.jend - j0, su) : 0u;
+    if (t > 0) SMX_CHECK(idx, a.bd.items, "listed item");
     uint32_t incl = t;
     for (int off = 1; off < 64; off <<= 1) {
       const uint32_t y = uint32_t(__shfl_up(int(incl), off));
@@ -1657,6 +1701,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
     for (uint32_t e = uint32_t(lane); e < kn; e += 64) {
       const uint32_t qs = wl.kslot[pp][e];
       const uint32_t sl = wl.q_slot[qs] + atomicAdd(&wl.qrun[qs], 1u);
+      SMX_GUARD(wl.prev_qid[qs], a.bd.nq, "list query")
       if (sl < a.cap) a.cand[size_t(wl.prev_qid[qs]) * a.cap + sl] = wl.kbuf[pp][e];
     }
     WaveLdsSync();
@@ -1669,6 +1714,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   auto flush_prev = [&]() {
     if ((ABL & 16) == 0 && lane < Q) {   // (16: timing ablation without the lists)
       const uint32_t m = wl.qcnt[lane];
+      if (m) SMX_CHECK(fqid, a.bd.nq, "slot query");
       slot = m ? atomicAdd(&a.cand_count[size_t(fqid) * kCounterStride], m) : 0u;
       wl.prev_qid[lane] = fqid;
     }
@@ -1737,6 +1783,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         cl = pf_rec;
       } else {
         item = __builtin_amdgcn_readfirstlane(s_item[sg]);
+        SMX_CHECK(item, a.bd.items, "segment item");
         cl = a.lanes[size_t(item) * Q + c];
       }
       const uint32_t qid = cl.qid;
@@ -1749,6 +1796,10 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
                             __builtin_amdgcn_readfirstlane(uint32_t(sd.member_off));
       const uint32_t n = __builtin_amdgcn_readfirstlane(sd.n);
       const int leaf = int(__builtin_amdgcn_readfirstlane(sd.leaf));
+      SMX_CHECK(qid == kNoQuery ? 0u : qid, a.bd.nq, "slot record query");
+      SMX_CHECK(leaf, a.bd.nl, "segment leaf");
+      SMX_CHECK(toff + (n + 31u) / 32u, a.bd.tiles + 1, "segment tiles");
+      SMX_CHECK(moff + n, a.bd.members + 1, "segment members");
       // this segment's B fragments (LUT rows 2s+h of query c) and first tile
       v8i b[K / 2];
       uint32_t codes[NW] = {};
@@ -1775,6 +1826,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         if (sn < nseg) {
           pf_seg = sn;
           pf_item = __builtin_amdgcn_readfirstlane(s_item[sn]);
+          SMX_CHECK(pf_item, a.bd.items, "prefetch item");
           pf_rec = a.lanes[size_t(pf_item) * Q + c];
         } else {
           pf_seg = ~0u;
@@ -2524,19 +2576,23 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
       const uint64_t kth = KthSmallestKey(ck, n, k, hist, wsum);
       for (uint32_t i = tid; i < n; i += 256) {
         const uint64_t key = ck[i];
-        if (key <= kth) sel[atomicAdd(&s_c, 1u)] = key;
+        if (key <= kth) {
+          // (equal keys -- SOAR copies without the global top-N tie -- can
+          // put one more key than k at kth: it ranks >= k and is dropped)
+          const uint32_t pos = atomicAdd(&s_c, 1u);
+          if (pos < uint32_t(kSelMax)) sel[pos] = key;
+        }
       }
     }
     __syncthreads();
   }
   SMX_PHASE(2, qi, 1);
-  const uint32_t c = n <= uint32_t(kSelMax) ? n : s_c;
-  // counting rank: keys are unique, so rank = number of smaller keys
+  const uint32_t c = n <= uint32_t(kSelMax) ? n : min(s_c, uint32_t(kSelMax));
+  // counting rank (stable: equal keys, the SOAR copies of an index without
+  // the global top-N tie, take consecutive ranks)
   if (uint32_t(tid) < c) {
     const uint64_t key = sel[tid];
-    uint32_t r = 0;
-    r = CountLess(sel, c, key);
-    out[r] = key;
+    out[RankStable(sel, c, key, uint32_t(tid))] = key;
   }
   __syncthreads();
   SMX_PHASE(2, qi, 2);
@@ -2551,13 +2607,16 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
     if (a.shift > 0) {
       const uint32_t leaf = tie >> a.shift;
       const uint32_t local = tie & ((1u << a.shift) - 1u);
+      SMX_CHECK(leaf, a.bd.nl, "select leaf");
       const uint64_t slot = a.member_off[leaf] + local;
+      SMX_CHECK(slot, a.bd.members, "select member");
       tie = a.members[slot];
       rid = a.member_rows ? uint32_t(slot) : tie;
       if (a.shard_out && a.row_base)   // whole-index tie for the merge
         out[tid] = (key & 0xFFFFFFFF00000000ull) |
                    ((leaf << a.shift) | (local + a.row_base[leaf]));
     }
+    SMX_CHECK(rid, a.member_rows ? a.bd.members : uint64_t(a.bd.datapoints), "select row");
     gid[tid] = tie;
     rowid[tid] = rid;
     dist[tid] = FromOrdered(uint32_t(key >> 32));
@@ -2687,10 +2746,13 @@ __global__ void __launch_bounds__(256) merge_shards_kernel(MergeArgs a) {
     uint32_t r = uint32_t(j);
     for (int v = 0; v < W && r < uint32_t(kk); ++v) {
       if (v == w) continue;
+      // equal keys in two lists (SOAR copies without the global top-N tie)
+      // rank by list: the lower list's copy first
       int lo = 0, hi = int(cnt[v]);
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if (lk[v * kk + mid] < key) lo = mid + 1; else hi = mid;
+        const uint64_t x = lk[v * kk + mid];
+        if (x < key || (v < w && x == key)) lo = mid + 1; else hi = mid;
       }
       r += uint32_t(lo);
     }
@@ -2891,8 +2953,10 @@ hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq, i
 WorklistArgs MakeWorklistArgs(const DeviceIndex& ix, const uint32_t* leaf_count, WorkItem* work,
                               uint32_t* leaf_item0, uint32_t* pos_unit0, uint32_t* gunits,
                               ItemLane* lanes, uint4* wave_start, int grid, uint32_t* totals,
-                              unsigned long long* code_bytes, uint32_t chunk_tiles) {
+                              unsigned long long* code_bytes, uint32_t chunk_tiles,
+                              const Bounds& bd) {
   WorklistArgs w;
+  w.bd = bd;
   w.cnt = leaf_count;
   w.order = ix.leaf_order;
   w.leaf_size = ix.leaf_size;
@@ -2917,9 +2981,8 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
                           uint32_t* leaf_item0, uint32_t* pos_unit0, uint32_t* gunits,
                           ItemLane* lanes, uint4* wave_start, int grid, uint32_t* totals,
                           unsigned long long* code_bytes, uint32_t chunk_tiles,
-                          unsigned long long* part, hipStream_t s) {
-  const int nblk = (ix.nl + 255) / 256;
-  if (nblk > 256) return hipErrorInvalidValue;   // more than 65536 leaves
+                          unsigned long long* part, const Bounds& bd, hipStream_t s) {
+  const int nblk = (ix.nl + 255) / 256;   // (worklist_kernel loops over any count)
   WorklistPart* wp = reinterpret_cast<WorklistPart*>(part);
   hipLaunchKernelGGL(worklist_part_kernel, dim3(nblk), dim3(256), 0, s, leaf_count, ix.leaf_order,
                      ix.leaf_size, ix.nl, ix.nb, chunk_tiles, wp);
@@ -2927,11 +2990,16 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
                      ix.leaf_size, ix.nl, ix.nb, chunk_tiles, wp, leaf_item0, pos_unit0, gunits,
                      totals, code_bytes);
   const WorklistArgs w = MakeWorklistArgs(ix, leaf_count, work, leaf_item0, pos_unit0, gunits,
-                                          lanes, wave_start, grid, totals, code_bytes, chunk_tiles);
+                                          lanes, wave_start, grid, totals, code_bytes, chunk_tiles,
+                                          bd);
   hipLaunchKernelGGL(items_kernel, dim3(ix.nl), dim3(64), 0, s, w);
   return hipGetLastError();
 }
 
+// The product library compiles the scan only; the timing ablations (2, 4,
+// 16: results invalid) and the per-segment stamps (8) exist in the
+// diagnostic build (-DSMX_SCAN_DIAGNOSTICS, tools/tune.py / scan_stamps.py).
+#ifdef SMX_SCAN_DIAGNOSTICS
 #define SMX_SCAN_CASE(KV)                                                                  \
   case KV:                                                                                 \
     if (variant == 16)                                                                     \
@@ -2950,6 +3018,14 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
                          0, s, a);                                                         \
     break;
+#else
+#define SMX_SCAN_CASE(KV)                                                                  \
+  case KV:                                                                                 \
+    if (variant != 0) return hipErrorInvalidValue;                                         \
+    hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()),  \
+                       0, s, a);                                                           \
+    break;
+#endif
 
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,
                       hipStream_t s) {
@@ -3068,8 +3144,30 @@ hipError_t LaunchMergeShards(const MergeArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+bool FinalSelectFits(const SelectArgs& a) {
+  if (a.kk <= kSelMax) return true;   // the rank kernel: fixed LDS
+  uint32_t kkp2 = 1;
+  while (kkp2 < uint32_t(a.kk)) kkp2 <<= 1;
+  uint32_t kcap = 1;
+  while (kcap < a.cap) kcap <<= 1;
+  const uint32_t selcap = std::max<uint32_t>(2048u, 2 * kkp2);
+  const size_t lds = size_t(kcap) * 8 + size_t(selcap) * 8 + size_t(kkp2) * 8 +
+                     size_t(a.dim) * 4 + size_t(a.kk) * 8 + (kSelBins + 256) * 4;
+  // the kernel's static LDS (the inlined overflow rescan's tables and the
+  // selection words) counts against the same 160 KiB
+  static const size_t static_lds = [] {
+    hipFuncAttributes fa{};
+    return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&final_select_kernel)) ==
+                   hipSuccess
+               ? size_t(fa.sharedSizeBytes)
+               : size_t(32 * 1024);
+  }();
+  return lds + static_lds <= 160 * 1024;
+}
+
 hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s) {
   if (nq == 0) return hipSuccess;
+  if (!FinalSelectFits(a)) return hipErrorInvalidValue;
   // the overflow flag is raised by the select kernels themselves; the
   // candidate-count statistics only for profiled calls
   if (a.stats)
@@ -3086,7 +3184,6 @@ hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s) {
   }
   const size_t lds = size_t(kcap) * 8 + size_t(selcap) * 8 + size_t(kkp2) * 8 +
                      size_t(a.dim) * 4 + size_t(a.kk) * 8 + (kSelBins + 256) * 4;
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(final_select_kernel, dim3(nq), dim3(256), lds, s, a);
   return hipGetLastError();
 }
@@ -3104,6 +3201,18 @@ hipError_t SetPhaseStamps(unsigned long long* p) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_phase_stamps), &p, sizeof(p));
 #else
   (void)p;
+  return hipSuccess;
+#endif
+}
+
+hipError_t TakeCheckFailures(unsigned int* out) {
+#ifdef SMX_DEBUG_CHECKS
+  unsigned int zero = 0;
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_check_failures), sizeof(unsigned int));
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_check_failures), &zero, sizeof(zero));
+  return e;
+#else
+  *out = 0;
   return hipSuccess;
 #endif
 }

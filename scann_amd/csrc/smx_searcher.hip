@@ -363,10 +363,22 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
   // tightening pass drops at least cap - k' keys
   const uint32_t base = h->cap_per_query ? h->cap_per_query
                                          : AutoCap(L, kk, std::min(h->seed_leaves, L));
-  const uint32_t cap = std::max<uint32_t>(base, 2u * uint32_t(kk));
-  if (nq <= w.nq && L <= w.L && kk <= w.kk && width <= w.width && cap == w.cap &&
-      ix.dim == w.dim)
+  uint32_t cap = std::max<uint32_t>(base, 2u * uint32_t(kk));
+  // a larger list than this call needs is reused as it is (w.cap is the
+  // stride every kernel uses): varying leaves_to_search never frees and
+  // reallocates the workspace (hipFree synchronises the device) unless it
+  // has to grow, and then it grows to cover both shapes
+  // (an explicit capacity, smx_set_tuning, is used exactly)
+  const bool cap_ok = h->cap_per_query ? cap == w.cap : cap <= w.cap;
+  if (nq <= w.nq && L <= w.L && kk <= w.kk && width <= w.width && cap_ok && ix.dim == w.dim)
     return SMX_OK;
+  if (w.nq) {
+    nq = std::max(nq, w.nq);
+    L = std::max(L, w.L);
+    kk = std::max(kk, w.kk);
+    width = std::max(width, w.width);
+    if (!h->cap_per_query) cap = std::max(cap, w.cap);
+  }
   w.Release();
   const int nl = ix.nl;
   const size_t pairs = size_t(nq) * L;
@@ -437,7 +449,16 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   const int seed = std::min(h->seed_leaves, L);
 
   const int variant = h->scan_variant;
+  smx::Bounds bd;
+  bd.nq = uint32_t(nq);
+  bd.items = w.max_items;
+  bd.grid = uint32_t(std::max(h->grid, 1));
+  bd.nl = uint32_t(nl);
+  bd.datapoints = ix.num_datapoints;
+  bd.members = ix.num_members;
+  bd.tiles = ix.num_tiles;
   smx::SeedArgs sa{};
+  sa.bd = bd;
   sa.topl_leaf = w.topl_leaf;
   sa.topl_dist = w.topl_dist;
   sa.rank = w.rank;
@@ -457,6 +478,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sa.residual = ix.residual;
 
   smx::ScanArgs a{};
+  a.bd = bd;
   a.tiles = ix.tiles;
   a.members = ix.members;
   a.lut = w.lut;
@@ -484,6 +506,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   a.shift = ix.shift;
 
   smx::SelectArgs sel{};
+  sel.bd = bd;
   sel.cand = w.cand;
   sel.cand_count = w.cand_count;
   sel.cap = w.cap;
@@ -507,6 +530,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sel.overflow = stats;
   sel.stats = h->profiling ? 1 : 0;
   smx::RescanArgs& ra = sel.rescan;
+  ra.bd = bd;
   ra.topl_leaf = w.topl_leaf;
   ra.topl_dist = w.topl_dist;
   ra.L = L;
@@ -529,6 +553,10 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sel.shard_out = shard_out;
   sel.row_base = ix.row_base;
   sel.member_rows = ix.member_rows;
+  if (!smx::FinalSelectFits(sel))
+    return Fail(SMX_INVALID_ARGUMENT,
+                "the candidate list capacity, k' and dim exceed the final selection's 160 KiB of "
+                "LDS (lower candidates_per_query or pre_reorder_num_neighbors)");
 
   // First pass: everything up to the stats copy.  Replayed as a captured
   // hipGraph when the call shape, buffers and stream repeat (one launch
@@ -558,7 +586,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
       // stream: a fork/join costs 5-10 us per cross-queue edge)
       const smx::WorklistArgs wla = smx::MakeWorklistArgs(
           ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes, w.wave_start, h->grid,
-          stats + 3, code_bytes, h->chunk_tiles);
+          stats + 3, code_bytes, h->chunk_tiles, bd);
       Mark(h, 3, s);
       SMX_HIP(smx::LaunchSeed(ix, sa, nq, s, &wla));
       Mark(h, 4, s);
@@ -578,7 +606,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
       SMX_HIP(hipStreamWaitEvent(h->side, h->fork_ev, 0));
       SMX_HIP(smx::LaunchWorklist(ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes,
                                   w.wave_start, h->grid, stats + 3, code_bytes, h->chunk_tiles,
-                                  w.wl_part, h->side));
+                                  w.wl_part, bd, h->side));
       Mark(h, 3, h->side);
       SMX_HIP(hipEventRecord(h->join_ev, h->side));
       SMX_HIP(hipStreamWaitEvent(s, h->join_ev, 0));   // join
@@ -593,6 +621,23 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     Mark(h, 7, s);
     return SMX_OK;
   };
+#ifdef SMX_PHASE_STAMPS
+  // diagnostic build: the stamp buffer is installed once, before the first
+  // call's kernels are enqueued and with the device idle.  (The first
+  // version installed it after the first call's launches with a null-stream
+  // hipMemcpyToSymbol, which does not order against the handle's
+  // non-blocking stream: kernels in flight read g_phase_stamps while it was
+  // being rewritten -- a torn 64-bit pointer -- and faulted.)
+  static unsigned long long* phase_buf = nullptr;
+  if (!phase_buf) {
+    const size_t words = size_t(3) * smx::kPhaseQueries * 8;
+    SMX_HIP(hipDeviceSynchronize());
+    SMX_HIP(hipMalloc(&phase_buf, words * 8));
+    SMX_HIP(hipMemset(phase_buf, 0, words * 8));
+    SMX_HIP(smx::SetPhaseStamps(phase_buf));
+    SMX_HIP(hipDeviceSynchronize());
+  }
+#endif
   // The workspace is shared by every stream: a call on another stream than
   // the last one waits for that one's work (stream-ordered, no host sync).
   // The event is recorded on the last stream only at such a switch (it then
@@ -666,21 +711,27 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
 #ifdef SMX_PHASE_STAMPS
   {
     // diagnostic build: the phase stamps of this call to $SMX_PHASE_FILE
-    static unsigned long long* ps = nullptr;
     const size_t words = size_t(3) * smx::kPhaseQueries * 8;
-    if (!ps) {
-      SMX_HIP(hipMalloc(&ps, words * 8));
-      SMX_HIP(smx::SetPhaseStamps(ps));
-    }
     if (const char* path = std::getenv("SMX_PHASE_FILE")) {
-      SMX_HIP(hipDeviceSynchronize());
+      SMX_HIP(hipStreamSynchronize(s));
       std::vector<unsigned long long> buf(words);
-      SMX_HIP(hipMemcpy(buf.data(), ps, words * 8, hipMemcpyDeviceToHost));
+      SMX_HIP(hipMemcpy(buf.data(), phase_buf, words * 8, hipMemcpyDeviceToHost));
       if (FILE* f = std::fopen(path, "wb")) {
         std::fwrite(buf.data(), 8, buf.size(), f);
         std::fclose(f);
       }
     }
+  }
+#endif
+#ifdef SMX_DEBUG_CHECKS
+  {
+    // debug build: every call is checked for index violations on the device
+    SMX_HIP(hipStreamSynchronize(s));
+    unsigned int bad = 0;
+    SMX_HIP(smx::TakeCheckFailures(&bad));
+    if (bad)
+      return Fail(SMX_INTERNAL, "debug build: " + std::to_string(bad) +
+                                    " device index-check violations (see the kernel printf)");
   }
 #endif
   smx_timings& t = h->timings;
@@ -756,8 +807,6 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
   if (rc) return rc;
   if (EffectiveKSteps(desc->num_blocks) < 0)
     return Fail(SMX_INVALID_ARGUMENT, "unsupported number of AH blocks");
-  if (desc->num_leaves > 65536)
-    return Fail(SMX_INVALID_ARGUMENT, "at most 65536 leaves (work-list block sums)");
   int ndev = 0;
   SMX_HIP(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return Fail(SMX_INVALID_ARGUMENT, "no such HIP device");
@@ -1150,10 +1199,17 @@ int smx_get_timings(const smx_index* h, smx_timings* out) {
 int smx_set_tuning(smx_index* h, int32_t candidates_per_query, int32_t seed_leaves,
                    int32_t scan_variant, int32_t chunk_tiles) {
   if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
+#ifdef SMX_SCAN_DIAGNOSTICS
   if (scan_variant != 0 && scan_variant != 2 && scan_variant != 4 && scan_variant != 8 &&
       scan_variant != 16)
     return Fail(SMX_INVALID_ARGUMENT,
                 "scan_variant is 0 (scan), 2 / 4 / 16 (timing ablations) or 8 (diagnostic stamps)");
+#else
+  if (scan_variant != 0)
+    return Fail(SMX_INVALID_ARGUMENT,
+                "scan_variant must be 0: the ablations and stamps exist only in the diagnostic "
+                "build (-DSMX_SCAN_DIAGNOSTICS)");
+#endif
   if (chunk_tiles != 0 && (chunk_tiles < 8 || chunk_tiles > 65535))
     return Fail(SMX_INVALID_ARGUMENT, "chunk_tiles must be 0 (default) or in [8, 65535]");
   if (candidates_per_query != 0 && (candidates_per_query < 32 || candidates_per_query > 8192))

@@ -121,7 +121,15 @@ def load_searcher(artifacts_dir, assets_backcompat_shim=True, device=0):
     (scann_ops_pybind_backcompat.py:30-70) and writes that list."""
     if not os.path.isdir(artifacts_dir):
         raise ValueError(f"{artifacts_dir} is not a directory.")
+    own = os.path.join(artifacts_dir, "smx_index.json")
     assets_pbtxt = os.path.join(artifacts_dir, "scann_assets.pbtxt")
+    if os.path.isfile(own) and not os.path.isfile(assets_pbtxt):
+        # this package's own format (TreeAHIndex.save) + scann_config.pbtxt
+        cfg = os.path.join(artifacts_dir, "scann_config.pbtxt")
+        if not os.path.isfile(cfg):
+            raise ValueError(f"{artifacts_dir}: smx_index.json needs scann_config.pbtxt beside it")
+        with open(cfg) as f:
+            return ScannSearcher(ScannNumpy(artifacts_dir, f.read(), device=device))
     if not os.path.exists(assets_pbtxt):
         if not assets_backcompat_shim:
             raise ValueError("No scann_assets.pbtxt found.")

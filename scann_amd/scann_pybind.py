@@ -24,6 +24,8 @@ from __future__ import annotations
 
 import ctypes
 
+import os
+
 import numpy as np
 
 from . import _native, assets
@@ -36,10 +38,25 @@ def _arg(v) -> int:
     return -1 if v is None else int(v)
 
 
+def _own_format(directory: str) -> bool:
+    """TreeAHIndex.save's layout (smx_index.json + .npy arrays) and no
+    reference asset list."""
+    return (os.path.isfile(os.path.join(directory, "smx_index.json")) and
+            not os.path.isfile(os.path.join(directory, "scann_assets.pbtxt")))
+
+
 class ScannNumpy:
     def __init__(self, db_or_dir, config: str, training_threads: int = 0, device: int = 0,
                  seed: int = 0):
-        if isinstance(db_or_dir, str):
+        if isinstance(db_or_dir, str) and _own_format(db_or_dir):
+            # a directory saved by TreeAHIndex.save (this package's own
+            # format) with the config text beside it in scann_config.pbtxt
+            index = TreeAHIndex.load(db_or_dir)
+            if not config:
+                with open(os.path.join(db_or_dir, "scann_config.pbtxt")) as f:
+                    config = f.read()
+            self._cfg = search_config_from_text(config)
+        elif isinstance(db_or_dir, str):
             index, tree, self._cfg = assets.load_artifacts(db_or_dir, config or None)
             config = assets.config_text(tree)
         else:

@@ -127,3 +127,19 @@ def test_cpp_core_defaults_and_errors(searcher, data):
         core.search_batched(q[0])
     with pytest.raises(RuntimeError, match="Error during search: "):
         core.search_batched(q[:4, :10])   # wrong dimensionality
+
+
+def test_own_format_directory_loads(searcher, data, tmp_path):
+    """A directory written by TreeAHIndex.save (this package's own format)
+    plus the config text loads through load_searcher / ScannNumpy as before
+    and searches identically."""
+    _, q = data
+    d = str(tmp_path / "own")
+    searcher.searcher.index.save(d)
+    with open(os.path.join(d, "scann_config.pbtxt"), "w") as f:
+        f.write(searcher.config())
+    loaded = scann_ops_pybind.load_searcher(d)
+    i0, d0 = searcher.search_batched(q)
+    i1, d1 = loaded.search_batched(q)
+    np.testing.assert_array_equal(i0, i1)
+    np.testing.assert_array_equal(d0, d1)

@@ -147,6 +147,33 @@ def test_soar_spilled_index_matches_oracle(native, oracle):
         np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
 
 
+@pytest.mark.parametrize("metric,residual", [(1, False), (0, False)])
+def test_soar_without_global_topn_matches_oracle(native, oracle, metric, residual):
+    """SOAR spilling on an index without the global top-N tie (squared L2, or
+    a non-residual dot index): both copies of a spilled datapoint carry the
+    same codes, no bias and the global id as tie, so their keys coincide; the
+    selection ranks equal keys stably (tree_x_hybrid_smmd.cc:784,
+    DeduplicateDatabaseSpilledResults then averages the copies)."""
+    from scann_amd import index_builder, synthetic
+    db = synthetic.mixture(5000, 32, 40, 0.9, 43, normalize=metric == 0)
+    q = synthetic.mixture(40, 32, 40, 0.9, 143, normalize=metric == 0, means_seed=43)
+    ix = index_builder.build_tree_ah(db, metric, 30, 2, training_iterations=4,
+                                     ah_training_iterations=4, soar_lambda=1.5,
+                                     residual=residual, seed=43)
+    assert not ix.disjoint
+    n = _nat(native, ix)
+    for leaves, pre in ((5, 20), (12, 100), (30, 128)):
+        gi, gd, gc = n.search_pre_reorder(q, leaves, pre)
+        oi, od, oc = oracle.search_pre_reorder(ix, q, leaves, pre, oracle.MODE_IDEAL)
+        np.testing.assert_array_equal(gc, oc)
+        np.testing.assert_array_equal(gi, oi)
+        np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+        gi, gd, gc = n.search_batched(q, leaves, pre, 10, True)
+        oi, od, oc = oracle.search(ix, q, leaves, pre, 10, True, oracle.MODE_IDEAL)
+        np.testing.assert_array_equal(gi, oi)
+        np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+
+
 def test_edge_cases(native, oracle):
     """Empty leaves, a single query, k larger than the candidates available,
     leaves_to_search larger than num_leaves, duplicate vectors (ties)."""
