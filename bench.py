@@ -122,6 +122,57 @@ def build_index(n, seed):
     return db, q, ix
 
 
+# The scan's ceiling: it issues v_smfmac_i32_32x32x64_i8, the 2:4 sparse i8
+# MFMA, which covers K = 64 in the 32 cycles of the dense K = 32 form
+# (tools/smfmac_chain.hip): 2 * 32 * 32 * 64 ops per 32 cycles per SIMD =
+# 4096 ops/clk/SIMD x 1024 SIMDs x 2.4 GHz = 10.07 POPS "dense-equivalent" --
+# twice the dense i8 peak (5 POPS, MI355X_MICROARCH.md), and exactly what
+# the one-hot LUT16 GEMM needs (a one-hot row is 2:4 sparse, so the sparse
+# instruction computes the whole dense product).
+SMFMAC_PEAK_TOPS = 2 * 32 * 32 * 64 / 32 * 1024 * 2.4e9 / 1e12
+DENSE_I8_PEAK_TOPS = 5000.0
+
+
+def scan_roofline(code_bytes, scan_ms, timings, num_blocks):
+    """roofline of the LUT16 scan kernel.  Unit of work = one (query, leaf)
+    visit; SURVEY §8d's algorithmic bytes 16*B*ceil(n/32) per unit; as a
+    one-hot int8 GEMM a unit is 32*ceil(n/32) datapoints x B blocks x 16
+    centers x 2 ops = 64 ops per code byte.
+    `frac` is against the ceiling of the instruction the kernel issues; the
+    executed-instruction view (`smfmac_pipe_frac`: executed smfmac x 32
+    cycles / (1024 SIMDs x 2.4 GHz x time)) also counts the padded query
+    slots and K steps the kernel runs."""
+    ops = 64.0 * code_bytes
+    sec = scan_ms * 1e-3
+    achieved = ops / sec / 1e12
+    k = scan_k(num_blocks)
+    smfmac = float(timings.get("scan_item_tiles", 0.0)) * (k // 2)
+    return {
+        "bound": "mfma", "achieved": round(achieved, 1), "peak": round(SMFMAC_PEAK_TOPS, 1),
+        "unit": "TOP/s", "frac": round(achieved / SMFMAC_PEAK_TOPS, 4),
+        "peak_basis": "v_smfmac_i32_32x32x64_i8 (2:4 sparse i8 MFMA: K=64 in the 32 cycles of "
+                      "the dense K=32 form) = 10.07 POPS dense-equivalent; the one-hot LUT16 "
+                      "rows are exactly 2:4 sparse",
+        "frac_vs_dense_i8_peak": round(achieved / DENSE_I8_PEAK_TOPS, 4),
+        "kernel": f"lut16_scan_kernel<{k}> (main pass)",
+        "avg_launch_ms_source": "HIP events around every scan launch, profiled replay of the "
+                                "timed steps",
+        "op_type": "int8 ops (TOP/s) of the one-hot LUT16 GEMM formulation",
+        "algorithmic_ops_per_launch": ops,
+        "algorithmic_code_bytes_per_launch": code_bytes,
+        "avg_launch_ms": round(scan_ms, 5),
+        "smfmac_executed_per_launch": smfmac,
+        "smfmac_pipe_frac": round(smfmac * 32.0 / (1024 * 2.4e9 * sec), 4) if smfmac else None,
+        # SURVEY §8d's byte roofline: algorithmic code bytes / time; above the
+        # 8 TB/s HBM peak by design (the query tiles of a leaf re-read its
+        # codes from L2), hence the MFMA bound
+        "code_GBps_algorithmic": round(code_bytes / sec / 1e9, 1),
+        # secondary (SURVEY §8d): LUT16 lookups per second; 16*B bytes hold
+        # 32 datapoints x B codes -> 2 lookups per byte
+        "lookups_per_s": round(2.0 * code_bytes / sec, 1),
+    }
+
+
 def cpu_info():
     """CPU model and SIMD ISA of the host (lscpu's fields, from /proc/cpuinfo)."""
     model, flags = "unknown", set()
@@ -189,21 +240,30 @@ def cpu_baseline(ix, q, gpu_idx, threads):
     out = port.search(q, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True, threads)
     per_batch = time.perf_counter() - t
     reps = max(1, int(np.ceil(2.0 / max(per_batch, 1e-3))))
-    runs, scan_runs, front_runs = [], [], []
     _, aff = host_threads()
-    for _ in range(5):
-        t_total, scan_s, front_s = 0.0, 0.0, 0.0
-        for _ in range(reps):
-            t = time.perf_counter()
-            out = port.search(q, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True, threads)
-            t_total += time.perf_counter() - t
-            scan_s += port.last_phase_s["scan"]
-            front_s += port.last_phase_s["front"]
-        nqs = reps * q.shape[0]
-        runs.append(nqs / t_total)
-        # a phase's CPU seconds spread over the cores
-        scan_runs.append(nqs * threads / max(scan_s, 1e-9))
-        front_runs.append(nqs * threads / max(front_s, 1e-9))
+
+    def timed_runs(n_runs, shared):
+        runs, scan_runs, front_runs, res = [], [], [], None
+        for _ in range(n_runs):
+            t_total, scan_s, front_s = 0.0, 0.0, 0.0
+            for _ in range(reps):
+                t = time.perf_counter()
+                res = port.search(q, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True, threads,
+                                  batch_shared=shared)
+                t_total += time.perf_counter() - t
+                scan_s += port.last_phase_s["scan"]
+                front_s += port.last_phase_s["front"]
+            nqs = reps * q.shape[0]
+            runs.append(nqs / t_total)
+            # a phase's CPU seconds spread over the cores
+            scan_runs.append(nqs * threads / max(scan_s, 1e-9))
+            front_runs.append(nqs * threads / max(front_s, 1e-9))
+        return runs, scan_runs, front_runs, res
+
+    # the reference's bottom loop (codes shared by a batch's <= 3 queries,
+    # kSmart prefetch) is the baseline; the round-2 per-query loop beside it
+    runs, scan_runs, front_runs, out = timed_runs(5, True)
+    _, scan_runs_pq, _, _ = timed_runs(3, False)
     # the port replays the reference's emulate semantics; the GPU computes the
     # ideal exact top-k', so this is the emulate-vs-GPU id mismatch
     mismatch = float((out[0] != gpu_idx).mean())
@@ -212,16 +272,21 @@ def cpu_baseline(ix, q, gpu_idx, threads):
                 affinity_cores=aff, kind="port", cpu_model=model, isa=isa,
                 runs_qps=[round(x, 1) for x in runs],
                 scan_only_qps=round(float(np.median(scan_runs)), 1),
+                scan_only_qps_per_query_loop=round(float(np.median(scan_runs_pq)), 1),
                 front_only_qps=round(float(np.median(front_runs)), 1),
                 sample=f"median of 5 runs x {reps} repeats of the same {q.shape[0]}-query batch "
                        f"through the AVX2 port of the reference's batched tree-AH path "
                        f"({pipeline}; oracle/lut16_avx2_port.cc: SearchBatchedParallel chunking, "
-                       f"pshufb LUT16 with int16 accumulation, emulate-mode FastTopNeighbors, "
+                       f"the reference's Avx2LUT16BottomLoop (pshufb LUT16 with the codes of a "
+                       f"32-datapoint group shared by the <= 3 queries of a batch, tag-along "
+                       f"int16 accumulation, kSmart next-partition prefetch), emulate-mode "
+                       f"FastTopNeighbors, "
                        f"partition scores "
                        f"8 centers per AVX2 vector in the many-to-many order), {threads} threads "
                        f"= every core this process may use ({aff} in its affinity mask, capped "
                        f"by the cgroup CPU quota); scan_only_qps = the leaf scan phase alone "
-                       f"(its CPU seconds / cores)",
+                       f"(its CPU seconds / cores); scan_only_qps_per_query_loop = the same "
+                       f"with one group pass per query (the round-2 port)",
                 id_mismatch_vs_gpu=mismatch)
 
 
@@ -364,15 +429,7 @@ def main():
 
     avg_scan_ms = float(np.mean(scan_ms))
     bytes_per_launch = float(np.mean(scan_bytes))
-    # The scan runs LUT16 as an int8 GEMM on MFMA: per (query, leaf) unit,
-    # 32*ceil(n/32) datapoints x B blocks x 16 one-hot centers, 2 ops each =
-    # 1024*B*ceil(n/32) = 64 x the unit's 16*B*ceil(n/32) code bytes (SURVEY
-    # §8d).  Its ceiling is the dense i8 MFMA peak, not HBM: the codes of a
-    # leaf are read once from HBM and re-read from L2 by its ~3 query tiles
-    # (see `traffic`, the measured HBM bytes per launch).
-    ops_per_launch = 64.0 * bytes_per_launch
-    achieved = ops_per_launch / (avg_scan_ms * 1e-3) / 1e12
-    peak = 5000.0   # dense i8 MFMA (2x the 2.5 PF bf16 dense peak), MI355X_MICROARCH.md
+    roof = scan_roofline(bytes_per_launch, avg_scan_ms, t_last, ix.num_blocks)
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "scan_traffic.json")
     if os.path.exists(tpath) and args.config == "glove":   # measured on the glove workload
@@ -404,25 +461,9 @@ def main():
                 "final_nn": FINAL_NN, "batch": NQ, "parallelism": f"query-sharded replicas x{world}",
             },
             "recall_at_10": round(recall, 4),
-            "roofline": {
-                "bound": "mfma", "achieved": round(achieved, 1), "peak": peak,
-                "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-                "kernel": f"lut16_scan_kernel<{scan_k(ix.num_blocks)}> (main pass)",
-                "avg_launch_ms_source": "HIP events around every scan launch, profiled replay of the timed steps",
-                "op_type": "int8 MFMA ops (TOPS) of the one-hot LUT16 GEMM formulation",
-                "algorithmic_ops_per_launch": ops_per_launch,
-                "algorithmic_code_bytes_per_launch": bytes_per_launch,
-                "avg_launch_ms": round(avg_scan_ms, 5),
-                # SURVEY §8d's byte roofline: algorithmic code bytes / time.
-                # Above the 8 TB/s HBM peak by design (L2 reuse across the
-                # query tiles of a leaf), hence the MFMA bound above.
-                "code_GBps_algorithmic": round(bytes_per_launch / (avg_scan_ms * 1e-3) / 1e9, 1),
-                "hbm_GBps_measured": (round(traffic / (avg_scan_ms * 1e-3) / 1e9, 1)
-                                      if traffic else None),
-                # secondary: LUT16 lookups per second;
-                # 16*B bytes hold 32 datapoints x B codes -> 2 lookups per byte
-                "lookups_per_s": round(2.0 * bytes_per_launch / (avg_scan_ms * 1e-3), 1),
-            },
+            "roofline": dict(roof, traffic=traffic,
+                             hbm_GBps_measured=(round(traffic / (avg_scan_ms * 1e-3) / 1e9, 1)
+                                                if traffic else None)),
             "stage_ms": {k: round(v, 4) for k, v in stage.items()},
             "operating_points": points,
             "qps_at_recall_0.95": next(({"leaves_to_search": p["leaves_to_search"],
@@ -549,8 +590,7 @@ def main_generated(args, rank, world, local, dist, dev):
     recall = synthetic.recall_at_k(gidx, truth, FINAL_NN)
     avg_scan_ms = float(np.mean(scan_ms))
     bytes_per_launch = float(np.mean(scan_bytes))
-    ops = 64.0 * bytes_per_launch
-    achieved = ops / (avg_scan_ms * 1e-3) / 1e12
+    roof = scan_roofline(bytes_per_launch, avg_scan_ms, stages, ix.num_blocks)
     if rank == 0:
         result = {
             "metric": CFG["metric_name"],
@@ -573,14 +613,7 @@ def main_generated(args, rank, world, local, dist, dev):
             "merge_ms": round(merge_s * 1000.0 / args.steps, 4),
             "merge_input": (f"all-gather of {split} ranks" if world == split else
                             f"{split} copies of this rank's [nq][{k}] list"),
-            "roofline": {
-                "bound": "mfma", "achieved": round(achieved, 1), "peak": 5000.0,
-                "unit": "TFLOP/s", "frac": round(achieved / 5000.0, 4), "traffic": None,
-                "kernel": f"lut16_scan_kernel<{scan_k(ix.num_blocks)}> (main pass)",
-                "avg_launch_ms": round(avg_scan_ms, 5),
-                "algorithmic_code_bytes_per_launch": bytes_per_launch,
-                "algorithmic_ops_per_launch": ops,
-            },
+            "roofline": dict(roof, traffic=None),
             "stage_ms": {k2: round(stages[k2], 4) for k2 in
                          ("partition_ms", "invert_ms", "seed_scan_ms", "scan_ms", "select_ms",
                           "total_ms")},

@@ -64,7 +64,8 @@ def lib():
         L.orc_avx2_prepare.argtypes = [vp]
         L.orc_avx2_prepare.restype = vp
         L.orc_avx2_release.argtypes = [vp]
-        L.orc_search_avx2.argtypes = [vp, vp] + [ctypes.c_int32] * 6 + [vp, vp, vp, vp]
+        L.orc_search_avx2.argtypes = [vp, vp] + [ctypes.c_int32] * 6 + [vp, vp, vp, vp,
+                                                                         ctypes.c_int32]
         L.orc_search_avx2.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -204,7 +205,8 @@ class Avx2Port:
         if not self._h:
             raise ValueError("index not covered by the AVX2 port (residual indexes need the global top-N path)")
 
-    def search(self, queries, leaves, pre_nn, final_nn, reorder=True, nthreads=8):
+    def search(self, queries, leaves, pre_nn, final_nn, reorder=True, nthreads=8,
+               batch_shared=True):
         q = _c(queries, np.float32)
         nq = q.shape[0]
         idx = np.zeros((nq, final_nn), np.uint32)
@@ -213,7 +215,7 @@ class Avx2Port:
         ph = np.zeros(3, np.float64)
         rc = lib().orc_search_avx2(self._h, q.ctypes.data, nq, leaves, pre_nn, final_nn,
                                    int(reorder), nthreads, idx.ctypes.data, dist.ctypes.data,
-                                   cnt.ctypes.data, ph.ctypes.data)
+                                   cnt.ctypes.data, ph.ctypes.data, int(bool(batch_shared)))
         if rc != 0:
             raise RuntimeError(f"orc_search_avx2 failed ({rc})")
         # CPU seconds (summed over threads) of the last call: partition +

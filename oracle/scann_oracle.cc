@@ -1194,6 +1194,10 @@ void orc_avq_encode(const float* residuals, const float* originals, int32_t n, i
 // ---------------------------------------------------------------------------
 namespace orc_port {
 using GroupFn = void (*)(const uint8_t*, int, const uint8_t*, int16_t*);
+// <= 3 queries' accumulators of one group at once (the reference's
+// Avx2LUT16BottomLoop): group, blocks, luts, count, out, prefetch pointer
+using BatchFn = void (*)(const uint8_t*, int, const uint8_t* const*, int, int16_t (*)[32],
+                         const uint8_t*);
 using MaskFn = uint32_t (*)(const int16_t*, int16_t);
 // Partition scores of one query against the transposed centers ct[dim][nlp]
 // (nlp = nl rounded up to 8), the same per-center FMA chain as
@@ -1248,7 +1252,7 @@ void Release(void* p) { delete static_cast<Prepared*>(p); }
 int Run(void* prepared, const float* queries, int nq, int leaves, int pre_nn,
         int final_nn, int do_reorder, int nthreads, uint32_t* out_idx,
         float* out_dist, int32_t* out_count, GroupFn group_fn, MaskFn mask_fn,
-        PartFn part_fn, double* phase_s) {
+        PartFn part_fn, double* phase_s, BatchFn batch_fn) {
   auto* P = static_cast<Prepared*>(prepared);
   if (!P || leaves <= 0 || final_nn < 0 || nq < 0) return -1;
   const orc_index* ix = P->ix;
@@ -1301,7 +1305,7 @@ int Run(void* prepared, const float* queries, int nq, int leaves, int pre_nn,
       tops.emplace_back(size_t(kk));
     }
     const double c1 = cpu_now();
-    int16_t acc[32];
+    int16_t accs[3][32];
     if (P->pipeline_b) {
       // orc::PipelineBEmulate's pushes, leaf-major: per leaf, batches of
       // <= 3 queries share each code group load (searcher.cc:332-416).
@@ -1325,11 +1329,15 @@ int Run(void* prepared, const float* queries, int nq, int leaves, int pre_nn,
             lts.emplace_back(size_t(kk), orc::LeafInt16Epsilon(tops[j].epsilon(), luts[j].mult));
             thr[t] = lts[t].epsilon();
           }
+          const uint8_t* bl[3];
+          for (size_t t = 0; t < nbatch; ++t) bl[t] = luts[ql[bs + t].first].u8.data();
           for (uint32_t g = 0; g < groups; ++g) {
             const uint8_t* grp = packed + size_t(g) * 16 * nb;
+            if (batch_fn) batch_fn(grp, nb, bl, int(nbatch), accs, nullptr);
             for (size_t t = 0; t < nbatch; ++t) {
               const int j = ql[bs + t].first;
-              group_fn(grp, nb, luts[j].u8.data(), acc);
+              int16_t* acc = accs[t];
+              if (!batch_fn) group_fn(grp, nb, luts[j].u8.data(), acc);
               uint32_t pm = mask_fn(acc, thr[t]);
               if (!pm) continue;
               if (g == groups - 1) pm &= fmask;
@@ -1360,6 +1368,21 @@ int Run(void* prepared, const float* queries, int nq, int leaves, int pre_nn,
         }
       }
     }
+    // the packed bytes of the leaf visited after `leaf` (with queries), for
+    // the prefetch of its first groups
+    std::vector<int> next_visit(nl, -1);
+    {
+      int nxt = -1;
+      for (int i = nl - 1; i >= 0; --i) {
+        const int l = P->leaf_order[i];
+        next_visit[l] = nxt;
+        if (!by_leaf[l].empty() && ix->leaf_offsets[l + 1] > ix->leaf_offsets[l]) nxt = l;
+      }
+    }
+    auto next_packed = [&](int leaf) -> const uint8_t* {
+      const int l = next_visit[leaf];
+      return l < 0 ? nullptr : P->packed[l].data();
+    };
     for (int leaf : P->leaf_order) {
       if (P->pipeline_b) break;
       const auto& ql = by_leaf[leaf];
@@ -1379,12 +1402,23 @@ int Run(void* prepared, const float* queries, int nq, int leaves, int pre_nn,
           thr[t] = int16_t(orc::Int16Threshold(tops[e.first].epsilon(), e.second,
                                                luts[e.first].mult));
         }
-        for (uint32_t g = 0; g < groups; ++g) {
+        const uint8_t* bl[3];
+        for (size_t t = 0; t < nbatch; ++t) bl[t] = luts[ql[bs + t].first].u8.data();
+        // kSmart prefetch (ComputeSmartPrefetchIndex, lut16_avx2.inc): the
+        // last groups of this leaf prefetch the next visited leaf's first
+        // bytes, 768 bytes ahead of the stream
+        const uint8_t* next = next_packed(leaf);
+        long pf_idx = std::min(0L, long((768 / 16 + nb - 1) / nb) - long(groups));
+        for (uint32_t g = 0; g < groups; ++g, ++pf_idx) {
           const uint8_t* grp = packed + size_t(g) * 16 * nb;
+          if (batch_fn)
+            batch_fn(grp, nb, bl, int(nbatch), accs,
+                     (pf_idx >= 0 && next) ? next + size_t(pf_idx) * 16 * nb : nullptr);
           for (size_t t = 0; t < nbatch; ++t) {
             const int j = ql[bs + t].first;
             const float bias = ql[bs + t].second;
-            group_fn(grp, nb, luts[j].u8.data(), acc);
+            int16_t* acc = accs[t];
+            if (!batch_fn) group_fn(grp, nb, luts[j].u8.data(), acc);
             uint32_t pm = mask_fn(acc, thr[t]);
             if (!pm) continue;
             if (g == groups - 1) pm &= fmask;

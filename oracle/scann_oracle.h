@@ -153,7 +153,12 @@ int orc_search_avx2(void* prepared, const float* queries, int32_t nq,
                     int32_t leaves, int32_t pre_nn, int32_t final_nn,
                     int32_t do_reorder, int32_t nthreads, uint32_t* out_idx,
                     float* out_dist, int32_t* out_count,
-                    double* phase_s /* [3] CPU seconds: front, scan, tail; or NULL */);
+                    double* phase_s /* [3] CPU seconds: front, scan, tail; or NULL */,
+                    int32_t batch_shared /* 1: the reference's bottom loop, the <= 3
+                                            queries of a batch sharing each group's
+                                            code extraction, tag-along accumulation
+                                            and kSmart prefetch (lut16_avx2.inc:
+                                            17-198); 0: one group pass per query */);
 
 #ifdef __cplusplus
 }

@@ -8,9 +8,10 @@
 
 namespace smx {
 
-// Query-tile width of the LUT16 scan: one MFMA i32_32x32x32_i8 covers 32
-// datapoints x 32 queries x 2 AH blocks.
-constexpr int kQueriesPerTile = 32;
+// Query-tile width of the LUT16 scan: one wave computes 32 datapoints x 64
+// query slots per tile, two v_smfmac_i32_32x32x64_i8 (32 queries each) per
+// one-hot A operand.
+constexpr int kQueriesPerTile = 64;
 constexpr int kDpPerTile = 32;
 constexpr int kMaxBlocks = 64;           // LUT16 blocks supported (K <= 32)
 constexpr uint64_t kNoThreshold = ~0ull;

@@ -53,11 +53,15 @@ def test_ideal_matches_exact_restatement(oracle):
         assert [bits(x) for x in gd[r, :gc[r]]] == [bits(t[0]) for t in want[r]]
 
 
+@pytest.mark.parametrize("shared", [True, False])
 @pytest.mark.parametrize("reorder", [True, False])
-def test_avx2_port_equals_emulate(oracle, small_dot, reorder):
+def test_avx2_port_equals_emulate(oracle, small_dot, reorder, shared):
+    """Both loop forms of the port (the reference's bottom loop with the
+    codes shared by a batch's <= 3 queries, and one pass per query) replay
+    the emulate semantics bit for bit."""
     ix, db, q = small_dot
     port = oracle.Avx2Port(ix)
-    pi, pd, pc = port.search(q, 12, 100, 10, reorder, 4)
+    pi, pd, pc = port.search(q, 12, 100, 10, reorder, 4, batch_shared=shared)
     ei, ed, ec = oracle.search(ix, q, 12, 100, 10, reorder, oracle.MODE_EMULATE)
     np.testing.assert_array_equal(pi, ei)
     np.testing.assert_array_equal(pd.view(np.uint32), ed.view(np.uint32))
@@ -101,8 +105,9 @@ def _pipeline_b(n=20000, leaves=64, seed=9):
     return ix, db, q
 
 
+@pytest.mark.parametrize("shared", [True, False])
 @pytest.mark.parametrize("reorder", [True, False])
-def test_avx2_port_equals_emulate_pipeline_b(oracle, reorder):
+def test_avx2_port_equals_emulate_pipeline_b(oracle, reorder, shared):
     """The port's leaf-major pipeline-B loop (per-leaf int16 top-N merged at
     visit time, tree_x_hybrid_smmd.cc:718-790) equals the oracle's per-query
     replay bit for bit (64 queries x 12 leaves >= 64 leaves: the reference's
@@ -110,7 +115,7 @@ def test_avx2_port_equals_emulate_pipeline_b(oracle, reorder):
     ix, db, q = _pipeline_b()
     port = oracle.Avx2Port(ix)
     for nthreads in (1, 4):
-        pi, pd, pc = port.search(q, 12, 100, 10, reorder, nthreads)
+        pi, pd, pc = port.search(q, 12, 100, 10, reorder, nthreads, batch_shared=shared)
         ei, ed, ec = oracle.search(ix, q, 12, 100, 10, reorder, oracle.MODE_EMULATE)
         np.testing.assert_array_equal(pi, ei)
         np.testing.assert_array_equal(pd.view(np.uint32), ed.view(np.uint32))

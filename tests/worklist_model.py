@@ -1,0 +1,157 @@
+"""A host model of the scan's work list (test infrastructure).
+
+Restates, in Python, what the device builds per call
+(scann_amd/csrc/smx_kernels.hip): PositionWork / WorklistFusedBlock (each
+leaf position's items and units, their exclusive prefixes, the 8 XCD
+groups' unit boundaries), ItemsCore (the work items and every scan
+workgroup's static share) and the scan's ListSegments walk over a share.
+`check()` asserts the invariants the scan relies on: every share's units are
+covered by real items, the shares tile each group exactly, and every tile of
+every (leaf, query tile) is scanned exactly once.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+GROUPS = 8
+
+
+def chunks_of(n, chunk_tiles):
+    tiles = (n + 31) // 32
+    return 1 if tiles == 0 else (tiles + chunk_tiles - 1) // chunk_tiles
+
+
+def chunk_tiles_range(n, chunk_tiles, ch):
+    tiles = (n + 31) // 32
+    chunks = 1 if tiles == 0 else (tiles + chunk_tiles - 1) // chunk_tiles
+    return (tiles * ch) // chunks, (tiles * (ch + 1)) // chunks
+
+
+def leaf_order(sizes):
+    """smx_searcher.hip UploadIndex: descending size, dealt to the groups in
+    a snake, each group contiguous."""
+    nl = len(sizes)
+    by_size = sorted(range(nl), key=lambda l: -sizes[l])   # stable
+    order = []
+    for g in range(GROUPS):
+        for p in range(nl):
+            r, i = divmod(p, GROUPS)
+            if (i if r % 2 == 0 else GROUPS - 1 - i) == g:
+                order.append(by_size[p])
+    return order
+
+
+def build(sizes, counts, grid, qtile, chunk_tiles):
+    nl = len(sizes)
+    order = leaf_order(sizes)
+    items_p, units_p = [], []
+    for p in range(nl):
+        leaf = order[p]
+        c, n = counts[leaf], sizes[leaf]
+        qt = (c + qtile - 1) // qtile
+        items_p.append(qt * chunks_of(n, chunk_tiles))
+        units_p.append(qt * ((n + 31) // 32))
+    ex_i = np.concatenate([[0], np.cumsum(items_p)[:-1]]).astype(int)
+    ex_u = np.concatenate([[0], np.cumsum(units_p)[:-1]]).astype(int)
+    total_w = int(sum(units_p))
+    wdiv = max(1, total_w)
+
+    def group_of(x):
+        return min(GROUPS - 1, (GROUPS * x) // wdiv)
+
+    gunits = [None] * (GROUPS + 1)
+    for p in range(nl):
+        eu = int(ex_u[p])
+        gp = group_of(eu)
+        prev = group_of(eu - units_p[p - 1]) if p > 0 else -1
+        for gg in range(prev + 1, gp + 1):
+            gunits[gg] = eu
+        if p == nl - 1:
+            for gg in range(gp + 1, GROUPS + 1):
+                gunits[gg] = total_w
+    work = [None] * int(sum(items_p))
+    wave_start = [None] * grid
+    for i in range(grid):
+        g = i & (GROUPS - 1)
+        if gunits[g + 1] == gunits[g]:
+            wave_start[i] = (0, 0, 0)
+    for p in range(nl):
+        leaf = order[p]
+        c, n = counts[leaf], sizes[leaf]
+        chunks = chunks_of(n, chunk_tiles)
+        qt = (c + qtile - 1) // qtile
+        item0 = int(ex_i[p])
+        for u in range(qt * chunks):
+            j0, j1 = chunk_tiles_range(n, chunk_tiles, u % chunks)
+            work[item0 + u] = (leaf, n, j0, j1, u // chunks)
+        ua, ub = int(ex_u[p]), int(ex_u[p]) + units_p[p]
+        if ua >= ub:
+            continue
+        g = group_of(ua)
+        nw = (grid - g + GROUPS - 1) // GROUPS
+        U0, span = gunits[g], gunits[g + 1] - gunits[g]
+        k = ((ua - U0) * nw + span - 1) // span
+        tiles = (n + 31) // 32
+        while k < nw:
+            us = U0 + (span * k) // nw
+            if us >= ub:
+                break
+            ue = U0 + (span * (k + 1)) // nw
+            off = us - ua
+            tq, rem = divmod(off, tiles)
+            ch = 0
+            while chunk_tiles_range(n, chunk_tiles, ch)[1] <= rem:
+                ch += 1
+            wave_start[GROUPS * k + g] = (item0 + tq * chunks + ch, rem, ue - us)
+            k += 1
+    return dict(order=order, work=work, wave_start=wave_start, gunits=gunits, total_w=total_w)
+
+
+def list_segments(wl, b, max_segs=512):
+    """The segments (item, j0, jend) of workgroup b's share, as ListSegments
+    walks it (64 lanes per step); raises if a taken item is not a real one."""
+    work = wl["work"]
+    sw, sj, su = wl["wave_start"][b]
+    segs = []
+    while su > 0:
+        ts, used_lanes = [], 0
+        excl = 0
+        for lane in range(64):
+            idx = sw + lane
+            it = work[min(idx, len(work) - 1)] if work else None
+            if idx >= len(work):
+                # the device reads a clamped item here; it must never be used
+                t = None
+            else:
+                j0 = sj if (lane == 0 and sj) else it[2]
+                t = min(it[3] - j0, su) if it[3] > j0 else 0
+            if excl >= su:
+                break
+            if t is None:
+                raise AssertionError(f"share of workgroup {b} runs past the items (item {idx})")
+            used_lanes += 1
+            if t > 0:
+                segs.append((idx, j0, j0 + min(t, su - excl)))
+            excl += t
+        sw += used_lanes
+        su -= min(su, excl)
+        sj = 0
+    return segs
+
+
+def check(sizes, counts, grid=256, qtile=64, chunk_tiles=20):
+    wl = build(sizes, counts, grid, qtile, chunk_tiles)
+    assert all(w is not None for w in wl["wave_start"]), "a workgroup's share is not written"
+    seen = {}
+    for b in range(grid):
+        for idx, j0, j1 in list_segments(wl, b):
+            for t in range(j0, j1):
+                key = (idx, t)
+                assert key not in seen, f"tile {t} of item {idx} scanned twice"
+                seen[key] = b
+    # every tile of every item exactly once
+    for idx, (leaf, n, j0, j1, qt) in enumerate(wl["work"]):
+        for t in range(j0, j1):
+            assert (idx, t) in seen, f"tile {t} of item {idx} (leaf {leaf}) never scanned"
+    assert len(seen) == wl["total_w"]
+    return wl

@@ -18,6 +18,10 @@ run_diag() {
   step "phase stamps" &&
   timeout -k 10 240 python tools/phase_stamps.py > $O/$TAG.phase.log 2>&1
 }
+if [ -n "${MB:-}" ]; then
+  step "microbench $MB"
+  timeout -k 10 120 $MB > $O/$TAG.mb.log 2>&1 || { step "microbench failed"; exit 1; }
+fi
 step "product suite" &&
 timeout -k 10 600 $PYTEST > $O/$TAG.tests.log 2>&1 &&
 step "smoke" &&
