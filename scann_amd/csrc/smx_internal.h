@@ -8,10 +8,9 @@
 
 namespace smx {
 
-// Query-tile width of the LUT16 scan: one wave computes 32 datapoints x 64
-// query slots per tile, two v_smfmac_i32_32x32x64_i8 (32 queries each) per
-// one-hot A operand.
-constexpr int kQueriesPerTile = 64;
+// Query-tile width of the LUT16 scan: one MFMA i32_32x32x32_i8 covers 32
+// datapoints x 32 queries x 2 AH blocks.
+constexpr int kQueriesPerTile = 32;
 constexpr int kDpPerTile = 32;
 constexpr int kMaxBlocks = 64;           // LUT16 blocks supported (K <= 32)
 constexpr uint64_t kNoThreshold = ~0ull;
@@ -86,7 +85,7 @@ struct Bounds {
   uint32_t grid = 0;        // scan workgroups (wave_start entries)
   uint32_t nl = 0;          // leaves
   uint32_t datapoints = 0;  // dataset rows
-  uint32_t pad = 0;
+  uint32_t recs = 0;        // slot records (lanes / leaf slots)
   uint64_t members = 0;     // leaf members (members[], member_rows)
   uint64_t tiles = 0;       // code tiles
 };
@@ -113,6 +112,18 @@ struct ItemLane {
   int32_t amax;   // the slot's sum limit (pair scatter, after the seed)
 };
 constexpr uint32_t kNoQuery = 0xFFFFFFFFu;     // ItemLane::qid of an empty slot
+
+// One leaf position of the work order (the fused front end's work list: the
+// scan derives its work items from these instead of a materialized list):
+// the position's first work item, its leaf, size, pair count and layout.
+struct PosDesc {
+  uint32_t item0;
+  uint32_t leaf;
+  uint32_t n;
+  uint32_t cnt;
+  uint64_t tile_off;
+  uint64_t member_off;
+};
 constexpr int32_t kNoSum = -2147483647 - 1;   // the sum limit of an empty slot
 
 struct ScanArgs {
@@ -120,9 +131,14 @@ struct ScanArgs {
   const uint32_t* members;
   const int8_t* lut;          // [nq][2K][16]
   const float* inv;           // [nq]
-  const WorkItem* work;       // [work items]
-  const ItemLane* lanes;      // [work items][32]
-  const uint4* wave_start;    // [grid] {first item, first tile, tiles, 0}
+  const WorkItem* work;       // [work items] (materialized list; null with pos)
+  const ItemLane* lanes;      // [work items][32] or [nl][slot_stride] (leaf slots, with pos)
+  const PosDesc* pos;         // [nl] fused front end: items derived from the positions
+  const uint32_t* pos_unit0;  // [nl + 1] (with pos) each position's first unit
+  const uint32_t* gunits;     // [9] (with pos) the XCD groups' unit boundaries
+  uint32_t slot_stride;       // leaf slots per leaf (with pos)
+  uint32_t chunk_tiles;
+  const uint4* wave_start;    // [grid] {first item, first tile, tiles, first position}
   uint32_t num_items;
   const uint64_t* tau_key;    // [nq] emission threshold keys
   uint64_t* cand;             // [nq][cap]
@@ -145,6 +161,8 @@ struct SeedArgs {
   const uint32_t* rank;       // [nq][L] position inside the leaf's list
   const uint32_t* leaf_item0; // [nl] the leaf's first work item
   ItemLane* lanes;            // [work items][32]
+  ItemLane* leaf_slots;       // fused front end: [nl][slot_stride], slot = rank
+  uint32_t slot_stride;
   uint32_t chunk_tiles;
   const int8_t* lut;          // [nq][2K][16]
   const float* inv;
@@ -180,6 +198,8 @@ struct WorklistArgs {
   WorkItem* work;
   ItemLane* lanes;
   uint4* wave_start;           // [grid]
+  PosDesc* pos;                // [nl] (fused front end)
+  uint32_t* done;              // top-L blocks finished (fused front end; zeroed per call)
   Bounds bd;                  // debug-build index checks
 };
 // Up to this many leaves the work list is built by one extra block of the
@@ -283,7 +303,15 @@ struct FrontArgs {
 hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int nq,
                                int L, int32_t* out_leaf, float* out_dist,
                                float* scores /*[nq][nl] scratch*/, hipStream_t s,
-                               const FrontArgs* front = nullptr);
+                               const FrontArgs* front = nullptr,
+                               const SeedArgs* seed = nullptr, const WorklistArgs* wl = nullptr,
+                               bool* fused = nullptr);
+// (With `seed` and `wl`: when the index's top-L runs in one 256-thread block
+// per query (nl <= 2048, L <= 512), the same launch (topl_seed_kernel) also
+// computes each query's seed threshold, writes its pairs' records into the
+// leaf slots (seed->leaf_slots) and, in the block that finishes last, the
+// positions and scan shares of the work list (wl->pos, wl->wave_start,
+// totals); *fused is set and the scan reads those directly.)
 hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq,
                           int8_t* lut, float* mult, float* inv, uint8_t* lut_u8,
                           hipStream_t s);

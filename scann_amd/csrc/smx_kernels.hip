@@ -485,9 +485,9 @@ constexpr int kBlockTopCand = 1024;    // compacted keys one block orders
 constexpr uint32_t kTopNarrow = 256;   // histogram rounds until this many keys
 
 template <int VPT, int NT>
-__global__ void __launch_bounds__(NT) topl_block_kernel(const float* __restrict__ scores, int nl,
-                                                        int L, int32_t* __restrict__ out_leaf,
-                                                        float* __restrict__ out_dist, TopLTail tail) {
+__device__ __forceinline__ void TopLBlock(const float* __restrict__ scores, int nl, int L,
+                                          int32_t* __restrict__ out_leaf,
+                                          float* __restrict__ out_dist, const TopLTail& tail) {
   constexpr int NWV = NT / 64;
   __shared__ uint32_t hist[256];
   __shared__ uint64_t sel[kBlockTopCand];
@@ -645,6 +645,13 @@ __global__ void __launch_bounds__(NT) topl_block_kernel(const float* __restrict_
   SMX_PHASE(0, qi, 4);
   if (tail.lut.lut) BuildLut(qi, tail.lut);
   SMX_PHASE(0, qi, 5);
+}
+
+template <int VPT, int NT>
+__global__ void __launch_bounds__(NT) topl_block_kernel(const float* __restrict__ scores, int nl,
+                                                        int L, int32_t* __restrict__ out_leaf,
+                                                        float* __restrict__ out_dist, TopLTail tail) {
+  TopLBlock<VPT, NT>(scores, nl, L, out_leaf, out_dist, tail);
 }
 
 __global__ void __launch_bounds__(256) topl_select_kernel(const float* __restrict__ scores, int nl,
@@ -921,6 +928,37 @@ __global__ void __launch_bounds__(256) worklist_kernel(
   }
 }
 
+// The scan workgroups whose share starts in position p's units [ua, ub)
+// (leaf size n, first item item0): workgroup i of group g (i % 8 == g) takes
+// the units [U0 + span * k / nw, U0 + span * (k + 1) / nw) of its group, k =
+// i / 8 of the group's nw; its start {item, first tile, units, position}.
+// Threads first, first + step, ... of the caller take the k in turn.
+__device__ void WaveStarts(const WorklistArgs& w, int p, const uint32_t* gunits, uint32_t item0,
+                           uint32_t ua, uint32_t ub, uint32_t n, uint32_t first, uint32_t step) {
+  if (ua >= ub) return;
+  const uint32_t chunk_tiles = w.chunk_tiles;
+  const uint32_t chunks = LeafChunks(n, chunk_tiles);
+  const uint32_t wdiv = max(1u, gunits[kGroups]);
+  const int g = int(min<uint64_t>(kGroups - 1, (uint64_t(kGroups) * ua) / wdiv));
+  const uint32_t nw = uint32_t(w.grid - g + kGroups - 1) / kGroups;
+  const uint32_t U0 = gunits[g], span = gunits[g + 1] - U0;
+  // the first k with U0 + span*k/nw >= ua
+  uint32_t k = uint32_t((uint64_t(ua - U0) * nw + span - 1) / span);
+  const uint32_t tiles = (n + 31u) / 32u;
+  for (k += first;; k += step) {
+    if (k >= nw) break;
+    const uint32_t us = U0 + uint32_t((uint64_t(span) * k) / nw);
+    if (us >= ub) break;
+    const uint32_t ue = U0 + uint32_t((uint64_t(span) * (k + 1)) / nw);
+    const uint32_t off = us - ua, tq = off / tiles, rem = off % tiles;
+    uint32_t ch = 0;
+    while (ChunkTiles(n, chunk_tiles, ch).y <= rem) ++ch;
+    SMX_CHECK(item0 + tq * chunks + ch, w.bd.items, "wave start item");
+    SMX_GUARD(kGroups * k + g, w.bd.grid, "wave start")
+    w.wave_start[kGroups * k + g] = make_uint4(item0 + tq * chunks + ch, rem, ue - us, uint32_t(p));
+  }
+}
+
 // Phase 2 (64 lanes per leaf position): the leaf's work items, the empty
 // query slots of its last query tile, and the start of every scan wave whose
 // share begins inside this leaf.  Wave i of group g (i % 8 == g) takes the
@@ -958,7 +996,7 @@ __device__ void ItemsCore(const WorklistArgs& w, int p, int lane, const uint32_t
     SMX_GUARD(item0 + u, w.bd.items, "work item") w.work[item0 + u] = it;
   }
   if (qt) {
-    const uint32_t first = c - (qt - 1) * kQueriesPerTile;   // empty slots [first, 64)
+    const uint32_t first = c - (qt - 1) * kQueriesPerTile;   // empty slots [first, 32)
     const uint32_t ne = kQueriesPerTile - first;
     for (uint32_t e = lane; e < ne * chunks; e += 64) {
       ItemLane v;
@@ -970,27 +1008,7 @@ __device__ void ItemsCore(const WorklistArgs& w, int p, int lane, const uint32_t
       w.lanes[size_t(item0 + (qt - 1) * chunks + e / ne) * kQueriesPerTile + first + e % ne] = v;
     }
   }
-  // the waves whose share starts in this leaf's units [ua, ub)
-  if (ua >= ub) return;
-  const uint32_t wdiv = max(1u, gunits[kGroups]);
-  const int g = int(min<uint64_t>(kGroups - 1, (uint64_t(kGroups) * ua) / wdiv));
-  const uint32_t nw = uint32_t(w.grid - g + kGroups - 1) / kGroups;
-  const uint32_t U0 = gunits[g], span = gunits[g + 1] - U0;
-  // the first k with U0 + span*k/nw >= ua
-  uint32_t k = uint32_t((uint64_t(ua - U0) * nw + span - 1) / span);
-  const uint32_t tiles = (n + 31u) / 32u;
-  for (k += lane;; k += 64) {
-    if (k >= nw) break;
-    const uint32_t us = U0 + uint32_t((uint64_t(span) * k) / nw);
-    if (us >= ub) break;
-    const uint32_t ue = U0 + uint32_t((uint64_t(span) * (k + 1)) / nw);
-    const uint32_t off = us - ua, tq = off / tiles, rem = off % tiles;
-    uint32_t ch = 0;
-    while (ChunkTiles(n, chunk_tiles, ch).y <= rem) ++ch;
-    SMX_CHECK(item0 + tq * chunks + ch, w.bd.items, "wave start item");
-    SMX_GUARD(kGroups * k + g, w.bd.grid, "wave start")
-    w.wave_start[kGroups * k + g] = make_uint4(item0 + tq * chunks + ch, rem, ue - us, 0);
-  }
+  WaveStarts(w, p, gunits, item0, ua, ub, n, uint32_t(lane), 64u);
 }
 
 __global__ void __launch_bounds__(64) items_kernel(WorklistArgs w) {
@@ -1392,8 +1410,8 @@ __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a, WorklistArgs 
 // (tree_ah_hybrid_residual.cc:610-622), with the slot's sum limit from the
 // query's seed threshold.  One thread per pair; runs after the seed pass and
 // the work list.
-__global__ void __launch_bounds__(256) pair_scatter_kernel(SeedArgs a, int nq) {
-  const size_t p = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void PairScatter(const SeedArgs& a, size_t p, int nq,
+                                            const uint32_t* __restrict__ leaf_item0) {
   if (p >= size_t(nq) * a.L) return;
   const int32_t leaf = a.topl_leaf[p];
   if (leaf < 0) return;
@@ -1413,50 +1431,202 @@ __global__ void __launch_bounds__(256) pair_scatter_kernel(SeedArgs a, int nq) {
                                : SumLimit(FromOrdered(uint32_t(tau >> 32)), v.inv, v.bias,
                                           -128 * a.nb, 128 * a.nb);
   SMX_CHECK(leaf, a.bd.nl, "pair leaf");
-  const uint32_t w0 = a.leaf_item0[leaf] + (r / kQueriesPerTile) * chunks;
+  const uint32_t w0 = leaf_item0[leaf] + (r / kQueriesPerTile) * chunks;
   for (uint32_t ch = 0; ch < chunks; ++ch) {
     SMX_GUARD(w0 + ch, a.bd.items, "pair lane")
     a.lanes[size_t(w0 + ch) * kQueriesPerTile + (r % kQueriesPerTile)] = v;
   }
 }
 
+__global__ void __launch_bounds__(256) pair_scatter_kernel(SeedArgs a, int nq) {
+  PairScatter(a, size_t(blockIdx.x) * blockDim.x + threadIdx.x, nq, a.leaf_item0);
+}
 
-// ---------------------------------------------------------------------------
-// One sparse MFMA step of a tile: acc += A(codes) x B on
-// v_smfmac_i32_32x32x64_i8, the 2:4 structured-sparse i8 MFMA (K = 64 at the
-// cycles of the dense K = 32 form, tools/smfmac_chain.hip).  A one-hot row
-// is exactly 2:4 sparse -- at most one non-zero in every group of 4 centers
-// -- so the sparse instruction computes the whole dense product.  Operand
-// layout (tools/smfmac_probe2/3): lane (r, hA) of A holds 16 compressed
-// values, j < 8 for B lanes (c, 0) and j >= 8 for B lanes (c, 1), two per
-// group of 4, value j selecting B byte 16*hA + 4*((j % 8) / 2) + idx_j
-// (idx_j = bits [2j, 2j+2) of the index VGPR).  Step s covers blocks
-// 4s + 2*hB + hA: lane (r, hA) needs the codes of blocks 4s + hA and 4s + 2
-// + hA = nibbles 2s and 2s + 1 of its stream (code byte s, EncodeCodePair),
-// and B lane (c, hB) the LUT rows 4s + 2hB and 4s + 2hB + 1 (32 contiguous
-// bytes).  Per step two conflict-free LDS reads (16-entry tables spanning
-// distinct banks; equal entries broadcast): the compressed values from the
-// byte's group nibble (a 1 at value 2*(x0 >> 2) and 8 + 2*(x1 >> 2)) and the
-// index word from its position nibble (x0 & 3 in fields 0..7, x1 & 3 in
-// fields 8..15).
-//
-// The instruction is an asm statement so that its B operand can be an AGPR:
-// a wave holds the B fragments of 64 query slots (two 32-query halves that
-// share every A operand, 2 x K/2 x v8i = 208 registers at K = 26), which
-// only fit in the accumulator half of the register file.  hipcc neither
-// knows the statement is an XDL op nor pads it (cdna_hip_programming.md
-// §5.7): the accumulator is zeroed by VALU moves followed by the 2 wait
-// states an MFMA operand read needs (ZeroAcc), every other reader of the
-// result sits behind XdlReadPad (>= 18 states for a 16-pass XDL write), and
-// tools/audit_isa.py checks the compiled kernels for both.
-// ---------------------------------------------------------------------------
-#define SMX_SMFMAC(acc, a, b, ix) \
-  asm volatile("v_smfmac_i32_32x32x64_i8 %0, %1, %2, %3" : "+v"(acc) : "v"(a), "a"(b), "v"(ix))
+// The fused front end's work list, built by the one block of the top-L launch
+// that finishes last (every leaf's pair count is final then): per position in
+// work order its first item and units (the exclusive prefixes of
+// WorklistFusedBlock), the PosDesc the scan derives its items from, the 8 XCD
+// groups' unit boundaries and the totals.  No item, lane record or share
+// start is written: each scan workgroup finds its share's start
+// (ShareStart) and computes its items' (leaf, query tile, chunk) from the
+// positions, and reads their records from the leaf slots.  256 threads, nl <=
+// 2048 (FusedFrontShape).
+constexpr int kPosPerThread = 8;   // BuildPositions: nl <= 2048 (FusedFrontShape)
 
-__device__ __forceinline__ void ZeroAcc(v16i& acc) {
-  // 8 x v_mov_b64 (a plain v16i{0} became 16 v_mov_b32 plus register-
-  // shifting copies), then the 2 states a VALU write needs before an MFMA
-  // reads the register
+__device__ void BuildPositions(const WorklistArgs& w) {
+  __shared__ uint32_t wsum[4], s_gunits[kGroups + 1], s_last_un[256];
+  __shared__ unsigned long long red[4][2];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nl = w.nl, p0 = tid * kPosPerThread;
+  uint32_t leafv[kPosPerThread], cv[kPosPerThread], nv[kPosPerThread];
+#pragma unroll
+  for (int k = 0; k < kPosPerThread; ++k) leafv[k] = p0 + k < nl ? w.order[p0 + k] : 0u;
+#pragma unroll
+  for (int k = 0; k < kPosPerThread; ++k) {
+    cv[k] = nv[k] = 0;
+    if (p0 + k < nl) {
+      // the count as the atomic unit holds it (every block's rank atomics
+      // have returned before it counted itself done)
+      cv[k] = atomicAdd(const_cast<uint32_t*>(&w.cnt[size_t(leafv[k]) * kCounterStride]), 0u);
+      nv[k] = w.leaf_size[leafv[k]];
+    }
+  }
+  uint32_t ti = 0, tu = 0, it, un = 0;
+  unsigned long long tp = 0, tb = 0;
+#pragma unroll
+  for (int k = 0; k < kPosPerThread; ++k) {
+    un = LeafUnits(cv[k], nv[k], w.chunk_tiles, it);
+    tp += cv[k];
+    tb += 16ull * w.nb * ((nv[k] + 31u) / 32u) * cv[k];   // algorithmic code bytes
+    ti += it;
+    tu += un;
+  }
+  s_last_un[tid] = un;
+  const uint32_t inc_i = BlockInclusiveScan256(ti, wsum);
+  __syncthreads();   // wsum is reused
+  const uint32_t inc_u = BlockInclusiveScan256(tu, wsum);
+  const uint32_t total_w = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  {
+    unsigned long long v[2] = {tp, tb};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
+      if (lane == 0) red[wid][k] = v[k];
+    }
+  }
+  __syncthreads();   // s_last_un, red
+  if (tid == 255) {
+    w.totals[0] = uint32_t(red[0][0] + red[1][0] + red[2][0] + red[3][0]);
+    w.totals[1] = inc_i;
+    w.totals[2] = total_w;
+    w.code_bytes[0] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+  }
+  const uint64_t wdiv = max(1u, total_w);
+  auto group_of = [&](uint32_t excl_w) {
+    return int(min<uint64_t>(kGroups - 1, (uint64_t(kGroups) * excl_w) / wdiv));
+  };
+  uint32_t ei = inc_i - ti, eu = inc_u - tu;
+  uint32_t prev_un = tid > 0 ? s_last_un[tid - 1] : 0u;
+#pragma unroll
+  for (int k = 0; k < kPosPerThread; ++k) {
+    const int p = p0 + k;
+    un = LeafUnits(cv[k], nv[k], w.chunk_tiles, it);
+    if (p < nl) {
+      PosDesc d;
+      d.item0 = ei;
+      d.leaf = leafv[k];
+      d.n = nv[k];
+      d.cnt = cv[k];
+      d.tile_off = w.tile_off[leafv[k]];
+      d.member_off = w.member_off[leafv[k]];
+      w.pos[p] = d;
+      w.pos_unit0[p] = eu;
+      const int gp = group_of(eu);
+      const int prev = p > 0 ? group_of(eu - prev_un) : -1;
+      for (int gg = prev + 1; gg <= gp; ++gg) s_gunits[gg] = eu;
+      if (p == nl - 1) {
+        for (int gg = gp + 1; gg <= kGroups; ++gg) s_gunits[gg] = total_w;
+        w.pos_unit0[nl] = total_w;
+      }
+    }
+    ei += it;
+    eu += un;
+    prev_un = un;
+  }
+  __syncthreads();   // s_gunits
+  if (tid <= kGroups) w.gunits[tid] = s_gunits[tid];
+}
+
+// Partition top-L (TopLBlock: the leaves, their ranks in the leaves' lists
+// and the query's LUT) and the query's seed threshold (SeedTau) in one block
+// per query: the seed reads only this query's LUT, leaves and distances,
+// which this block has just written (visible to the block after a barrier).
+// With leaf slots (the fused front end), each pair's record {query, bias,
+// 1/multiplier, sum limit} goes to slot `rank` of its leaf, and the block
+// that finishes last builds the work list's positions (BuildPositions):
+// every block releases its rank atomics (device-scope fence) before counting
+// itself done, and the last one acquires before reading the counts.
+template <int VPT, int K>
+__global__ void __launch_bounds__(256, 4) topl_seed_kernel(const float* __restrict__ scores, int nl,
+                                                        int L, int32_t* __restrict__ out_leaf,
+                                                        float* __restrict__ out_dist,
+                                                        TopLTail tail, SeedArgs sa, WorklistArgs wl) {
+  __shared__ uint32_t s_last;
+  const int qi = int(blockIdx.x);
+  TopLBlock<VPT, 256>(scores, nl, L, out_leaf, out_dist, tail);
+  __syncthreads();
+  const uint64_t T = SeedTau<K>(sa, qi);
+  if (threadIdx.x == 0) sa.tau_key[qi] = T;
+  if (!sa.leaf_slots) return;   // block-uniform
+  {
+    const float inv = sa.inv[qi];
+    const float td = T == kNoThreshold ? 0.0f : FromOrdered(uint32_t(T >> 32));
+    for (int i = threadIdx.x; i < L; i += 256) {
+      const int32_t leaf = out_leaf[size_t(qi) * L + i];
+      if (leaf < 0) continue;
+      const uint32_t r = tail.rank[size_t(qi) * L + i];
+      ItemLane v;
+      v.qid = uint32_t(qi);
+      v.bias = sa.residual ? out_dist[size_t(qi) * L + i] : 0.0f;
+      v.inv = inv;
+      // the slot's sum limit: the largest LUT16 sum whose distance can pass
+      // the query's threshold (PairScatter's)
+      v.amax = T == kNoThreshold ? 128 * sa.nb
+                                 : SumLimit(td, inv, v.bias, -128 * sa.nb, 128 * sa.nb);
+      SMX_CHECK(size_t(leaf) * sa.slot_stride + r, sa.bd.recs, "leaf slot");
+      sa.leaf_slots[size_t(leaf) * sa.slot_stride + r] = v;
+    }
+  }
+  // The last block to finish builds the work list.  It needs only the pair
+  // counts, which every block changed by returning atomics whose results it
+  // has consumed (the ranks) before this barrier, and which the last block
+  // reads back through the atomic unit: no cache write-back or invalidation
+  // (a device-scope fence per block cost ~100 us here).  The records and
+  // positions reach the scan through the kernel boundary.
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(wl.done, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!s_last) return;
+  BuildPositions(wl);
+}
+
+
+// One tile: S[dp][q] for 32 datapoints x 32 queries with the item's B
+// fragments (LUT rows) held in registers, on the 2:4 structured-sparse MFMA
+// (v_smfmac_i32_32x32x64_i8:
+// K = 64 at the cycles of the dense K = 32 form, measured by
+// tools/smfmac_probe.hip).  A one-hot row is exactly 2:4 sparse -- at most
+// one non-zero in every group of 4 centers -- so the sparse instruction
+// computes the whole dense product.  Operand layout (tools/smfmac_probe2/3):
+// lane (r, hA) of A holds 16 compressed values, j < 8 for B lanes (c, 0) and
+// j >= 8 for B lanes (c, 1), two per group of 4, value j selecting B byte
+// 16*hA + 4*((j % 8) / 2) + idx_j (idx_j = bits [2j, 2j+2) of the index
+// VGPR).  Step s covers blocks 4s + 2*hB + hA: lane (r, hA) needs the
+// codes of blocks 4s + hA and 4s + 2 + hA = nibbles 2s and 2s + 1 of its
+// stream (code byte s, EncodeCodePair), and B lane (c, hB) the LUT rows
+// 4s + 2hB and 4s + 2hB + 1 (32 contiguous bytes).  Per step two
+// conflict-free LDS reads (16-entry tables spanning distinct banks; equal
+// entries broadcast): the compressed values from the byte's group nibble
+// (a 1 at value 2*(x0 >> 2) and 8 + 2*(x1 >> 2)) and the index word from its
+// position nibble (x0 & 3 in fields 0..7, x1 & 3 in fields 8..15), each
+// address two VALU ops; a 256-entry table of both spent 60% of the LDS
+// cycles in bank conflicts.
+template <int K, int R>
+__device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)[K / 2],
+                                           const v4i* grp_tab, const int* pos_tab) {
+  constexpr int KS = K / 2;
+  auto grp = [&](int t) { return (codes[t >> 2] >> ((t & 3) * 8)) & 0xFu; };
+  auto pos = [&](int t) { return (codes[t >> 2] >> ((t & 3) * 8 + 4)) & 0xFu; };
+  v4i o[R];
+  int ix[R];
+#pragma unroll
+  for (int p = 0; p < R; ++p)
+    if (p < KS) {
+      o[p] = grp_tab[grp(p)];
+      ix[p] = pos_tab[pos(p)];
+    }
+  // zeroed as 8 x v_mov_b64 (the plain v16i{0} became 16 v_mov_b32 plus a
+  // chain of 8 register-shifting v_mov_b64 copies per tile)
   typedef long long v8l __attribute__((ext_vector_type(8)));
   v8l z;
 #pragma unroll
@@ -1465,31 +1635,32 @@ __device__ __forceinline__ void ZeroAcc(v16i& acc) {
     asm volatile("v_mov_b64 %0, 0" : "=v"(t));
     z[k] = t;
   }
-  acc = __builtin_bit_cast(v16i, z);
-  asm volatile("s_nop 1" : "+v"(acc));
-}
-
-// the wait states between the last smfmac writing a / b and any other reader
-__device__ __forceinline__ void XdlReadPad(v16i& a, v16i& b) {
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 2" : "+v"(a), "+v"(b));
-}
-
-__device__ __forceinline__ int Min16(const v16i& a) {
-  int m = min(min(a[0], a[1]), a[2]);
+  v16i acc = __builtin_bit_cast(v16i, z);
 #pragma unroll
-  for (int i = 3; i < 15; i += 2) m = min(min(m, a[i]), a[i + 1]);
-  return min(m, a[15]);
+  for (int s = 0; s < KS; ++s) {
+    acc = __builtin_amdgcn_smfmac_i32_32x32x64_i8(o[s % R], b[s], acc, ix[s % R], 0, 0);
+    if (s + R < KS) {
+      o[s % R] = grp_tab[grp(s + R)];
+      ix[s % R] = pos_tab[pos(s + R)];
+    }
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, 2 * R, 0);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if (s == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    if (s + R < KS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+  }
+  return acc;
 }
 
 // ---------------------------------------------------------------------------
-// The scan kernel: one 256-thread workgroup per CU, one wave per SIMD (the
-// B fragments of 64 query slots fill the AGPRs; the VALU and LDS work of one
-// one-hot lookup is shared by two MFMAs), the CU's waves sharing a static
-// share of the work and balancing it among themselves through LDS atomics
-// (a returning device-scope atomic costs microseconds under this load; an
-// LDS atomic ~100 cycles).
+// The scan kernel: one workgroup of kScanWaves waves per CU (3 per SIMD), the
+// CU's waves sharing a static share of the work and balancing it among
+// themselves through LDS atomics (a returning device-scope atomic costs
+// microseconds under this load; an LDS atomic ~100 cycles).
 //
-// Work items (leaf, 64-query tile of that leaf, chunk of tiles) are listed in
+// Work items (leaf, 32-query tile of that leaf, chunk of tiles) are listed in
 // 8 groups of consecutive leaves with equal MFMA work, one per XCD group
 // (blockIdx % 8 share an XCD under the observed round-robin placement; speed
 // only, never correctness), so a leaf's query tiles run on one XCD and re-read
@@ -1497,41 +1668,45 @@ __device__ __forceinline__ int Min16(const v16i& a) {
 // tiles into equal contiguous shares, one per workgroup (wave_start); a share
 // may begin and end inside an item.  Wave 0 lists the share's segments (item,
 // tile range) in LDS; each wave claims a segment, loads its B fragments once
-// and takes the segment's tiles one at a time from the segment's LDS counter
-// (one tile claimed ahead); a wave with no unclaimed segment left joins the
+// and takes the segment's tiles two at a time from the segment's LDS counter
+// (one pair claimed ahead); a wave with no unclaimed segment left joins the
 // segment with the most tiles left.  Every wave therefore works until the
 // CU's share is done, whatever its tiles' hit rates and setup costs.
 //
-// Per segment: lane (c, h) takes the records of query slots c and 32 + c
-// (query, sum limit, bias, 1/multiplier; written by the pair scatter) and
-// loads the int8 LUT rows of both queries (the B fragments, AGPRs, for the
-// whole segment; an empty slot loads query 0's rows and never passes its
-// sum limit).  Per tile: K/2 steps of one lookup + two smfmac give S[dp][q] = sum_b
-// LUT_q[b][code(dp, b)] exactly (|S| <= 127*B) for 32 datapoints x 64
-// queries.  Tiles alternate between two accumulator pairs and two code
-// buffers: tile t's test runs at step kEpiStep of tile t+1 (beside its
-// MFMAs), and the codes of tile t+2 are loaded into tile t's buffer as soon
-// as its last lookup has been issued.  A datapoint can only pass when S <=
-// amax_q (the largest sum whose distance can pass the query's threshold; d
-// is monotone in S); a lane whose 16-sum minimum passes appends its sums
-// (packed int16) and a tag to the wave's LDS hit list; drain() runs the
-// per-element test and the distance
+// Per segment: lane (c, h) takes its query slot's record (query, sum limit,
+// bias; written by the seed kernel), loads the int8 LUT rows 2s+h, s < K, of
+// query c into K registers (the MFMA B fragments); then for each tile K x MFMA
+// i32_32x32x32_i8 with A = one-hot codes (row = datapoint, 16 bytes per
+// lane-half = one block's 16 centers) gives S[dp][q] = sum_b LUT_q[b][code(dp,
+// b)] exactly (|S| <= 127*B).  A datapoint can only pass when S <= amax_q (the
+// largest sum whose distance can pass the query's threshold; d is monotone in
+// S); a lane whose 16-sum minimum passes appends its sums (packed int16) and a
+// tag to the wave's LDS hit list; drain() runs the per-element test, the
+// distance
 //     d = fl(fl(float(S) * inv_q) + bias_{q,leaf})
-// lane-parallel over the hits, and stages the segment's survivors in LDS:
-// one global atomic per query per segment reserves their list slots (issued
-// at the next segment's start, its result consumed after that segment's
-// first tile).
-// Diagnostic build only: ABL = 4 runs without the epilogue (timing
-// ablation, results invalid), ABL = 8 writes per-segment stamps.
+// and the key test (ordered(d) << 32 | tie) <= threshold key lane-parallel
+// over the hits, and stages the segment's survivors in LDS: one global atomic
+// per query per segment reserves their list slots (issued at the segment's
+// end, its result consumed after the next segment's first tile).
+// ABL = 4: timing ablation without the epilogue; ABL = 2: with the hit test
+// but no hit list; ABL = 16: with hit lists and drains but no copy to the
+// candidate lists (results invalid for all three).
 // ---------------------------------------------------------------------------
-constexpr int kHitCap = 256;       // hit list entries (a tile adds <= 128)
+
+constexpr int kHitsPerWave = 64;   // a tile adds at most one hit per lane
 constexpr int kItemKeys = 256;     // survivors one segment stages in LDS
 constexpr int kMaxSegs = 512;      // share segments listed per round
 constexpr uint32_t kStealMin = 3;  // tiles left for a second wave to join a segment
-constexpr int kScanWaves = 4;      // one per SIMD
-constexpr int kEpiStep = 3;        // the previous tile's test runs after this step
+
+// Waves per scan workgroup: 3 per SIMD (168 VGPRs) up to K = 26; 2 per SIMD
+// above (the K B-fragment registers).
+#ifndef SMX_SCAN_WAVES
+#define SMX_SCAN_WAVES 12
+#endif
+template <int K>
+constexpr int ScanWaves() { return K <= 26 ? SMX_SCAN_WAVES : 8; }
 #ifndef SMX_SCAN_R
-#define SMX_SCAN_R 2               // one-hot lookups in flight ahead of their MFMAs
+#define SMX_SCAN_R 3
 #endif
 
 // Diagnostic stamps (ABL & 8; a separate buffer that nothing else reads):
@@ -1557,7 +1732,7 @@ __device__ __forceinline__ void StampItem(const ScanArgs& a, uint32_t worker, ui
   }
 }
 
-// The query parameters of a segment's 64 slots, in LDS for the drain.
+// The query parameters of a segment's 32 slots, in LDS for the drain.
 struct QParam {
   uint32_t qid;
   int32_t amax;
@@ -1568,14 +1743,13 @@ struct QParam {
 // A wave's own LDS: hit list, survivor stage (double buffered: a segment's
 // survivors are copied to the lists during the next segment), per-slot counts.
 struct ScanWaveLds {
-  uint4 hsum[kHitCap][2];            // 16 sums as int16 pairs
-  uint32_t hmeta[kHitCap];           // tile << 7 | h << 6 | slot
+  uint4 hsum[2 * kHitsPerWave][2];   // 16 sums as int16 pairs
+  uint32_t hmeta[2 * kHitsPerWave];  // tile << 6 | lane
   uint64_t kbuf[2][kItemKeys];
   uint8_t kslot[2][kItemKeys];
   uint32_t s_kn[2];
-  uint32_t qcnt[kQueriesPerTile], q_slot[kQueriesPerTile], qrun[kQueriesPerTile],
-      prev_qid[kQueriesPerTile];
-  QParam qp[kQueriesPerTile];
+  uint32_t qcnt[32], q_slot[32], qrun[32], prev_qid[32];
+  QParam qp[32];
 };
 
 // A segment's item descriptor, kept in LDS: a segment's setup reads it from
@@ -1585,20 +1759,124 @@ struct SegDesc {
   uint64_t member_off;
   uint32_t n;
   uint32_t leaf;
+  uint32_t slot0;    // the item's first slot record (a.lanes)
+  uint32_t nslots;   // records [slot0, slot0 + nslots); the other slots are empty
 };
 
 // Wave 0 of a scan workgroup: the next segments of the share (item, first
 // tile, end tile, descriptor) into the LDS table, 64 items per step (a prefix
 // of their tiles), at most kMaxSegs; the share's remainder stays in s_sw /
 // s_su.
+// The fused front end's items come from the positions instead of a list: lane
+// l holds position sp + l's descriptor, item idx = sw + lane lies in the last
+// of those positions whose first item is <= idx (a 6-step search over the
+// lanes), and its (query tile, chunk) follow from the offset inside the
+// position (items are query-tile-major, chunk-minor, as WorklistFusedBlock
+// numbers them).  Items past the 64 positions loaded are left to the next
+// step (`valid` is a prefix of the lanes).
+// The fused front end: workgroup b's share start {item, first tile, units,
+// position}, as WaveStarts assigns it -- group g = b % 8, k = b / 8 of the
+// group's nw, units [U0 + span * k / nw, U0 + span * (k + 1) / nw) -- found
+// by one wave: the position holding the first unit is the last one whose
+// unit prefix is <= it (a 64-ary search over a.pos_unit0 in two rounds of
+// lane loads; nl <= 2048), then its query tile, tile and chunk.
+__device__ uint4 ShareStart(const ScanArgs& a, int lane) {
+  const uint32_t b = blockIdx.x, grid = gridDim.x;
+  const uint32_t g = b & (kGroups - 1), k = b / kGroups;
+  const uint32_t nw = (grid - g + kGroups - 1) / kGroups;
+  const uint32_t U0 = a.gunits[g], span = a.gunits[g + 1] - U0;
+  const uint32_t us = U0 + uint32_t((uint64_t(span) * k) / nw);
+  const uint32_t ue = U0 + uint32_t((uint64_t(span) * (k + 1)) / nw);
+  if (us >= ue) return make_uint4(0, 0, 0, 0);
+  const uint32_t nl = uint32_t(a.nl);
+  // round 1: positions 32 l; round 2: positions 32 L1 + l, l < 32
+  const uint32_t p1 = min(uint32_t(lane) * 32u, nl);
+  const uint64_t b1 = __ballot(p1 < nl && a.pos_unit0[p1] <= us);
+  const uint32_t l1 = 63u - uint32_t(__clzll(b1));   // lane 0 always qualifies
+  const uint32_t p2 = l1 * 32u + uint32_t(lane);
+  const uint64_t b2 = __ballot(lane < 32 && p2 < nl && a.pos_unit0[p2] <= us);
+  const uint32_t p = l1 * 32u + (63u - uint32_t(__clzll(b2)));
+  SMX_CHECK(p, a.bd.nl, "share position");
+  const PosDesc d = a.pos[p];
+  const uint32_t tiles = (d.n + 31u) / 32u;
+  const uint32_t off = us - a.pos_unit0[p], tq = off / tiles, rem = off % tiles;
+  const uint32_t chunks = LeafChunks(d.n, a.chunk_tiles);
+  uint32_t ch = 0;
+  while (ChunkTiles(d.n, a.chunk_tiles, ch).y <= rem) ++ch;
+  return make_uint4(d.item0 + tq * chunks + ch, rem, ue - us, p);
+}
+
+struct PosItem {
+  WorkItem it;
+  uint32_t slot0, nslots, pos;
+  bool valid;
+};
+
+__device__ __forceinline__ PosItem ItemFromPositions(const ScanArgs& a, int lane, uint32_t sp,
+                                                     uint32_t idx) {
+  PosDesc d;
+  const uint32_t p = sp + uint32_t(lane);
+  if (p < uint32_t(a.nl)) {
+    d = a.pos[p];
+  } else {
+    d.item0 = ~0u;   // never <= an item index
+    d.leaf = d.n = d.cnt = 0;
+    d.tile_off = d.member_off = 0;
+  }
+  const uint32_t chunks_l = LeafChunks(d.n, a.chunk_tiles);
+  const uint32_t qt_l = (d.cnt + kQueriesPerTile - 1) / kQueriesPerTile;
+  const uint32_t end_l = d.item0 == ~0u ? ~0u : d.item0 + qt_l * chunks_l;
+  int q = 0;
+#pragma unroll
+  for (int st = 32; st > 0; st >>= 1) {
+    const uint32_t v = uint32_t(__shfl(int(d.item0), q + st));
+    if (v <= idx) q += st;
+  }
+  PosItem r;
+  const uint32_t item0 = uint32_t(__shfl(int(d.item0), q));
+  const uint32_t end = uint32_t(__shfl(int(end_l), q));
+  r.valid = idx >= item0 && idx < end;
+  r.pos = sp + uint32_t(q);
+  r.it.leaf = uint32_t(__shfl(int(d.leaf), q));
+  r.it.n = uint32_t(__shfl(int(d.n), q));
+  const uint32_t cnt = uint32_t(__shfl(int(d.cnt), q));
+  r.it.tile_off = (uint64_t(uint32_t(__shfl(int(uint32_t(d.tile_off >> 32)), q))) << 32) |
+                  uint32_t(__shfl(int(uint32_t(d.tile_off)), q));
+  r.it.member_off = (uint64_t(uint32_t(__shfl(int(uint32_t(d.member_off >> 32)), q))) << 32) |
+                    uint32_t(__shfl(int(uint32_t(d.member_off)), q));
+  const uint32_t chunks = max(1u, LeafChunks(r.it.n, a.chunk_tiles));
+  const uint32_t u = r.valid ? idx - item0 : 0u;
+  const uint32_t tq = u / chunks;
+  const uint2 cr = ChunkTiles(r.it.n, a.chunk_tiles, u - tq * chunks);
+  r.it.j0 = cr.x;
+  r.it.jend = r.valid ? cr.y : 0u;
+  r.slot0 = r.it.leaf * a.slot_stride + tq * kQueriesPerTile;
+  r.nslots = min(uint32_t(kQueriesPerTile), cnt - min(cnt, tq * kQueriesPerTile));
+  return r;
+}
+
 __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32_t& sj,
                                              uint32_t* s_item, uint32_t* s_end, uint32_t* s_next,
                                              SegDesc* s_desc, uint32_t& s_sw, uint32_t& s_su,
-                                             uint32_t& s_nseg, uint32_t& s_claim) {
-  uint32_t sw = s_sw, su = s_su, nseg = 0;
+                                             uint32_t& s_sp, uint32_t& s_nseg, uint32_t& s_claim) {
+  uint32_t sw = s_sw, su = s_su, sp = s_sp, nseg = 0;
   while (su > 0 && nseg + 64 <= uint32_t(kMaxSegs)) {
     const uint32_t idx = sw + uint32_t(lane);
-    const WorkItem it = a.work[min(idx, a.num_items - 1)];
+    WorkItem it;
+    uint32_t slot0, nslots, ipos = 0;
+    bool valid = true;
+    if (a.pos) {   // (uniform)
+      const PosItem pi = ItemFromPositions(a, lane, sp, idx);
+      it = pi.it;
+      slot0 = pi.slot0;
+      nslots = pi.nslots;
+      valid = pi.valid;
+      ipos = pi.pos;
+    } else {
+      it = a.work[min(idx, a.num_items - 1)];
+      slot0 = idx * uint32_t(kQueriesPerTile);
+      nslots = kQueriesPerTile;
+    }
     const uint32_t j0 = (lane == 0 && sj) ? sj : it.j0;
     const uint32_t t = it.jend > j0 ? min(it.jend - j0, su) : 0u;
     uint32_t incl = t;
@@ -1607,7 +1885,7 @@ __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32
       if (lane >= off) incl += y;
     }
     const uint32_t excl = incl - t;
-    const bool used = excl < su;   // a prefix of the lanes
+    const bool used = valid && excl < su;   // a prefix of the lanes
     const bool take = used && t > 0;
     if (take) SMX_CHECK(idx, a.bd.items, "listed item");
     const uint64_t bt = __ballot(take);
@@ -1621,10 +1899,14 @@ __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32
       dsc.member_off = it.member_off;
       dsc.n = it.n;
       dsc.leaf = it.leaf;
+      dsc.slot0 = slot0;
+      dsc.nslots = nslots;
       s_desc[pos] = dsc;
     }
     const uint32_t nused = uint32_t(__popcll(__ballot(used)));
+    if (nused == 0) break;   // (cannot happen: lane 0's item is in position sp)
     const uint32_t last_incl = uint32_t(__shfl(int(incl), int(nused) - 1));
+    sp = uint32_t(__shfl(int(ipos), int(nused) - 1));   // the next item is there or later
     sw += nused;
     su -= min(su, last_incl);
     nseg += uint32_t(__popcll(bt));
@@ -1633,31 +1915,26 @@ __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32
   if (lane == 0) {
     s_sw = sw;
     s_su = su;
+    s_sp = sp;
     s_nseg = nseg;
     s_claim = 0;
   }
 }
 
 template <int K, int ABL = 0>
-__global__ void __launch_bounds__(64 * kScanWaves, 1) lut16_scan_kernel(ScanArgs a) {
+__global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(ScanArgs a) {
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
   constexpr int W = 4 * NW;
-  constexpr int KS = K / 2;
-  constexpr int Q = kQueriesPerTile, KB = kItemKeys;
-  constexpr int R = SMX_SCAN_R;
+  constexpr int Q = 32, KB = kItemKeys, NWAVES = ScanWaves<K>();
+  constexpr int R = SMX_SCAN_R;   // one-hot reads in flight ahead of their MFMA
   static_assert(K % 2 == 0, "the sparse scan takes two code nibbles per step");
-  static_assert(Q == 64, "a wave holds two 32-query halves");
-  // the step after which the previous tile's test runs, and the step after
-  // which the tile's code buffer is dead (its last lookup issued)
-  constexpr int EPI = KS - 1 < kEpiStep ? KS - 1 : kEpiStep;
-  constexpr int RELOAD = KS - 1 - R < 0 ? 0 : KS - 1 - R;
-  __shared__ ScanWaveLds wl_[kScanWaves];
+  __shared__ ScanWaveLds wl_[NWAVES];
   __shared__ __align__(256) v4i grp_tab[16];   // 256-aligned: base | (x & 0xF0)
   __shared__ int pos_tab[16];
   __shared__ uint32_t s_item[kMaxSegs], s_end[kMaxSegs], s_next[kMaxSegs];
   __shared__ SegDesc s_desc[kMaxSegs];
-  __shared__ uint32_t s_nseg, s_claim, s_sw, s_su;
-  // wave-uniform values in scalar registers
+  __shared__ uint32_t s_nseg, s_claim, s_sw, s_su, s_sp;
+  // wave-uniform values in scalar registers (the B fragments need the VGPRs)
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int c = lane & 31;
@@ -1672,26 +1949,35 @@ __global__ void __launch_bounds__(64 * kScanWaves, 1) lut16_scan_kernel(ScanArgs
     // position nibble p0 | p1 << 2: p0 in index fields 0..7, p1 in 8..15
     pos_tab[threadIdx.x] = int((threadIdx.x & 3u) * 0x5555u | ((threadIdx.x >> 2) * 0x5555u) << 16);
   }
-  const uint32_t worker = blockIdx.x * kScanWaves + wv;
+  const uint32_t worker = blockIdx.x * NWAVES + wv;
   // this workgroup's share: `units` tiles from tile jfirst of item w on
-  const uint4 ws = a.wave_start[blockIdx.x];
+  // (wave 0 lists the segments; only its copy is used)
+  const uint4 ws = wv != 0 ? make_uint4(0, 0, 0, 0)
+                   : a.pos ? ShareStart(a, lane) : a.wave_start[blockIdx.x];
   if (threadIdx.x == 0) {
     s_sw = ws.x;
     s_su = ws.z;
+    s_sp = ws.w;   // (fused front end) the position of item ws.x
   }
   uint32_t sj = ws.y;   // the share's first tile inside its first item
   bool pending = false;   // the previous segment's survivors await their copy
   bool flush = false;     // ... and, before that, their list-slot atomics
-  uint32_t fqid = 0;      // that segment's query id of slot `lane`
-  uint32_t slot = 0;      // that copy's first list slot of slot `lane`
+  uint32_t fqid = 0;      // that segment's query ids (lanes < 32)
+  uint32_t slot = 0;      // that copy's first list slot (lanes < 32)
   uint32_t par = 0;       // this segment's survivor buffer
   // the previous segment's survivors to their queries' lists: each key's
   // place = its query's reserved first slot (the returned value of the
   // segment-end atomic, waited for only here) + a running count
   auto copy_prev = [&]() {
+    if (ABL & 16) {
+      pending = false;
+      return;
+    }
     const uint32_t pp = par ^ 1u;
-    wl.q_slot[lane] = slot;
-    wl.qrun[lane] = 0;
+    if (lane < Q) {
+      wl.q_slot[lane] = slot;
+      wl.qrun[lane] = 0;
+    }
     WaveLdsSync();
     const uint32_t kn = min(wl.s_kn[pp], uint32_t(KB));
     for (uint32_t e = uint32_t(lane); e < kn; e += 64) {
@@ -1703,40 +1989,42 @@ __global__ void __launch_bounds__(64 * kScanWaves, 1) lut16_scan_kernel(ScanArgs
     WaveLdsSync();
     pending = false;
   };
-  // one list-slot atomic per query slot with survivors of the last segment
-  // (lane l: slot l); issued behind the next segment's loads (vmcnt is in
-  // order: a wait for those loads would otherwise wait for these atomics
-  // too), consumed by copy_prev after that segment's first tile
+  // one list-slot atomic per query slot with survivors of the last segment;
+  // issued behind the next segment's loads (vmcnt is in order: a wait for
+  // those loads would otherwise wait for these atomics too), consumed by
+  // copy_prev after that segment's first tile
   auto flush_prev = [&]() {
-    const uint32_t m = wl.qcnt[lane];
-    if (m) SMX_CHECK(fqid, a.bd.nq, "slot query");
-    slot = m ? atomicAdd(&a.cand_count[size_t(fqid) * kCounterStride], m) : 0u;
-    wl.prev_qid[lane] = fqid;
+    if ((ABL & 16) == 0 && lane < Q) {   // (16: timing ablation without the lists)
+      const uint32_t m = wl.qcnt[lane];
+      if (m) SMX_CHECK(fqid, a.bd.nq, "slot query");
+      slot = m ? atomicAdd(&a.cand_count[size_t(fqid) * kCounterStride], m) : 0u;
+      wl.prev_qid[lane] = fqid;
+    }
     flush = false;
     pending = true;
   };
-  // one LDS claim of a tile of segment `sg` (lane 0; broadcast at use)
-  auto claim1 = [&](uint32_t sg) -> uint32_t {
+  // one LDS claim of two tiles of segment `sg` (lane 0; broadcast at use)
+  auto claim2 = [&](uint32_t sg) -> uint32_t {
     uint32_t v = 0;
-    if (lane == 0) v = atomicAdd(&s_next[sg], 1u);
+    if (lane == 0) v = atomicAdd(&s_next[sg], 2u);
     return v;
   };
 
   for (;;) {   // rounds of at most kMaxSegs segments (block-uniform)
     __syncthreads();   // s_sw / s_su / the segment table are free
-    if (wv == 0) ListSegments(a, lane, sj, s_item, s_end, s_next, s_desc, s_sw, s_su, s_nseg,
-                                 s_claim);
+    if (wv == 0) ListSegments(a, lane, sj, s_item, s_end, s_next, s_desc, s_sw, s_su, s_sp,
+                                 s_nseg, s_claim);
     __syncthreads();
     const uint32_t nseg = s_nseg;
     if (nseg == 0) break;
     // claim-ahead segment (a reservation: joiners may still take its tiles)
     uint32_t sg_next = 0;
     if (lane == 0) sg_next = atomicAdd(&s_claim, 1u);
-    // the claimed-ahead segment's item and records, loaded during the
-    // segment before it: the B-fragment addresses need the query ids, so
+    // the claimed-ahead segment's item and query ids, loaded during the
+    // segment before it: the B-fragment addresses need the query id, so
     // without this a segment's setup is two dependent global latencies
     uint32_t pf_seg = ~0u, pf_item = 0;
-    ItemLane pf_ra = {}, pf_rb = {};
+    ItemLane pf_rec = {};
     for (;;) {
       uint32_t sg = __builtin_amdgcn_readfirstlane(sg_next);
       if (sg >= nseg) {
@@ -1759,7 +2047,7 @@ __global__ void __launch_bounds__(64 * kScanWaves, 1) lut16_scan_kernel(ScanArgs
         sg_next = atomicAdd(&s_claim, 1u);   // the next one, claimed ahead
       }
       const uint32_t end = __builtin_amdgcn_readfirstlane(s_end[sg]);
-      const uint32_t j = __builtin_amdgcn_readfirstlane(claim1(sg));
+      uint32_t j = __builtin_amdgcn_readfirstlane(claim2(sg));
       if (j >= end) continue;   // (joined too late)
       uint64_t st_rt = 0, st_t0 = 0, st_t1 = 0, st_t2 = 0;
       uint32_t st_hits = 0, st_surv = 0;
@@ -1767,24 +2055,38 @@ __global__ void __launch_bounds__(64 * kScanWaves, 1) lut16_scan_kernel(ScanArgs
         st_rt = __builtin_amdgcn_s_memrealtime();
         st_t0 = __builtin_amdgcn_s_memtime();
       }
-      // the slots' records {query, bias, 1/multiplier, sum limit}: prefetched
-      // during the segment before (the claimed-ahead one), so the
-      // B-fragment loads issue at once
+      // the slot's lane record {query, bias, 1/multiplier, sum limit}:
+      // prefetched during the segment before (the claimed-ahead one), so
+      // the B-fragment loads issue at once
+      // (slot c of the item: record slot0 + c when c < nslots, else empty)
+      auto slot_rec = [&](uint32_t sgi) {
+        const uint32_t s0 = __builtin_amdgcn_readfirstlane(s_desc[sgi].slot0);
+        const uint32_t ns = __builtin_amdgcn_readfirstlane(s_desc[sgi].nslots);
+        ItemLane r;
+        if (uint32_t(c) < ns) {
+          SMX_CHECK(s0 + uint32_t(c), a.bd.recs, "slot record");
+          r = a.lanes[size_t(s0) + c];
+        } else {
+          r.qid = kNoQuery;
+          r.bias = 0.0f;
+          r.inv = 0.0f;
+          r.amax = kNoSum;
+        }
+        return r;
+      };
       uint32_t item;
-      ItemLane ra, rb;   // slots c and 32 + c
+      ItemLane cl;
       if (sg == pf_seg) {
         item = pf_item;
-        ra = pf_ra;
-        rb = pf_rb;
+        cl = pf_rec;
       } else {
         item = __builtin_amdgcn_readfirstlane(s_item[sg]);
         SMX_CHECK(item, a.bd.items, "segment item");
-        ra = a.lanes[size_t(item) * Q + c];
-        rb = a.lanes[size_t(item) * Q + 32 + c];
+        cl = slot_rec(sg);
       }
+      const uint32_t qid = cl.qid;
       // an empty slot (kNoQuery) loads query 0's rows and never passes (amax)
-      const uint32_t qa = ra.qid == kNoQuery ? 0u : ra.qid;
-      const uint32_t qb = rb.qid == kNoQuery ? 0u : rb.qid;
+      const uint32_t lq = qid == kNoQuery ? 0u : qid;
       const SegDesc& sd = s_desc[sg];
       const uint64_t toff = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(sd.tile_off >> 32))) << 32) |
                             __builtin_amdgcn_readfirstlane(uint32_t(sd.tile_off));
@@ -1792,60 +2094,58 @@ __global__ void __launch_bounds__(64 * kScanWaves, 1) lut16_scan_kernel(ScanArgs
                             __builtin_amdgcn_readfirstlane(uint32_t(sd.member_off));
       const uint32_t n = __builtin_amdgcn_readfirstlane(sd.n);
       const int leaf = int(__builtin_amdgcn_readfirstlane(sd.leaf));
-      SMX_CHECK(ra.qid == kNoQuery ? 0u : ra.qid, a.bd.nq, "slot record query");
-      SMX_CHECK(rb.qid == kNoQuery ? 0u : rb.qid, a.bd.nq, "slot record query");
+      SMX_CHECK(qid == kNoQuery ? 0u : qid, a.bd.nq, "slot record query");
       SMX_CHECK(leaf, a.bd.nl, "segment leaf");
       SMX_CHECK(toff + (n + 31u) / 32u, a.bd.tiles + 1, "segment tiles");
       SMX_CHECK(moff + n, a.bd.members + 1, "segment members");
-      // the B fragments of both halves (LUT rows 4s + 2h, 4s + 2h + 1 of
-      // queries qa and qb: 32 bytes per step), held for the whole segment;
-      // the smfmac statements read them as AGPR operands, so hipcc keeps
-      // them in the accumulator file (no copies; tools/audit_isa.py)
-      v8i ba[KS], bb[KS];
-      {
-        const uint8_t* lutb = reinterpret_cast<const uint8_t*>(a.lut);
-        const v8i* pa = reinterpret_cast<const v8i*>(lutb + size_t((qa * uint32_t(K) + uint32_t(h)) * 32u));
-        const v8i* pb = reinterpret_cast<const v8i*>(lutb + size_t((qb * uint32_t(K) + uint32_t(h)) * 32u));
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          ba[s] = pa[2 * s];
-          bb[s] = pb[2 * s];   // (an all-empty half loads query 0's rows)
-        }
-      }
-      // addresses as a wave-uniform base + a 32-bit lane offset (saddr loads)
+      // this segment's B fragments (LUT rows 2s+h of query c) and first tile
+      v8i b[K / 2];
+      uint32_t codes[NW] = {};
+      // addresses as a wave-uniform base + a 32-bit lane offset (saddr
+      // loads: no 64-bit per-lane pointers live across the tile loop)
       const uint8_t* tseg = a.tiles + toff * 64ull * W;
       auto tile_ptr = [&](uint32_t t) {
         return tseg + size_t(t * uint32_t(64 * W) + uint32_t(lane) * uint32_t(W));
       };
-      uint32_t cA[NW] = {}, cB[NW] = {};
-      LoadCodes<K>(tile_ptr(j), cA);
-      // the claimed-ahead segment's item and records, for its setup
+      // LUT rows 4s + 2h, 4s + 2h + 1 of query c (32 bytes) per sparse step
+      const uint32_t boff = (lq * uint32_t(K) + uint32_t(h)) * 32u;
+      const uint8_t* lutb = reinterpret_cast<const uint8_t*>(a.lut);
+      auto load_b = [&]() {
+        // one per-lane address, the steps as immediate offsets
+        const v8i* bp = reinterpret_cast<const v8i*>(lutb + size_t(boff));
+#pragma unroll
+        for (int s2 = 0; s2 < K / 2; ++s2) b[s2] = bp[2 * s2];
+      };
+      load_b();
+      LoadCodes<K>(tile_ptr(j), codes);
+      // the claimed-ahead segment's item and query ids, for its setup
       {
         const uint32_t sn = __builtin_amdgcn_readfirstlane(sg_next);
         if (sn < nseg) {
           pf_seg = sn;
           pf_item = __builtin_amdgcn_readfirstlane(s_item[sn]);
           SMX_CHECK(pf_item, a.bd.items, "prefetch item");
-          pf_ra = a.lanes[size_t(pf_item) * Q + c];
-          pf_rb = a.lanes[size_t(pf_item) * Q + 32 + c];
+          pf_rec = slot_rec(sn);
         } else {
           pf_seg = ~0u;
         }
       }
+
+      // the slot's sum limit (written with the record by the pair scatter:
+      // the largest LUT16 sum whose distance can pass the query's threshold)
+      const int amax = cl.amax;
       if (flush) flush_prev();
-      {
-        const ItemLane& mine = h ? rb : ra;   // lane l: slot l
+      if (lane < Q) {
         QParam v;
-        v.qid = mine.qid;
-        v.amax = mine.amax;
-        v.bias = mine.bias;
-        v.inv = mine.inv;
+        v.qid = qid;
+        v.amax = amax;
+        v.bias = cl.bias;
+        v.inv = cl.inv;
         wl.qp[lane] = v;
         wl.qcnt[lane] = 0;
       }
       if (lane == 0) wl.s_kn[par] = 0;
       WaveLdsSync();
-      const int amax_a = ra.amax, amax_b = rb.amax;
       uint32_t whits = 0;   // wave-uniform
 
       // the hit list's elements (16 sums per hit) spread over the lanes,
@@ -1866,8 +2166,8 @@ __global__ void __launch_bounds__(64 * kScanWaves, 1) lut16_scan_kernel(ScanArgs
           if (e < total) {
             const uint32_t hidx = e >> 4, i = e & 15u;
             const uint32_t meta = wl.hmeta[hidx];
-            cc = int(meta & 63u);
-            const uint32_t hh = (meta >> 6) & 1u, jj = meta >> 7;
+            cc = int(meta & 31u);
+            const uint32_t hh = (meta >> 5) & 1u, jj = meta >> 6;
             const uint32_t word = reinterpret_cast<const uint32_t*>(&wl.hsum[hidx][0])[i >> 1];
             const int sum = int(int16_t(uint16_t(word >> (16u * (i & 1u)))));
             const QParam pq = wl.qp[cc];
@@ -1902,164 +2202,123 @@ __global__ void __launch_bounds__(64 * kScanWaves, 1) lut16_scan_kernel(ScanArgs
         WaveLdsSync();   // the hit list is rewritten next
       };
 
-      // the test of a finished tile's sums (accumulators p0 = slots c, p1 =
-      // slots 32 + c of tile jt): rows past the leaf's end masked, the
-      // 16-sum minimum against the slot's sum limit, hits appended
-      auto epilogue = [&](v16i& p0, v16i& p1, uint32_t jt) {
-        XdlReadPad(p0, p1);
+      // one tile: K MFMAs, then the hit test
+      auto tile = [&](const uint32_t (&cd)[NW], uint32_t jt) {
+        v16i acc = TileSmfmac<K, R>(cd, b, grp_tab, pos_tab);
         if (ABL & 4) {
-          int x = p0[0] ^ p1[0];
+          int x = acc[0];
 #pragma unroll
-          for (int i = 1; i < 16; ++i) x ^= p0[i] ^ p1[i];
-          if (x == 0x7fffffff) a.cand_count[0] = uint32_t(x);
+          for (int i = 1; i < 16; ++i) x ^= acc[i];
+          if (x == 0x7fffffff) a.cand_count[0] = x;
           return;
         }
         const uint32_t rows_left = n - jt * kDpPerTile;
         if (rows_left < uint32_t(kDpPerTile)) {  // last tile of the leaf
           // row (i&3) + 8(i>>2) + 4h >= rows_left, against one per-tile value
+          // (16 hoisted row numbers would cost 16 registers for the loop)
           const int lim = int(rows_left) - 4 * h;
 #pragma unroll
           for (int i = 0; i < 16; ++i)
-            if ((i & 3) + 8 * (i >> 2) >= lim) {
-              p0[i] = 0x7FFF;
-              p1[i] = 0x7FFF;
-            }
+            if ((i & 3) + 8 * (i >> 2) >= lim) acc[i] = 0x7FFF;
         }
-        const bool hit_a = Min16(p0) <= amax_a;
-        const bool hit_b = Min16(p1) <= amax_b;
-        const uint64_t ha = __builtin_amdgcn_ballot_w64(hit_a);
-        const uint64_t hb = __builtin_amdgcn_ballot_w64(hit_b);
-        if (ha | hb) {
-          // whits <= kHitCap - 128 here and a tile adds at most 128: the
-          // list always has room, so the sums are dead before any drain
-          const uint32_t na = uint32_t(__popcll(ha));
-          auto append = [&](const v16i& p, uint32_t pos, uint32_t sl) {
+        int m = min(min(acc[0], acc[1]), acc[2]);
+#pragma unroll
+        for (int i = 3; i < 15; i += 2) m = min(min(m, acc[i]), acc[i + 1]);
+        m = min(m, acc[15]);
+        const bool hit = m <= amax;
+        const uint64_t hb = __builtin_amdgcn_ballot_w64(hit);
+        if (ABL & 2) {   // timing ablation: the hit test without its list
+          if (hb == 0x1234567ull) a.cand_count[0] = 1u;
+          return;
+        }
+        if (hb) {
+          // whits <= 64 here and a tile adds at most 64: the list (128)
+          // always has room, so the sums are dead before any drain
+          const uint32_t nh = uint32_t(__popcll(hb));
+          if (hit) {
+            const uint32_t hs =
+                whits + __builtin_amdgcn_mbcnt_hi(uint32_t(hb >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo(uint32_t(hb), 0u));
             uint32_t pk[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k)
-              pk[k] = (uint32_t(p[2 * k]) & 0xFFFFu) | (uint32_t(p[2 * k + 1]) << 16);
-            wl.hsum[pos][0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-            wl.hsum[pos][1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
-            wl.hmeta[pos] = (jt << 7) | (uint32_t(h) << 6) | sl;
-          };
-          if (hit_a)
-            append(p0, whits + __builtin_amdgcn_mbcnt_hi(uint32_t(ha >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo(uint32_t(ha), 0u)),
-                   uint32_t(c));
-          if (hit_b)
-            append(p1, whits + na + __builtin_amdgcn_mbcnt_hi(uint32_t(hb >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo(uint32_t(hb), 0u)),
-                   32u + uint32_t(c));
-          whits += na + uint32_t(__popcll(hb));
-          if (ABL & 8) st_hits += na + uint32_t(__popcll(hb));
+              pk[k] = (uint32_t(acc[2 * k]) & 0xFFFFu) | (uint32_t(acc[2 * k + 1]) << 16);
+            wl.hsum[hs][0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            wl.hsum[hs][1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+            wl.hmeta[hs] = (jt << 6) | uint32_t(lane);
+          }
+          whits += nh;
+          if (ABL & 8) st_hits += nh;
           // no wait for the writes: a wave's LDS instructions execute in
           // order, so the drain's later reads see them (compiler barrier only)
           asm volatile("" ::: "memory");
         }
       };
-
-      if (ABL & 8) st_t1 = __builtin_amdgcn_s_memtime();
-      // The tiles this wave takes, claimed one at a time from the segment's
-      // LDS counter.  Tile i computes with code buffer / accumulator pair
-      // (i & 1); once its last lookup has been issued its buffer is
-      // reloaded with tile i + 2's codes (claimed a tile before), and tile
-      // i - 1's test runs at its step kEpiStep.  Every tile issues exactly
-      // one codes load (an exhausted segment reloads the current tile), so
-      // the wait for a tile's codes always leaves the next one's in flight.
-      uint32_t tiles_done = 0;
-      uint32_t t_cur = j, t_next = end;
-      uint32_t claim_raw = 0;
-      bool claims_done = false;
-      {
-        const uint32_t j1 = __builtin_amdgcn_readfirstlane(claim1(sg));
-        t_next = j1 < end ? j1 : end;
-        LoadCodes<K>(tile_ptr(j1 < end ? j1 : j), cB);
-        if (j1 < end) claim_raw = claim1(sg);
-        else claims_done = true;
-      }
-      v16i xa, xb, ya, yb;
-      // one tile: its steps, with the reload of its code buffer and (PREV)
-      // the previous tile's test among them; returns the tile loaded
-      auto step_tile = [&](auto prev_tag, uint32_t (&cd)[NW], v16i& a0, v16i& a1, v16i& p0,
-                           v16i& p1, uint32_t t, uint32_t t_prev) -> uint32_t {
-        constexpr bool PREV = decltype(prev_tag)::value;
-        uint32_t t_load = end;
-        // R lookups in flight over R + 1 rotating registers: a lookup never
-        // overwrites the A operand of the MFMAs issued just before it
-        constexpr int NB = R + 1;
-        v4i o[NB];
-        int ix[NB];
-#pragma unroll
-        for (int p = 0; p < (R < KS ? R : KS); ++p) {
-          const uint32_t gv = (cd[p >> 2] >> ((p & 3) * 8)) & 0xFu;
-          const uint32_t pv = (cd[p >> 2] >> ((p & 3) * 8 + 4)) & 0xFu;
-          o[p] = grp_tab[gv];
-          ix[p] = pos_tab[pv];
-        }
-        ZeroAcc(a0);
-        ZeroAcc(a1);
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          SMX_SMFMAC(a0, o[s % NB], ba[s], ix[s % NB]);
-          SMX_SMFMAC(a1, o[s % NB], bb[s], ix[s % NB]);
-          if (s + R < KS) {
-            const int u = s + R;
-            const uint32_t gv = (cd[u >> 2] >> ((u & 3) * 8)) & 0xFu;
-            const uint32_t pv = (cd[u >> 2] >> ((u & 3) * 8 + 4)) & 0xFu;
-            o[u % NB] = grp_tab[gv];
-            ix[u % NB] = pos_tab[pv];
-          }
-          if (s == RELOAD) {
-            // cd is dead: the tile after next into it
-            if (!claims_done) {
-              t_load = __builtin_amdgcn_readfirstlane(claim_raw);
-              if (t_load < end) claim_raw = claim1(sg);
-              else claims_done = true;
-            }
-            LoadCodes<K>(tile_ptr(t_load < end ? t_load : t), cd);
-          }
-          if (PREV && s == EPI) epilogue(p0, p1, t_prev);
-        }
-        ++tiles_done;
-        return t_load;
-      };
-      // a test appends at most 128 hits: drain the list first when it could
-      // overflow (the pending accumulators stay in registers)
-      auto room = [&]() {
-        if (whits > uint32_t(kHitCap - 128)) {
+      // a hit list over half full is drained between tiles with the B
+      // fragments dead (reloaded after, from L2): the drain's registers
+      // then never compete with them (rare: ~1 hit lane per tile)
+      auto drain_mid = [&]() {
+        if (whits > 64u) {
           drain();
           whits = 0;
+          load_b();
         }
       };
+
+      if (ABL & 8) st_t1 = __builtin_amdgcn_s_memtime();
+      // the tiles this wave takes, a claimed pair at a time with the next
+      // pair claimed ahead; two code buffers in turn (the load of the next
+      // tile is in flight while this one computes; a rotating copy would
+      // force a wait for it at the copy)
+      uint32_t pe = min(j + 2, end);        // the current pair [.., pe)
+      uint32_t na_raw = claim2(sg);          // the next pair (lane 0)
+      bool na_known = false;
+      uint32_t na = end;
+      auto next_tile = [&](uint32_t t, uint32_t& tn) -> bool {
+        if (t + 1 < pe) {
+          tn = t + 1;
+          return true;
+        }
+        if (!na_known) {
+          na = __builtin_amdgcn_readfirstlane(na_raw);
+          na_known = true;
+        }
+        if (na >= end) return false;
+        tn = na;
+        return true;
+      };
+      auto advance = [&](uint32_t t, uint32_t tn) {
+        if (!(t + 1 < pe)) {   // moved into the pair claimed ahead: claim another
+          pe = min(tn + 2, end);
+          na_raw = claim2(sg);
+          na_known = false;
+        }
+      };
+      uint32_t tiles_done = 0;
       {
-        // the first tile (no test pending), then tiles in pairs: buffer cB /
-        // accumulators y with x's test inside, buffer cA / x with y's test
-        uint32_t t_load = step_tile(std::false_type{}, cA, xa, xb, ya, yb, t_cur, 0u);
-        if (pending) copy_prev();   // after the segment's first tile: the atomic has returned
-        room();
-        if (t_next >= end) {
-          epilogue(xa, xb, t_cur);
-        } else {
-          for (;;) {
-            uint32_t t_prev = t_cur;
-            t_cur = t_next;
-            t_next = t_load;
-            t_load = step_tile(std::true_type{}, cB, ya, yb, xa, xb, t_cur, t_prev);
-            room();
-            if (t_next >= end) {
-              epilogue(ya, yb, t_cur);
-              break;
-            }
-            t_prev = t_cur;
-            t_cur = t_next;
-            t_next = t_load;
-            t_load = step_tile(std::true_type{}, cA, xa, xb, ya, yb, t_cur, t_prev);
-            room();
-            if (t_next >= end) {
-              epilogue(xa, xb, t_cur);
-              break;
-            }
-          }
+        uint32_t cb[NW];
+        uint32_t t = j, tn = 0;
+        for (;;) {
+          bool more = next_tile(t, tn);
+          // unconditional (the current tile again when none follows): one
+          // load per tile on every path, so the wait for this tile's codes
+          // leaves the next tile's load in flight (vmcnt(1), not vmcnt(0))
+          LoadCodes<K>(tile_ptr(more ? tn : t), cb);
+          tile(codes, t);
+          ++tiles_done;
+          if (pending) copy_prev();   // after the segment's first tile: the atomic has returned
+          if (!more) break;
+          drain_mid();
+          advance(t, tn);
+          t = tn;
+          more = next_tile(t, tn);
+          LoadCodes<K>(tile_ptr(more ? tn : t), codes);
+          tile(cb, t);
+          ++tiles_done;
+          if (!more) break;
+          drain_mid();
+          advance(t, tn);
+          t = tn;
         }
       }
       if (whits) {
@@ -2068,12 +2327,12 @@ __global__ void __launch_bounds__(64 * kScanWaves, 1) lut16_scan_kernel(ScanArgs
       }
       if (ABL & 8) st_t2 = __builtin_amdgcn_s_memtime();
       if (ABL & 8) {
-        uint32_t sv = wl.qcnt[lane];
+        uint32_t sv = lane < Q ? wl.qcnt[lane] : 0u;
         for (int off = 32; off > 0; off >>= 1) sv += uint32_t(__shfl_xor(int(sv), off));
         st_surv = sv;
       }
       flush = true;   // (its slot atomics: at the next segment's start)
-      fqid = h ? rb.qid : ra.qid;
+      fqid = qid;
       par ^= 1u;
       if ((ABL & 8) && lane == 0)
         StampItem(a, worker, item, st_rt, st_t0, st_t1, st_t2, __builtin_amdgcn_s_memtime(),
@@ -2926,7 +3185,9 @@ __global__ void fill64_kernel(uint64_t* p, uint64_t v, size_t n) {
 // ---------------------------------------------------------------------------
 hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int nq, int L,
                                int32_t* out_leaf, float* out_dist, float* scores, hipStream_t s,
-                               const FrontArgs* front) {
+                               const FrontArgs* front, const SeedArgs* seed,
+                               const WorklistArgs* wl, bool* fused) {
+  if (fused) *fused = false;
   if (nq == 0) return hipSuccess;
   uint32_t kcap = 1;
   while (kcap < uint32_t(ix.nl)) kcap <<= 1;
@@ -2955,7 +3216,33 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   // static LDS of the kernel besides the dynamic key buffers: the LUT build's
   // raw table and reduction (~5 KB) and the selection's words
   constexpr size_t kStaticLds = 6 * 1024;
-  if (L <= kWaveTopL && ix.nl <= 256 * 4) {
+  if (seed && wl && fused && seed->leaf_slots && wl->pos && L <= kWaveTopL && ix.nl <= 256 * 8) {
+    const bool v4 = ix.nl <= 256 * 4;
+#define SMX_TOPL_SEED_CASE(KV)                                                               \
+  case KV:                                                                                   \
+    if (v4)                                                                                  \
+      hipLaunchKernelGGL((topl_seed_kernel<4, KV>), dim3(nq), dim3(256), 0, s, scores, ix.nl, \
+                         L, out_leaf, out_dist, tail, *seed, *wl);                            \
+    else                                                                                     \
+      hipLaunchKernelGGL((topl_seed_kernel<8, KV>), dim3(nq), dim3(256), 0, s, scores, ix.nl, \
+                         L, out_leaf, out_dist, tail, *seed, *wl);                            \
+    break;
+    switch (ix.ksteps) {
+      SMX_TOPL_SEED_CASE(4)
+      SMX_TOPL_SEED_CASE(8)
+      SMX_TOPL_SEED_CASE(12)
+      SMX_TOPL_SEED_CASE(16)
+      SMX_TOPL_SEED_CASE(20)
+      SMX_TOPL_SEED_CASE(24)
+      SMX_TOPL_SEED_CASE(26)
+      SMX_TOPL_SEED_CASE(28)
+      SMX_TOPL_SEED_CASE(32)
+      default:
+        return hipErrorInvalidValue;
+    }
+#undef SMX_TOPL_SEED_CASE
+    *fused = true;
+  } else if (L <= kWaveTopL && ix.nl <= 256 * 4) {
     hipLaunchKernelGGL((topl_block_kernel<4, 256>), dim3(nq), dim3(256), 0, s, scores, ix.nl, L,
                        out_leaf, out_dist, tail);
   } else if (L <= kWaveTopL && ix.nl <= 256 * 8) {
@@ -3013,6 +3300,8 @@ WorklistArgs MakeWorklistArgs(const DeviceIndex& ix, const uint32_t* leaf_count,
   w.work = work;
   w.lanes = lanes;
   w.wave_start = wave_start;
+  w.pos = nullptr;
+  w.done = nullptr;
   return w;
 }
 
@@ -3035,30 +3324,34 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
   return hipGetLastError();
 }
 
-// The product library compiles the scan only; the timing ablation (4: no
-// epilogue, results invalid) and the per-segment stamps (8) exist in the
+// The product library compiles the scan only; the timing ablations (2, 4,
+// 16: results invalid) and the per-segment stamps (8) exist in the
 // diagnostic build (-DSMX_SCAN_DIAGNOSTICS, tools/tune.py / scan_stamps.py).
 #ifdef SMX_SCAN_DIAGNOSTICS
 #define SMX_SCAN_CASE(KV)                                                                  \
   case KV:                                                                                 \
-    if (variant == 4)                                                                      \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 4>), dim3(grid), dim3(64 * kScanWaves), 0, \
-                         s, a);                                                            \
+    if (variant == 16)                                                                     \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 16>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
+                         0, s, a);                                                         \
+    else if (variant == 2)                                                                 \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 2>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
+                         0, s, a);                                                         \
+    else if (variant == 4)                                                                 \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 4>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
+                         0, s, a);                                                         \
     else if (variant == 8)                                                                 \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 8>), dim3(grid), dim3(64 * kScanWaves), 0, \
-                         s, a);                                                            \
-    else if (variant == 0)                                                                 \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * kScanWaves), 0, \
-                         s, a);                                                            \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 8>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
+                         0, s, a);                                                         \
     else                                                                                   \
-      return hipErrorInvalidValue;                                                         \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
+                         0, s, a);                                                         \
     break;
 #else
 #define SMX_SCAN_CASE(KV)                                                                  \
   case KV:                                                                                 \
     if (variant != 0) return hipErrorInvalidValue;                                         \
-    hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * kScanWaves), 0, s, \
-                       a);                                                                 \
+    hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()),  \
+                       0, s, a);                                                           \
     break;
 #endif
 
@@ -3083,7 +3376,7 @@ hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int va
 #define SMX_OCC_CASE(KV)                                                                 \
   case KV:                                                                               \
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(                                 \
-        blocks, reinterpret_cast<const void*>(&lut16_scan_kernel<KV, 0>), 64 * kScanWaves, 0);
+        blocks, reinterpret_cast<const void*>(&lut16_scan_kernel<KV, 0>), 64 * ScanWaves<KV>(), 0);
 
 hipError_t ScanBlocksPerCU(const DeviceIndex& ix, int* blocks) {
   *blocks = 0;

@@ -103,6 +103,9 @@ struct Workspace {
   smx::ItemLane* lanes = nullptr;   // [max_items][32]
   uint4* wave_start = nullptr;      // [grid] each scan wave's static share
   uint32_t* pos_unit0 = nullptr;    // [nl+1] work units before each leaf (work order)
+  smx::PosDesc* pos = nullptr;      // [nl] fused front end: the work order's positions
+  smx::ItemLane* leaf_slots = nullptr;   // fused front end: [nl][slot_stride] pair records
+  uint32_t slot_stride = 0;         // nq rounded up to 32 (0: no leaf slots)
   uint32_t* gunits = nullptr;       // [16] the XCD groups' unit boundaries
   unsigned long long* wl_part = nullptr;   // [4 * ceil(nl / 256)] work-list block sums
   uint64_t* tau = nullptr;          // [nq]
@@ -116,7 +119,8 @@ struct Workspace {
     DFree(queries); DFree(topl_leaf); DFree(topl_dist); DFree(scores); DFree(lut); DFree(mult);
     DFree(inv);
     DFree(counters); DFree(rank); DFree(leaf_item0); DFree(lanes); DFree(wave_start);
-    DFree(pos_unit0); DFree(gunits); DFree(wl_part);
+    DFree(pos_unit0); DFree(gunits); DFree(wl_part); DFree(pos); DFree(leaf_slots);
+    slot_stride = 0;
     DFree(work); DFree(tau); DFree(cand); DFree(cand_count); DFree(out_idx);
     DFree(out_dist);
     DFree(out_count);
@@ -137,6 +141,13 @@ struct smx_index {
   int seed_leaves = 4;
   int scan_variant = 0;            // see smx::LaunchScan
   int fused_worklist_leaves = smx::kFusedWorklistLeaves;   // 0: always the side stream
+  // SMX_FUSED_FRONT=1: the top-L launch also computes the seed thresholds, the
+  // pairs' leaf-slot records and the work list's positions (four launches a
+  // call instead of six); measured 2% slower than the separate launches at
+  // glove shape (the seed blocks' LDS pair-table lookups, not the launches,
+  // bound the front end), so off by default
+  bool fused_front = false;
+  bool front_fused_last = false;   // the last call ran the fused front end (timings)
   uint32_t chunk_tiles = 20;       // tiles per work item (tools/tune.py: 16-20 best at glove)
   int grid = 0;                    // scan grid: resident one-wave workgroups (occupancy API)
   bool profiling = false;
@@ -355,6 +366,12 @@ uint32_t AutoCap(int L, int kk, int seed) {
   return cap;
 }
 
+uint32_t RoundUp32(int n) { return (uint32_t(n) + 31u) & ~31u; }
+
+// The index shapes the fused front end takes (one 256-thread top-L block per
+// query, the work list's positions built by one block): nl <= 2048, L <= 512.
+bool FusedFrontShape(const smx::DeviceIndex& ix, int L) { return ix.nl <= 2048 && L <= 512; }
+
 int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
   Workspace& w = h->ws;
   const smx::DeviceIndex& ix = h->ix;
@@ -400,6 +417,16 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
       (rc = DAlloc(&w.out_dist, size_t(nq) * width)) || (rc = DAlloc(&w.out_count, nq))) {
     w.Release();
     return rc;
+  }
+  // leaf slots of the fused front end (smx::LaunchPartitionTopL): one record
+  // per possible (leaf, query) pair, at most 1 GiB
+  if (FusedFrontShape(ix, L) && uint64_t(nl) * RoundUp32(nq) * sizeof(smx::ItemLane) <= (1ull << 30)) {
+    if ((rc = DAlloc(&w.pos, size_t(nl))) ||
+        (rc = DAlloc(&w.leaf_slots, size_t(nl) * RoundUp32(nq)))) {
+      w.Release();
+      return rc;
+    }
+    w.slot_stride = RoundUp32(nq);
   }
   w.nq = nq; w.L = L; w.kk = kk; w.width = width; w.dim = ix.dim;
   w.gen = ++h->ws_generation;
@@ -457,6 +484,11 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   bd.datapoints = ix.num_datapoints;
   bd.members = ix.num_members;
   bd.tiles = ix.num_tiles;
+  // the fused front end (top-L + seed + pair records + work-list positions in
+  // one launch; the scan derives its items from the positions)
+  const bool fuse = h->fused_front && w.slot_stride >= uint32_t(nq) && w.leaf_slots &&
+                    FusedFrontShape(ix, L);
+  bd.recs = fuse ? uint32_t(nl) * w.slot_stride : w.max_items * uint32_t(smx::kQueriesPerTile);
   smx::SeedArgs sa{};
   sa.bd = bd;
   sa.topl_leaf = w.topl_leaf;
@@ -476,6 +508,8 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sa.seed = seed;
   sa.kk = kk;
   sa.residual = ix.residual;
+  sa.leaf_slots = fuse ? w.leaf_slots : nullptr;
+  sa.slot_stride = w.slot_stride;
 
   smx::ScanArgs a{};
   a.bd = bd;
@@ -484,7 +518,12 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   a.lut = w.lut;
   a.inv = w.inv;
   a.work = w.work;
-  a.lanes = w.lanes;
+  a.lanes = fuse ? w.leaf_slots : w.lanes;
+  a.pos = fuse ? w.pos : nullptr;
+  a.pos_unit0 = w.pos_unit0;
+  a.gunits = w.gunits;
+  a.slot_stride = w.slot_stride;
+  a.chunk_tiles = h->chunk_tiles;
   a.wave_start = w.wave_start;
   a.num_items = w.max_items;   // bound of the one-ahead descriptor prefetch
   a.tau_key = w.tau;
@@ -579,8 +618,29 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     f.mult = w.mult;
     f.inv = w.inv;
     f.one_to_many = single ? 1 : 0;
-    SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s, &f));
+    // Fused front end: the seed thresholds, the pairs' slot records and the
+    // work list's positions in the top-L launch -- four launches in all
+    smx::WorklistArgs fwl = smx::MakeWorklistArgs(
+        ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes, w.wave_start, h->grid,
+        stats + 3, code_bytes, h->chunk_tiles, bd);
+    fwl.pos = w.pos;
+    fwl.done = stats + 16;   // zeroed by the state reset above
+    bool fused = false;
+    SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s, &f,
+                                     fuse ? &sa : nullptr, fuse ? &fwl : nullptr,
+                                     fuse ? &fused : nullptr));
     Mark(h, 1, s);
+    h->front_fused_last = fused;
+    if (fuse && !fused)
+      return Fail(SMX_INTERNAL, "fused front end not taken for a shape that selected it");
+    if (fused) {
+      Mark(h, 5, s);
+      SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s));
+      Mark(h, 6, s);
+      SMX_HIP(smx::LaunchFinalSelect(sel, nq, s));
+      Mark(h, 7, s);
+      return SMX_OK;
+    }
     if (ix.nl <= h->fused_worklist_leaves) {
       // the work list is built by extra blocks of the seed launch (one
       // stream: a fork/join costs 5-10 us per cross-queue edge)
@@ -741,8 +801,15 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     // stream) and the seed overlap, each timed from the fork
     t.partition_ms = Elapsed(h, 0, 1);
     t.lut_ms = 0.0f;
-    t.invert_ms = Elapsed(h, 1, 3);
-    t.seed_scan_ms = Elapsed(h, 1, 4);
+    if (h->front_fused_last) {
+      // the seed, the pair records and the work list ran inside the top-L
+      // launch (partition_ms)
+      t.invert_ms = Elapsed(h, 1, 5);
+      t.seed_scan_ms = 0.0f;
+    } else {
+      t.invert_ms = Elapsed(h, 1, 3);
+      t.seed_scan_ms = Elapsed(h, 1, 4);
+    }
     t.seed_select_ms = 0.0f;
     t.scan_ms = Elapsed(h, 5, 6);
     t.select_ms = Elapsed(h, 6, 7);
@@ -847,6 +914,7 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
   }
   if (const char* fw = std::getenv("SMX_FUSED_WORKLIST"))
     h->fused_worklist_leaves = std::min(std::atoi(fw), smx::kFusedWorklistLeaves);
+  if (const char* ff = std::getenv("SMX_FUSED_FRONT")) h->fused_front = ff[0] != '0';
   const char* ng = std::getenv("SMX_NO_GRAPH");
   // Eager launches by default: six kernels a call queue back to back on the
   // stream, while consecutive replays of a captured graph left ~13 us
@@ -1200,9 +1268,10 @@ int smx_set_tuning(smx_index* h, int32_t candidates_per_query, int32_t seed_leav
                    int32_t scan_variant, int32_t chunk_tiles) {
   if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
 #ifdef SMX_SCAN_DIAGNOSTICS
-  if (scan_variant != 0 && scan_variant != 4 && scan_variant != 8)
+  if (scan_variant != 0 && scan_variant != 2 && scan_variant != 4 && scan_variant != 8 &&
+      scan_variant != 16)
     return Fail(SMX_INVALID_ARGUMENT,
-                "scan_variant is 0 (scan), 4 (timing ablation) or 8 (diagnostic stamps)");
+                "scan_variant is 0 (scan), 2 / 4 / 16 (timing ablations) or 8 (diagnostic stamps)");
 #else
   if (scan_variant != 0)
     return Fail(SMX_INVALID_ARGUMENT,

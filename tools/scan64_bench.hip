@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include <algorithm>
 
 #define CHECK(x)                                                                       \
   do {                                                                                 \
@@ -91,7 +92,10 @@ __device__ __forceinline__ int Min16(const v16i& a) {
 // ---------------------------------------------------------------------------
 // cur: 32 slots, 12 waves per CU
 // ---------------------------------------------------------------------------
-template <int NB>
+// MODE bits (timing ablations, results invalid): 1 = no code loads after the
+// first tile, 2 = no one-hot lookups in the loop, 4 = B fragments loaded once
+// per wave instead of once per segment
+template <int NB, int MODE = 0>
 __global__ void __launch_bounds__(768, 1) scan_cur(const uint8_t* __restrict__ tiles, uint32_t ntiles,
                                                    const int8_t* __restrict__ lut, int nq, int seg,
                                                    int amax, unsigned long long* __restrict__ out,
@@ -104,21 +108,31 @@ __global__ void __launch_bounds__(768, 1) scan_cur(const uint8_t* __restrict__ t
   const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
   const uint32_t nseg = (ntiles + seg - 1) / seg;
   unsigned long long hits = 0;
+  v8i b[KS];
+  v16i acc;
+  const uint64_t ck0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
   for (uint32_t sg = wave; sg < nseg; sg += nwaves) {
     const uint32_t q = (sg * 32 + c) % uint32_t(nq);
     const v8i* bp = reinterpret_cast<const v8i*>(lut + (size_t(q) * K + h) * 32);
-    v8i b[KS];
+    if (!(MODE & 4) || sg == wave) {
 #pragma unroll
-    for (int s = 0; s < KS; ++s) b[s] = bp[2 * s];
+      for (int s = 0; s < KS; ++s) b[s] = bp[2 * s];
+    }
     const uint32_t t0 = sg * seg, t1 = min(ntiles, t0 + seg);
     uint32_t codes[4], nxt[4];
+    if (MODE & 8) acc = Zero16();
     {
       const uint4 v = *reinterpret_cast<const uint4*>(tiles + (size_t(t0) * 64 + lane) * W);
       codes[0] = v.x; codes[1] = v.y; codes[2] = v.z; codes[3] = v.w;
     }
     for (uint32_t t = t0; t < t1; ++t) {
       const uint32_t tn = t + 1 < t1 ? t + 1 : t;
-      const uint4 v = *reinterpret_cast<const uint4*>(tiles + (size_t(tn) * 64 + lane) * W);
+      uint4 v;
+      if (MODE & 1) {
+        v = make_uint4(codes[0] ^ t, codes[1], codes[2], codes[3]);
+      } else {
+        v = *reinterpret_cast<const uint4*>(tiles + (size_t(tn) * 64 + lane) * W);
+      }
       constexpr int R = 3;
       v4i o[NB];
       int ix[NB];
@@ -127,11 +141,12 @@ __global__ void __launch_bounds__(768, 1) scan_cur(const uint8_t* __restrict__ t
         o[p] = grp_tab[Grp(codes, p)];
         ix[p] = pos_tab[Pos(codes, p)];
       }
-      v16i acc = Zero16();
+      if (!(MODE & 8)) acc = Zero16();
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        acc = __builtin_amdgcn_smfmac_i32_32x32x64_i8(o[s % NB], b[s], acc, ix[s % NB], 0, 0);
-        if (s + R < KS) {
+        acc = __builtin_amdgcn_smfmac_i32_32x32x64_i8(o[(MODE & 2) ? 0 : s % NB], b[s], acc,
+                                                      ix[(MODE & 2) ? 0 : s % NB], 0, 0);
+        if (!(MODE & 2) && s + R < KS) {
           o[(s + R) % NB] = grp_tab[Grp(codes, s + R)];
           ix[(s + R) % NB] = pos_tab[Pos(codes, s + R)];
         }
@@ -141,15 +156,23 @@ __global__ void __launch_bounds__(768, 1) scan_cur(const uint8_t* __restrict__ t
         for (int i = 0; i < 16; ++i)
           dump[(size_t(t) * 64 + c) * 32 + (i & 3) + 8 * (i >> 2) + 4 * h] = acc[i];
       }
-      const int m = Min16(acc);
-      const unsigned long long hb = __builtin_amdgcn_ballot_w64(m <= amax);
-      hits += __popcll(hb);
+      if (!(MODE & 8)) {
+        const int m = Min16(acc);
+        const unsigned long long hb = __builtin_amdgcn_ballot_w64(m <= amax);
+        hits += __popcll(hb);
+      }
       nxt[0] = v.x; nxt[1] = v.y; nxt[2] = v.z; nxt[3] = v.w;
 #pragma unroll
       for (int i = 0; i < 4; ++i) codes[i] = nxt[i];
     }
+    if (MODE & 8) hits += __popcll(__builtin_amdgcn_ballot_w64(Min16(acc) <= amax));
   }
-  if (lane == 0) out[wave] = hits;
+  if (lane == 0) {
+    out[wave] = hits;
+    // in-kernel clock: shader cycles over 100 MHz realtime ticks
+    const uint64_t ck1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    out[4096 + wave] = ((ck1 - ck0) << 24) | ((rt1 - rt0) & 0xFFFFFFull);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -259,6 +282,93 @@ __global__ void __launch_bounds__(64 * NWV, 1) scan_q64(const uint8_t* __restric
   if (lane == 0) out[wave] = hits;
 }
 
+// ---------------------------------------------------------------------------
+// p32: 32 slots, two accumulators in turn (tile t's test while tile t+1's
+// MFMAs run), codes two tiles ahead, NWV waves per CU
+// ---------------------------------------------------------------------------
+template <int NWV, int R, int NB, int EPI>
+__global__ void __launch_bounds__(64 * NWV, 1) scan_p32(const uint8_t* __restrict__ tiles,
+                                                        uint32_t ntiles,
+                                                        const int8_t* __restrict__ lut, int nq,
+                                                        int seg, int amax,
+                                                        unsigned long long* __restrict__ out,
+                                                        int* __restrict__ dump) {
+  __shared__ __align__(256) v4i grp_tab[16];
+  __shared__ int pos_tab[16];
+  Tables(grp_tab, pos_tab);
+  const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+  const uint32_t wave = blockIdx.x * NWV + (threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * NWV;
+  const uint32_t nseg = (ntiles + seg - 1) / seg;
+  unsigned long long hits = 0;
+  for (uint32_t sg = wave; sg < nseg; sg += nwaves) {
+    const uint32_t qa = (sg * 32 + c) % uint32_t(nq);
+    const v8i* bpa = reinterpret_cast<const v8i*>(lut + (size_t(qa) * K + h) * 32);
+    v8i ba[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) ba[s] = bpa[2 * s];
+    const uint32_t t0 = sg * seg, t1 = min(ntiles, t0 + seg);
+    auto ld = [&](uint32_t t, uint32_t* cd) {
+      const uint4 v = *reinterpret_cast<const uint4*>(tiles + (size_t(min(t, t1 - 1)) * 64 + lane) * W);
+      cd[0] = v.x; cd[1] = v.y; cd[2] = v.z; cd[3] = v.w;
+    };
+    uint32_t c0[4], c1[4];
+    ld(t0, c0);
+    ld(t0 + 1, c1);
+    v16i x0, y0;
+    bool pend = false;
+    uint32_t pt = 0;
+    auto epilogue = [&](v16i& p0, uint32_t t) {
+      XDL_READ_PAD(p0);
+      if (dump) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          dump[(size_t(t) * 64 + c) * 32 + (i & 3) + 8 * (i >> 2) + 4 * h] = p0[i];
+      }
+      const unsigned long long hb = __builtin_amdgcn_ballot_w64(Min16(p0) <= amax);
+      hits += __popcll(hb);
+    };
+    auto tile = [&](uint32_t* cd, uint32_t t, v16i& a0, v16i& p0) {
+      uint32_t cn[4];
+      ld(t + 2, cn);
+      v4i o[NB];
+      int ix[NB];
+#pragma unroll
+      for (int p = 0; p < R; ++p) {
+        o[p] = grp_tab[Grp(cd, p)];
+        ix[p] = pos_tab[Pos(cd, p)];
+      }
+      ZeroAcc(a0);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        SMFMAC_AB(a0, o[s % NB], ba[s], ix[s % NB]);
+        if (s + R < KS) {
+          o[(s + R) % NB] = grp_tab[Grp(cd, s + R)];
+          ix[(s + R) % NB] = pos_tab[Pos(cd, s + R)];
+        }
+        if (s == EPI && pend) epilogue(p0, pt);
+      }
+      pend = true;
+      pt = t;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) cd[i] = cn[i];
+    };
+    uint32_t t = t0;
+    for (; t + 1 < t1; t += 2) {
+      tile(c0, t, x0, y0);
+      tile(c1, t + 1, y0, x0);
+    }
+    if (t < t1) {
+      tile(c0, t, x0, y0);
+      epilogue(x0, t);
+    } else if (pend) {
+      epilogue(y0, t - 1);
+    }
+    pend = false;
+  }
+  if (lane == 0) out[wave] = hits;
+}
+
 static uint32_t Enc(uint32_t x0, uint32_t x1) {
   return ((x0 >> 2) | ((x1 >> 2) << 2)) | (((x0 & 3u) | ((x1 & 3u) << 2)) << 4);
 }
@@ -284,6 +394,7 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&d_tiles, h_tiles.size()));
   CHECK(hipMalloc(&d_lut, h_lut.size()));
   CHECK(hipMalloc(&d_out, sizeof(unsigned long long) * 8192));
+  CHECK(hipMemset(d_out, 0, sizeof(unsigned long long) * 8192));
   CHECK(hipMalloc(&d_dump, sizeof(int) * vt * 64 * 32));
   CHECK(hipMemcpy(d_tiles, h_tiles.data(), h_tiles.size(), hipMemcpyHostToDevice));
   CHECK(hipMemcpy(d_lut, h_lut.data(), h_lut.size(), hipMemcpyHostToDevice));
@@ -327,6 +438,11 @@ int main(int argc, char** argv) {
                      nq, seg, 0, d_out, d_dump);
   CHECK(hipDeviceSynchronize());
   bad += verify("q64", 64);
+  CHECK(hipMemset(d_dump, 0, sizeof(int) * vt * 64 * 32));
+  hipLaunchKernelGGL((scan_p32<8, 3, 4, 3>), dim3(cus), dim3(512), 0, 0, d_tiles, vt, d_lut, nq,
+                     seg, 0, d_out, d_dump);
+  CHECK(hipDeviceSynchronize());
+  bad += verify("p32", 32);
 
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
@@ -345,15 +461,32 @@ int main(int argc, char** argv) {
     ms /= reps;
     // MFMA-bound time: smfmac x 32 cycles over 4 * cus SIMDs at 2.4 GHz
     const double bound_ms = smfmac * 32.0 / (4.0 * cus) / 2.4e9 * 1e3;
-    std::printf("%-26s %8.2f us  %.1f cycles per smfmac per SIMD  MFMA bound %.2f us  frac %.3f\n",
+    // median in-kernel clock of the last launch's waves (scan_cur only)
+    std::vector<unsigned long long> ck(4096);
+    CHECK(hipMemcpy(ck.data(), d_out + 4096, 4096 * 8, hipMemcpyDeviceToHost));
+    std::vector<double> mhz;
+    for (auto v : ck) {
+      const double cyc = double(v >> 24), rt = double(v & 0xFFFFFFull);
+      if (rt > 0) mhz.push_back(cyc / rt * 100.0);
+    }
+    std::sort(mhz.begin(), mhz.end());
+    const double clk = mhz.empty() ? 0.0 : mhz[mhz.size() / 2];
+    std::printf("%-26s %8.2f us  %.1f cycles per smfmac per SIMD at 2.4 GHz  MFMA bound %.2f us  "
+                "frac %.3f  in-kernel clock %.0f MHz (%.1f cycles per smfmac)\n",
                 name, ms * 1e3, ms * 1e-3 * 2.4e9 * 4.0 * cus / smfmac, bound_ms * 1e3,
-                bound_ms / ms);
+                bound_ms / ms, clk, ms * 1e-3 * clk * 1e6 * 4.0 * cus / smfmac);
+    CHECK(hipMemset(d_out + 4096, 0, 4096 * 8));
   };
   const double sm = double(ntiles) * KS;   // cur: ntiles x 32 slots; q64: ntiles/2 x 64
 #define CUR(NB, NAME)                                                                         \
   timeit(NAME, [&] {                                                                          \
     hipLaunchKernelGGL(scan_cur<NB>, dim3(cus), dim3(768), 0, 0, d_tiles, ntiles, d_lut, nq, seg, \
                        amax, d_out, nullptr);                                                 \
+  }, sm)
+#define CURM(MODE, NAME)                                                                      \
+  timeit(NAME, [&] {                                                                          \
+    hipLaunchKernelGGL((scan_cur<3, MODE>), dim3(cus), dim3(768), 0, 0, d_tiles, ntiles, d_lut, nq, \
+                       seg, amax, d_out, nullptr);                                            \
   }, sm)
 #define CUR1(NB, NAME)                                                                        \
   timeit(NAME, [&] {                                                                          \
@@ -365,14 +498,22 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL((scan_q64<4, R, NB, ONLY>), dim3(cus), dim3(256), 0, 0, d_tiles, ntiles / 2, \
                        d_lut, nq, seg, amax, d_out, nullptr);                                 \
   }, sm)
+#define P32(NWV, R, NB, EPI, NAME)                                                            \
+  timeit(NAME, [&] {                                                                          \
+    hipLaunchKernelGGL((scan_p32<NWV, R, NB, EPI>), dim3(cus), dim3(64 * NWV), 0, 0, d_tiles,   \
+                       ntiles, d_lut, nq, seg, amax, d_out, nullptr);                         \
+  }, sm)
   CUR(3, "cur R3 NB3 (product)");
-  CUR(4, "cur R3 NB4");
-  CUR1(3, "cur 1 wave/SIMD NB3");
-  CUR1(4, "cur 1 wave/SIMD NB4");
+  P32(8, 3, 4, 3, "p32 2/SIMD R3 NB4 E3");
+  P32(8, 4, 5, 3, "p32 2/SIMD R4 NB5 E3");
+  P32(8, 2, 3, 2, "p32 2/SIMD R2 NB3 E2");
+  P32(8, 3, 4, 6, "p32 2/SIMD R3 NB4 E6");
+  P32(12, 2, 3, 2, "p32 3/SIMD R2 NB3 E2");
+  P32(4, 4, 5, 3, "p32 1/SIMD R4 NB5 E3");
+  CURM(7, "cur MFMA only");
+  CURM(15, "cur MFMA chain, no test");
+  CURM(8, "cur no per-tile test");
   Q64(2, 2, false, "q64 R2 NB2");
-  Q64(2, 3, false, "q64 R2 NB3");
-  Q64(3, 4, false, "q64 R3 NB4");
-  Q64(2, 4, false, "q64 R2 NB4");
   Q64(2, 2, true, "q64 mfma only");
   CHECK(hipGetLastError());
   std::printf("tiles %u seg %d CUs %d\n", ntiles, seg, cus);
