@@ -693,23 +693,95 @@ static int32_t SpillK(const IndexView& v, int32_t k) {
 // (asymmetric_hashing_impl.h:207-219) of the global epsilon, then
 // min(., int16 max - 1) + 1 (querying.h:413-423), narrowed to int16 by the
 // FastTopNeighbors<int16_t> constructor.
-static int16_t LeafInt16Epsilon(float eps, float mult) {
+static int32_t FixedPointMaxDistance(float eps, float mult) {
   constexpr int32_t kI32Max = std::numeric_limits<int32_t>::max();
-  int32_t e;
-  if (eps == kInf) {
-    e = kI32Max;
-  } else {
-    const float x = eps * mult;
-    if (x >= static_cast<float>(kI32Max)) {
-      e = kI32Max;
-    } else {
-      const float f = std::floor(x);
-      e = f < -2147483648.0f ? std::numeric_limits<int32_t>::min() : static_cast<int32_t>(f);
-    }
-  }
-  e = std::min<int32_t>(e, std::numeric_limits<int16_t>::max() - 1) + 1;
+  if (eps == kInf) return kI32Max;
+  const float x = eps * mult;
+  if (x >= static_cast<float>(kI32Max)) return kI32Max;
+  const float f = std::floor(x);
+  return f < -2147483648.0f ? std::numeric_limits<int32_t>::min() : static_cast<int32_t>(f);
+}
+
+static int16_t LeafInt16Epsilon(float eps, float mult) {
+  const int32_t e =
+      std::min<int32_t>(FixedPointMaxDistance(eps, mult), std::numeric_limits<int16_t>::max() - 1) + 1;
   return static_cast<int16_t>(e);
 }
+
+// One leaf of pipeline B through GetTopInt16DistancesImpl with one query
+// (lut16_avx2.inc:308-389): FastTopNeighbors<int16_t>(k, eps16) over the raw
+// sums, pushing iff sum < threshold, the threshold re-read after every GC;
+// FinishUnsorted's contents (storage order) into `local` as (leaf-local
+// index, int16 sum).
+static void LeafInt16TopN(const orc_index* ix, int leaf, const Lut& lut, size_t k, int16_t eps16,
+                          std::vector<std::pair<uint32_t, int16_t>>* local) {
+  const int nb = ix->num_blocks;
+  const uint64_t beg = ix->leaf_offsets[leaf];
+  const uint32_t n = uint32_t(ix->leaf_offsets[leaf + 1] - beg);
+  local->clear();
+  if (n == 0 || k == 0) return;
+  FastTopNT<int16_t> lt(k, eps16);
+  int32_t thr = lt.epsilon();
+  int32_t acc[32];
+  const uint32_t groups = (n + 31) / 32;
+  for (uint32_t g = 0; g < groups; ++g) {
+    const int lanes = (g == groups - 1) ? int(n - 32 * g) : 32;
+    for (int l = 0; l < lanes; ++l)
+      acc[l] = Accumulate(ix->member_codes + (beg + 32 * g + l) * nb, nb, lut.u8.data());
+    auto push_mask = [&]() {
+      uint32_t pm = 0;
+      for (int l = 0; l < lanes; ++l) pm |= uint32_t(acc[l] < thr) << l;
+      return pm;
+    };
+    uint32_t pm = push_mask();
+    while (pm) {
+      const int l = Ctz(pm);
+      pm &= pm - 1;
+      if (lt.Push(32 * g + l, static_cast<int16_t>(acc[l]))) {
+        lt.GarbageCollectApprox();
+        thr = lt.epsilon();
+        pm &= push_mask();
+      }
+    }
+  }
+  lt.Finish(local);
+}
+
+// TopNeighbors<float> (top_n_amortized_constant.h:34-140): elements kept
+// unsorted up to 2 * limit, then partitioned to the exact best `limit` under
+// (distance, index) with approx_bottom = the limit-th; while fewer than
+// `limit` are held, approx_bottom tracks the worst pushed.
+class TopNeighborsF {
+ public:
+  explicit TopNeighborsF(size_t limit) : limit_(limit) {}
+  void Push(uint32_t i, float d) {
+    const std::pair<uint32_t, float> e{i, d};
+    if (el_.size() < limit_) {
+      if (el_.empty() || NNLess(bottom_, e)) bottom_ = e;
+      el_.push_back(e);
+    } else if (NNLess(e, bottom_)) {
+      el_.push_back(e);
+      if (el_.size() >= 2 * limit_) Partition();
+    }
+  }
+  bool Full() const { return el_.size() >= limit_; }
+  float ApproxBottomDistance() const { return bottom_.second; }
+  void TakeUnsorted(NN* out) {
+    if (el_.size() > limit_) Partition();
+    *out = std::move(el_);
+    el_.clear();
+  }
+
+ private:
+  void Partition() {
+    std::nth_element(el_.begin(), el_.begin() + (limit_ - 1), el_.end(), NNLess);
+    el_.resize(limit_);
+    bottom_ = el_.back();
+  }
+  size_t limit_;
+  std::vector<std::pair<uint32_t, float>> el_;
+  std::pair<uint32_t, float> bottom_{0, 0.0f};
+};
 
 // Pipeline B emulate mode (A.9): the replay of one query through
 // TreeXHybridSMMD::FindNeighborsPreTokenizedBatchedOptimizedImpl
@@ -725,45 +797,18 @@ static int16_t LeafInt16Epsilon(float eps, float mult) {
 // are pushed in storage order into the global FastTopNeighbors<float> iff
 // d <= epsilon (SingleMachineSearcherBase::FindNeighborsBatchedImpl,
 // single_machine_base.cc:759-808), local ids mapped to global ids.
-// The generic per-query path (nq * L < num_leaves) is not restated.
+// The generic per-query path (nq * L < num_leaves) is PipelineBGeneric.
 static void PipelineBEmulate(const IndexView& v, const std::vector<int>& leaves,
                              const Lut& lut, float inv, int32_t kk, NN* out) {
   const orc_index* ix = v.ix;
-  const int nb = ix->num_blocks;
   std::vector<int> ord(leaves);
   std::sort(ord.begin(), ord.end());
   const size_t k = size_t(std::max(kk, 0));
   FastTopN top(k);  // pre_reordering_epsilon = +inf
   std::vector<std::pair<uint32_t, int16_t>> local;
-  int32_t acc[32];
   for (int leaf : ord) {
     const uint64_t beg = ix->leaf_offsets[leaf];
-    const uint32_t n = uint32_t(ix->leaf_offsets[leaf + 1] - beg);
-    if (n == 0 || k == 0) continue;
-    FastTopNT<int16_t> lt(k, LeafInt16Epsilon(top.epsilon(), lut.mult));
-    int32_t thr = lt.epsilon();
-    const uint32_t groups = (n + 31) / 32;
-    for (uint32_t g = 0; g < groups; ++g) {
-      const int lanes = (g == groups - 1) ? int(n - 32 * g) : 32;
-      for (int l = 0; l < lanes; ++l)
-        acc[l] = Accumulate(ix->member_codes + (beg + 32 * g + l) * nb, nb, lut.u8.data());
-      auto push_mask = [&]() {
-        uint32_t pm = 0;
-        for (int l = 0; l < lanes; ++l) pm |= uint32_t(acc[l] < thr) << l;
-        return pm;
-      };
-      uint32_t pm = push_mask();
-      while (pm) {
-        const int l = Ctz(pm);
-        pm &= pm - 1;
-        if (lt.Push(32 * g + l, static_cast<int16_t>(acc[l]))) {
-          lt.GarbageCollectApprox();
-          thr = lt.epsilon();
-          pm &= push_mask();
-        }
-      }
-    }
-    lt.Finish(&local);
+    LeafInt16TopN(ix, leaf, lut, k, LeafInt16Epsilon(top.epsilon(), lut.mult), &local);
     float eps = top.epsilon();
     for (const auto& e : local) {
       const float d = static_cast<float>(e.second) * inv;
@@ -776,9 +821,45 @@ static void PipelineBEmulate(const IndexView& v, const std::vector<int>& leaves,
   top.Finish(out);
 }
 
-// One query's pre-reorder candidates (global ids), unsorted.
+// Pipeline B emulate mode, the generic per-query path the reference takes
+// when nq * leaves_to_search < num_leaves
+// (TreeXHybridSMMD::FindNeighborsPreTokenizedBatchedGenericImpl,
+// tree_x_hybrid_smmd.cc:669-691 -> FindNeighborsPreTokenizedImpl, :875-1028):
+// the query's tokens in top-L order (sequential ParallelFor without a pool);
+// per leaf the leaf searcher's single-query LUT16 path
+// (FindApproximateNeighborsForceLUT16, querying.h:711-734): no results when
+// the fixed-point max distance of the forwarded epsilon is below int16 min,
+// else FindApproxNeighborsFastTopNeighbors<1> (:402-459) -- the per-leaf int16
+// FastTopNeighbors -- with the results scaled by 1.0f / mult; every result,
+// mapped to its global id, pushed into one TopNeighbors<float>(k'); once it
+// is full the next leaf's epsilon is its approx_bottom (:1004-1010).
+static void PipelineBGeneric(const IndexView& v, const std::vector<int>& leaves,
+                             const Lut& lut, float inv, int32_t kk, NN* out) {
+  const orc_index* ix = v.ix;
+  out->clear();
+  const size_t k = size_t(std::max(kk, 0));
+  if (k == 0 || leaves.empty()) return;
+  TopNeighborsF top(k);
+  float eps = kInf;  // pre_reordering_epsilon
+  std::vector<std::pair<uint32_t, int16_t>> local;
+  for (int leaf : leaves) {
+    if (FixedPointMaxDistance(eps, lut.mult) < std::numeric_limits<int16_t>::min()) {
+      local.clear();
+    } else {
+      LeafInt16TopN(ix, leaf, lut, k, LeafInt16Epsilon(eps, lut.mult), &local);
+    }
+    const uint64_t beg = ix->leaf_offsets[leaf];
+    for (const auto& e : local)
+      top.Push(ix->leaf_members[beg + e.first], static_cast<float>(e.second) * inv);
+    if (top.Full()) eps = top.ApproxBottomDistance();
+  }
+  top.TakeUnsorted(out);
+}
+
+// One query's pre-reorder candidates (global ids), unsorted.  `generic`:
+// pipeline B's emulate mode takes the per-query path (PipelineBGeneric).
 static void QueryPreReorder(const IndexView& v, const float* q, int L,
-                            int pre_nn, int mode, std::vector<float>* scratch,
+                            int pre_nn, int mode, bool generic, std::vector<float>* scratch,
                             NN* out) {
   const orc_index* ix = v.ix;
   const int nl = ix->num_leaves, nb = ix->num_blocks, dim = ix->dim;
@@ -858,6 +939,8 @@ static void QueryPreReorder(const IndexView& v, const float* q, int L,
       p.first = ix->leaf_members[ix->leaf_offsets[leaf] + local];
     }
     *out = std::move(res);
+  } else if (mode == ORC_MODE_EMULATE && !residual && generic) {
+    PipelineBGeneric(v, leaves, lut, inv, kk, out);
   } else if (mode == ORC_MODE_EMULATE && !residual) {
     PipelineBEmulate(v, leaves, lut, inv, kk, out);
   } else {
@@ -929,11 +1012,15 @@ static int SearchImpl(const orc_index* ix, const float* queries, int nq,
   // scann.cc:406-430: without reordering pre_nn = final_nn.
   const int pnn = reorder ? pre_nn : final_nn;
   const int width = pre_only ? pnn : final_nn;
+  // tree_x_hybrid_smmd.cc:660-667: the generic per-query path when the
+  // batch's tokens number fewer than the leaves
+  const bool generic =
+      uint64_t(nq) * uint64_t(std::min(leaves, ix->num_leaves)) < uint64_t(ix->num_leaves);
   ParallelFor(nq, nthreads, [&](int qi) {
     std::vector<float> scratch;
     const float* q = queries + size_t(qi) * ix->dim;
     NN r;
-    QueryPreReorder(v, q, leaves, pnn, mode, &scratch, &r);
+    QueryPreReorder(v, q, leaves, pnn, mode, generic, &scratch, &r);
     if (pre_only) {
       std::sort(r.begin(), r.end(), NNLess);
     } else {

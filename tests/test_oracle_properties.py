@@ -150,3 +150,42 @@ def test_emulate_pipeline_b_tight_epsilon(oracle):
         lut = dict(zip(wi[r, :wc[r]].tolist(), wd[r, :wc[r]].view(np.uint32).tolist()))
         for i, d in zip(ei[r].tolist(), ed[r].view(np.uint32).tolist()):
             assert lut[i] == d
+
+
+def test_emulate_pipeline_b_generic_path(oracle):
+    """The reference's per-query path for small batches (nq * L < num_leaves,
+    tree_x_hybrid_smmd.cc:660-667, 669-691, 875-1028): leaves in top-L
+    order, per-leaf int16 FastTopNeighbors, one TopNeighbors<float> per
+    query forwarding its approx_bottom.  Against the ideal exact top-k':
+    same counts, every emulate distance a genuine LUT16 distance of its id,
+    the k'-th never smaller, and the id mismatch below the reference's 1e-3
+    tolerance between its search modes."""
+    ix, db, q = _pipeline_b()
+    for nq, L, k in ((3, 8, 100), (7, 8, 10), (1, 40, 5)):
+        assert nq * L < ix.num_leaves          # the generic branch
+        qq = q[:nq]
+        ii, idist, ic = oracle.search_pre_reorder(ix, qq, L, k, oracle.MODE_IDEAL)
+        ei, ed, ec = oracle.search_pre_reorder(ix, qq, L, k, oracle.MODE_EMULATE)
+        np.testing.assert_array_equal(ic, ec)
+        assert np.all(ed[:, -1] >= idist[:, -1])
+        mism = float(np.mean([len(set(a) ^ set(b)) / (2 * len(a)) for a, b in zip(ii, ei)]))
+        assert mism < 1e-3
+        wi, wd, wc = oracle.search_pre_reorder(ix, qq, L, 20000, oracle.MODE_IDEAL)
+        for r in range(nq):
+            assert len(set(ei[r].tolist())) == ec[r]
+            lut = dict(zip(wi[r, :wc[r]].tolist(), wd[r, :wc[r]].view(np.uint32).tolist()))
+            for i, d in zip(ei[r, :ec[r]].tolist(), ed[r, :ec[r]].view(np.uint32).tolist()):
+                assert lut[i] == d
+
+
+def test_emulate_pipeline_b_generic_tight_epsilon(oracle):
+    """Generic path with k' = 5 over 32 leaves of one query: the forwarded
+    epsilon is the TopNeighbors approx_bottom (not FastTopNeighbors'), so
+    later leaves see tight int16 epsilons; results stay k' distinct genuine
+    candidates and agree with the ideal top-k' here."""
+    ix, db, q = _pipeline_b(n=12000, leaves=64, seed=4)
+    qq = q[:1]
+    ei, ed, ec = oracle.search_pre_reorder(ix, qq, 32, 5, oracle.MODE_EMULATE)
+    ii, idist, ic = oracle.search_pre_reorder(ix, qq, 32, 5, oracle.MODE_IDEAL)
+    assert ec[0] == 5 and len(set(ei[0].tolist())) == 5
+    assert set(ei[0].tolist()) == set(ii[0].tolist())
