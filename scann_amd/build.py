@@ -87,6 +87,19 @@ DIAG_OUT = os.path.join(ROOT, "scann_amd", "lib", "libscann_mi355x_diag.so")
 DIAG_DEFINES = ("SMX_DEBUG_CHECKS", "SMX_SCAN_DIAGNOSTICS", "SMX_PHASE_STAMPS")
 
 
+TIME_OUT = os.path.join(ROOT, "scann_amd", "lib", "libscann_mi355x_time.so")
+# The timing library: the scan ablations/stamps and the phase stamps without
+# the device index checks (whose extra registers and branches change the
+# kernels' occupancy and timing); loaded through $SMX_LIB by tools/ only.
+TIME_DEFINES = ("SMX_SCAN_DIAGNOSTICS", "SMX_PHASE_STAMPS")
+
+
+def build_time(force: bool = False, verbose: bool = False) -> str:
+    if not force and os.path.exists(TIME_OUT) and not needs_build_for(TIME_OUT):
+        return TIME_OUT
+    return build(force=True, verbose=verbose, defines=TIME_DEFINES, out=TIME_OUT)
+
+
 def build_diag(force: bool = False, verbose: bool = False) -> str:
     if not force and os.path.exists(DIAG_OUT) and not needs_build_for(DIAG_OUT):
         return DIAG_OUT
@@ -102,6 +115,9 @@ def needs_build_for(out: str) -> bool:
 if __name__ == "__main__":
     if "--diag" in sys.argv:
         print(build_diag(force="--force" in sys.argv, verbose=True))
+        sys.exit(0)
+    if "--time" in sys.argv:
+        print(build_time(force="--force" in sys.argv, verbose=True))
         sys.exit(0)
     print(build(force="--force" in sys.argv, verbose=True))
     print(build_pybind(force="--force" in sys.argv, verbose=True))

@@ -1690,7 +1690,9 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
 // end, its result consumed after the next segment's first tile).
 // ABL = 4: timing ablation without the epilogue; ABL = 2: with the hit test
 // but no hit list; ABL = 16: with hit lists and drains but no copy to the
-// candidate lists (results invalid for all three).
+// candidate lists; ABL = 32: every tile of a segment computed from its first
+// tile's codes (cache-hot: the code loads' latency out of the loop); results
+// invalid for all four.
 // ---------------------------------------------------------------------------
 
 constexpr int kHitsPerWave = 64;   // a tile adds at most one hit per lane
@@ -2105,6 +2107,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       // loads: no 64-bit per-lane pointers live across the tile loop)
       const uint8_t* tseg = a.tiles + toff * 64ull * W;
       auto tile_ptr = [&](uint32_t t) {
+        if (ABL & 32) t = j;   // timing ablation: every tile's codes = the first one's (cache-hot)
         return tseg + size_t(t * uint32_t(64 * W) + uint32_t(lane) * uint32_t(W));
       };
       // LUT rows 4s + 2h, 4s + 2h + 1 of query c (32 bytes) per sparse step
@@ -3341,6 +3344,9 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
                          0, s, a);                                                         \
     else if (variant == 8)                                                                 \
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 8>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
+                         0, s, a);                                                         \
+    else if (variant == 32)                                                                \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 32>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
                          0, s, a);                                                         \
     else                                                                                   \
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()), \

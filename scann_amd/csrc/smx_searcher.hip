@@ -1269,9 +1269,9 @@ int smx_set_tuning(smx_index* h, int32_t candidates_per_query, int32_t seed_leav
   if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
 #ifdef SMX_SCAN_DIAGNOSTICS
   if (scan_variant != 0 && scan_variant != 2 && scan_variant != 4 && scan_variant != 8 &&
-      scan_variant != 16)
+      scan_variant != 16 && scan_variant != 32)
     return Fail(SMX_INVALID_ARGUMENT,
-                "scan_variant is 0 (scan), 2 / 4 / 16 (timing ablations) or 8 (diagnostic stamps)");
+                "scan_variant is 0 (scan), 2 / 4 / 16 / 32 (timing ablations) or 8 (diagnostic stamps)");
 #else
   if (scan_variant != 0)
     return Fail(SMX_INVALID_ARGUMENT,

@@ -1,9 +1,9 @@
 """Phase timeline of the front-end and select kernels (diagnostic build).
 
-    python tools/phase_stamps.py build     (here: compiles lib/libscann_mi355x_diag.so)
+    python tools/phase_stamps.py build     (here: compiles lib/libscann_mi355x_time.so)
     python tools/phase_stamps.py [seed]    (on the GPU box)
 
-The diagnostic library (-DSMX_PHASE_STAMPS, scann_amd/build.py build_diag) writes the 100 MHz clock at phase boundaries
+The diagnostic library (-DSMX_PHASE_STAMPS, scann_amd/build.py build_time) writes the 100 MHz clock at phase boundaries
 of topl_wave_kernel (0), seed_tau_kernel (1) and final_select_rank_kernel (2)
 per query; this prints each phase's duration and where the kernels' spans go.
 """
@@ -14,7 +14,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-LIB = os.path.join(ROOT, "scann_amd", "lib", "libscann_mi355x_diag.so")
+LIB = os.path.join(ROOT, "scann_amd", "lib", "libscann_mi355x_time.so")
 NAMES = {0: ("topl_wave", ["load", "rounds", "compact+rank", "out+rank atomics", "lut"]),
          1: ("seed_tau", ["lut+prefix", "score loop", "k'-th select"]),
          2: ("final_select", ["load+narrow", "rank", "gid gather", "dedupe", "exact", "out"])}
@@ -23,7 +23,7 @@ NAMES = {0: ("topl_wave", ["load", "rounds", "compact+rank", "out+rank atomics",
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "build":
         from scann_amd import build
-        print(build.build_diag(force=True))
+        print(build.build_time(force=True))
         return
     seed = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     os.environ["SMX_LIB"] = LIB

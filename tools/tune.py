@@ -11,7 +11,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 # the scan variants other than 0 exist only in the diagnostic library
 os.environ.setdefault("SMX_LIB", os.path.join(os.path.dirname(os.path.dirname(
-    os.path.abspath(__file__))), "scann_amd", "lib", "libscann_mi355x_diag.so"))
+    os.path.abspath(__file__))), "scann_amd", "lib", "libscann_mi355x_time.so"))
 import torch  # noqa: E402
 
 from bench import LEAVES_TO_SEARCH, NQ, PRE_NN, FINAL_NN, build_index  # noqa: E402
