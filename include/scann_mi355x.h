@@ -250,6 +250,54 @@ int smx_nearest_centers(const float* d_x, int64_t n, int32_t d, const float* d_c
                         int32_t k, const int32_t* d_primary, float lambda, int32_t* d_out,
                         float* d_out_loss, void* stream);
 
+/* The rest of the index build on the device (scann_amd/device_builder.py
+ * drives them; device buffers, enqueued on `stream`):
+ *
+ * smx_block_encode: codes[i][b] = the nearest of block b's 16 codebook
+ *   centers to rows[i]'s block b (squared L2 over the block's coordinates in
+ *   order, the last block zero-padded, ties to the lowest center) -- the AH
+ *   encoding of IndexDatapoint (asymmetric_hashing_impl.cc).  rows [n][dim],
+ *   codebook [nb][16][dpb] float32, codes [n][nb] uint8.
+ * smx_avq_encode: the anisotropic noise-shaped codes of
+ *   IndexDatapointNoiseShaped (asymmetric_hashing_impl.cc:434-503) with the
+ *   given noise_shaping_threshold: residuals and the datapoints themselves
+ *   [n][dim]; double precision, bit for bit the oracle's orc_avq_encode.
+ * smx_kmeans_accumulate / smx_kmeans_finalize: the k-means mean step
+ *   (gmm_utils.cc:539-1318) as exact fixed-point sums: sums[label][j] +=
+ *   llrint(x[i][j] * scale), counts[label]++ (int64 / uint32 device arrays
+ *   zeroed by the caller; scale a power of two small enough that no sum
+ *   overflows), then centers[c] = sums[c] / scale / counts[c] for every
+ *   non-empty c (empty centers keep their values).  Order-independent, so
+ *   deterministic run to run.
+ * smx_codebook_accumulate: the same mean step for all blocks' 16-center
+ *   codebooks at once (asymmetric_hashing_impl.cc:41-198): sums[nb][16][dpb],
+ *   counts[nb][16], from rows [n][dim] and their codes [n][nb].
+ * smx_group_by_leaf: members by (leaf, id) -- datapoints_by_token
+ *   (kmeans_tree_partitioner.cc:477-620) -- from m (label, id) pairs: keys
+ *   [2 m] uint64 scratch, offsets [k + 1] uint64, members [m] uint32,
+ *   member_leaf [m] int32.  Call first with temp = NULL to get temp_bytes.
+ * smx_gather_residuals: out[i] = x[rows[i] - row_base] - centers[leaf[i]]
+ *   (float32), or the row itself when centers is NULL. */
+int smx_block_encode(const float* d_rows, int64_t n, int32_t dim, const float* d_codebook,
+                     int32_t num_blocks, int32_t dims_per_block, uint8_t* d_codes, void* stream);
+int smx_avq_encode(const float* d_residuals, const float* d_datapoints, int64_t n, int32_t dim,
+                   const float* d_codebook, int32_t num_blocks, int32_t dims_per_block,
+                   double threshold, uint8_t* d_codes, void* stream);
+int smx_kmeans_accumulate(const float* d_x, int64_t n, int32_t d, const int32_t* d_label,
+                          int32_t k, double scale, uint64_t* d_sums, uint32_t* d_counts,
+                          void* stream);
+int smx_kmeans_finalize(const uint64_t* d_sums, const uint32_t* d_counts, int32_t k, int32_t d,
+                        double scale, float* d_centers, void* stream);
+int smx_codebook_accumulate(const float* d_rows, int64_t n, int32_t dim, const uint8_t* d_codes,
+                            int32_t num_blocks, int32_t dims_per_block, double scale,
+                            uint64_t* d_sums, uint32_t* d_counts, void* stream);
+int smx_group_by_leaf(const int32_t* d_labels, const uint32_t* d_ids, int64_t m, int32_t k,
+                      void* d_temp, size_t* temp_bytes, uint64_t* d_keys, uint64_t* d_offsets,
+                      uint32_t* d_members, int32_t* d_member_leaf, void* stream);
+int smx_gather_residuals(const float* d_x, int32_t d, const uint32_t* d_rows,
+                         const int32_t* d_leaf, const float* d_centers, int64_t m,
+                         int64_t row_base, float* d_out, void* stream);
+
 /* ---- diagnostics ---------------------------------------------------------- */
 int smx_set_profiling(smx_index* index, int32_t enabled);
 int smx_get_timings(const smx_index* index, smx_timings* out);

@@ -65,6 +65,19 @@ SIGNATURES = {
     "smx_merge_shards_device": (ctypes.c_int, [_vp, _i32, _i32, ctypes.POINTER(SearchParams), _vp, _vp, _vp, _vp, _vp]),
     "smx_nearest_centers": (ctypes.c_int, [_vp, ctypes.c_int64, _i32, _vp, _i32, _vp,
                                            ctypes.c_float, _vp, _vp, _vp]),
+    "smx_block_encode": (ctypes.c_int, [_vp, ctypes.c_int64, _i32, _vp, _i32, _i32, _vp, _vp]),
+    "smx_avq_encode": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _i32, _vp, _i32, _i32,
+                                      ctypes.c_double, _vp, _vp]),
+    "smx_kmeans_accumulate": (ctypes.c_int, [_vp, ctypes.c_int64, _i32, _vp, _i32,
+                                             ctypes.c_double, _vp, _vp, _vp]),
+    "smx_kmeans_finalize": (ctypes.c_int, [_vp, _vp, _i32, _i32, ctypes.c_double, _vp, _vp]),
+    "smx_codebook_accumulate": (ctypes.c_int, [_vp, ctypes.c_int64, _i32, _vp, _i32, _i32,
+                                               ctypes.c_double, _vp, _vp, _vp]),
+    "smx_group_by_leaf": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _i32, _vp,
+                                         ctypes.POINTER(ctypes.c_size_t), _vp, _vp, _vp, _vp,
+                                         _vp]),
+    "smx_gather_residuals": (ctypes.c_int, [_vp, _i32, _vp, _vp, _vp, ctypes.c_int64,
+                                            ctypes.c_int64, _vp, _vp]),
     "smx_last_error": (ctypes.c_char_p, []),
     "smx_version": (ctypes.c_char_p, []),
 }

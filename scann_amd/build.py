@@ -11,7 +11,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "scann_amd", "csrc")
 OUT = os.path.join(ROOT, "scann_amd", "lib", "libscann_mi355x.so")
-SOURCES = ["smx_kernels.hip", "smx_searcher.hip", "smx_builder.hip"]
+SOURCES = ["smx_kernels.hip", "smx_searcher.hip", "smx_builder.hip", "smx_sort.hip"]
 HEADERS = ["smx_internal.h", os.path.join("..", "..", "include", "scann_mi355x.h")]
 ARCH = os.environ.get("SMX_OFFLOAD_ARCH", "gfx950")
 

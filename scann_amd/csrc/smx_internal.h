@@ -356,6 +356,29 @@ bool FinalSelectFits(const SelectArgs& a);
 hipError_t LaunchNearestCenters(const float* x, int64_t n, int d, const float* centers, int k,
                                 const int32_t* primary, float lambda, int32_t* out,
                                 float* out_loss, hipStream_t s);
+// Index-build kernels (smx_builder.hip, smx_sort.hip).
+hipError_t LaunchBlockEncode(const float* r, int64_t n, int dim, const float* cb, int nb, int dpb,
+                             uint8_t* out, hipStream_t s);
+hipError_t LaunchKmeansAccumulate(const float* x, int64_t n, int d, const int32_t* label, int k,
+                                  double scale, unsigned long long* sums, uint32_t* counts,
+                                  hipStream_t s);
+hipError_t LaunchKmeansFinalize(const unsigned long long* sums, const uint32_t* counts, int k,
+                                int d, double scale, float* centers, hipStream_t s);
+size_t CodebookAccumulateLds(int nb, int dpb);
+hipError_t LaunchCodebookAccumulate(const float* r, int64_t n, int dim, const uint8_t* codes,
+                                    int nb, int dpb, double scale, unsigned long long* sums,
+                                    uint32_t* counts, hipStream_t s);
+size_t AvqEncodeLds(int nb, int dpb);
+hipError_t LaunchAvqEncode(const float* resid, const float* orig, int64_t n, int dim,
+                           const float* cb, int nb, int dpb, double threshold, uint8_t* out,
+                           hipStream_t s);
+// Members grouped by leaf: sort (leaf, id) pairs, then the leaf offsets.
+hipError_t GroupByLeaf(const int32_t* labels, const uint32_t* ids, int64_t m, int k, void* temp,
+                       size_t* temp_bytes, uint64_t* keys, uint64_t* offsets, uint32_t* members,
+                       int32_t* member_leaf, hipStream_t s);
+hipError_t LaunchGatherResiduals(const float* x, int d, const uint32_t* rows, const int32_t* leaf,
+                                 const float* centers, int64_t m, int64_t row_base, float* out,
+                                 hipStream_t s);
 hipError_t LaunchMergeShards(const MergeArgs& a, hipStream_t s);
 hipError_t LaunchExactDistances(const DeviceIndex& ix, const float* queries, int nq,
                                 const uint32_t* ids, int k, float* out, hipStream_t s);

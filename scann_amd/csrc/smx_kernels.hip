@@ -1611,7 +1611,7 @@ __global__ void __launch_bounds__(256, 4) topl_seed_kernel(const float* __restri
 // position nibble (x0 & 3 in fields 0..7, x1 & 3 in fields 8..15), each
 // address two VALU ops; a 256-entry table of both spent 60% of the LDS
 // cycles in bank conflicts.
-template <int K, int R>
+template <int K, int R, bool NOLDS = false>
 __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)[K / 2],
                                            const v4i* grp_tab, const int* pos_tab) {
   constexpr int KS = K / 2;
@@ -1619,12 +1619,21 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
   auto pos = [&](int t) { return (codes[t >> 2] >> ((t & 3) * 8 + 4)) & 0xFu; };
   v4i o[R];
   int ix[R];
+  // NOLDS (timing ablation, results invalid): operands straight from the
+  // code registers (one VALU each), no LDS table reads in the chain
+  auto ld = [&](int slot, int t) {
+    if constexpr (NOLDS) {
+      const int w = int(codes[t >> 2] >> ((t & 3) * 8));
+      o[slot] = v4i{w & 0x00010001, 0, w & 0x01000100, 0};
+      ix[slot] = w;
+    } else {
+      o[slot] = grp_tab[grp(t)];
+      ix[slot] = pos_tab[pos(t)];
+    }
+  };
 #pragma unroll
   for (int p = 0; p < R; ++p)
-    if (p < KS) {
-      o[p] = grp_tab[grp(p)];
-      ix[p] = pos_tab[pos(p)];
-    }
+    if (p < KS) ld(p, p);
   // zeroed as 8 x v_mov_b64 (the plain v16i{0} became 16 v_mov_b32 plus a
   // chain of 8 register-shifting v_mov_b64 copies per tile)
   typedef long long v8l __attribute__((ext_vector_type(8)));
@@ -1639,10 +1648,7 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     acc = __builtin_amdgcn_smfmac_i32_32x32x64_i8(o[s % R], b[s], acc, ix[s % R], 0, 0);
-    if (s + R < KS) {
-      o[s % R] = grp_tab[grp(s + R)];
-      ix[s % R] = pos_tab[pos(s + R)];
-    }
+    if (s + R < KS) ld(s % R, s + R);
   }
   __builtin_amdgcn_sched_group_barrier(0x100, 2 * R, 0);
 #pragma unroll
@@ -1691,8 +1697,9 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
 // ABL = 4: timing ablation without the epilogue; ABL = 2: with the hit test
 // but no hit list; ABL = 16: with hit lists and drains but no copy to the
 // candidate lists; ABL = 32: every tile of a segment computed from its first
-// tile's codes (cache-hot: the code loads' latency out of the loop); results
-// invalid for all four.
+// tile's codes (cache-hot: the code loads' latency out of the loop); ABL =
+// 64: the MFMA operands straight from the code registers, no LDS table reads
+// (68: and no epilogue); results invalid for all of them.
 // ---------------------------------------------------------------------------
 
 constexpr int kHitsPerWave = 64;   // a tile adds at most one hit per lane
@@ -2207,7 +2214,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
 
       // one tile: K MFMAs, then the hit test
       auto tile = [&](const uint32_t (&cd)[NW], uint32_t jt) {
-        v16i acc = TileSmfmac<K, R>(cd, b, grp_tab, pos_tab);
+        v16i acc = TileSmfmac<K, R, (ABL & 64) != 0>(cd, b, grp_tab, pos_tab);
         if (ABL & 4) {
           int x = acc[0];
 #pragma unroll
@@ -3347,6 +3354,12 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
                          0, s, a);                                                         \
     else if (variant == 32)                                                                \
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 32>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
+                         0, s, a);                                                         \
+    else if (variant == 64)                                                                \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 64>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
+                         0, s, a);                                                         \
+    else if (variant == 68)                                                                \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 68>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
                          0, s, a);                                                         \
     else                                                                                   \
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()), \

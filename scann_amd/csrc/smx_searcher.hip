@@ -1027,6 +1027,102 @@ int smx_nearest_centers(const float* x, int64_t n, int32_t d, const float* cente
   return SMX_OK;
 }
 
+namespace {
+int CheckBlocks(int64_t n, int32_t dim, int32_t nb, int32_t dpb) {
+  if (n < 0 || dim <= 0 || nb <= 0 || dpb <= 0)
+    return Fail(SMX_INVALID_ARGUMENT, "need n >= 0, dim > 0, num_blocks > 0, dims_per_block > 0");
+  if (int64_t(nb) * dpb < dim || int64_t(nb - 1) * dpb >= dim)
+    return Fail(SMX_INVALID_ARGUMENT, "num_blocks must be ceil(dim / dims_per_block)");
+  return SMX_OK;
+}
+}  // namespace
+
+int smx_block_encode(const float* r, int64_t n, int32_t dim, const float* codebook, int32_t nb,
+                     int32_t dpb, uint8_t* out, void* stream) {
+  if (int e = CheckBlocks(n, dim, nb, dpb)) return e;
+  if (n == 0) return SMX_OK;
+  if (!r || !codebook || !out) return Fail(SMX_INVALID_ARGUMENT, "null input or output buffer");
+  SMX_HIP(smx::LaunchBlockEncode(r, n, dim, codebook, nb, dpb, out,
+                                 static_cast<hipStream_t>(stream)));
+  return SMX_OK;
+}
+
+int smx_avq_encode(const float* resid, const float* orig, int64_t n, int32_t dim,
+                   const float* codebook, int32_t nb, int32_t dpb, double threshold, uint8_t* out,
+                   void* stream) {
+  if (int e = CheckBlocks(n, dim, nb, dpb)) return e;
+  if (n == 0) return SMX_OK;
+  if (!resid || !orig || !codebook || !out)
+    return Fail(SMX_INVALID_ARGUMENT, "null input or output buffer");
+  if (dim < 2) return Fail(SMX_INVALID_ARGUMENT, "noise shaping needs dim >= 2");
+  if (!(threshold == threshold)) return Fail(SMX_INVALID_ARGUMENT, "threshold is NaN");
+  if (smx::AvqEncodeLds(nb, dpb) > 65536)
+    return Fail(SMX_INVALID_ARGUMENT, "num_blocks * dims_per_block too large for the AVQ kernel");
+  SMX_HIP(smx::LaunchAvqEncode(resid, orig, n, dim, codebook, nb, dpb, threshold, out,
+                               static_cast<hipStream_t>(stream)));
+  return SMX_OK;
+}
+
+int smx_kmeans_accumulate(const float* x, int64_t n, int32_t d, const int32_t* label, int32_t k,
+                          double scale, uint64_t* sums, uint32_t* counts, void* stream) {
+  if (n < 0 || d <= 0 || k <= 0 || !(scale > 0.0))
+    return Fail(SMX_INVALID_ARGUMENT, "need n >= 0, d > 0, k > 0, scale > 0");
+  if (n == 0) return SMX_OK;
+  if (!x || !label || !sums || !counts) return Fail(SMX_INVALID_ARGUMENT, "null buffer");
+  SMX_HIP(smx::LaunchKmeansAccumulate(x, n, d, label, k, scale,
+                                      reinterpret_cast<unsigned long long*>(sums), counts,
+                                      static_cast<hipStream_t>(stream)));
+  return SMX_OK;
+}
+
+int smx_kmeans_finalize(const uint64_t* sums, const uint32_t* counts, int32_t k, int32_t d,
+                        double scale, float* centers, void* stream) {
+  if (d <= 0 || k <= 0 || !(scale > 0.0))
+    return Fail(SMX_INVALID_ARGUMENT, "need d > 0, k > 0, scale > 0");
+  if (!sums || !counts || !centers) return Fail(SMX_INVALID_ARGUMENT, "null buffer");
+  SMX_HIP(smx::LaunchKmeansFinalize(reinterpret_cast<const unsigned long long*>(sums), counts, k, d,
+                                    scale, centers, static_cast<hipStream_t>(stream)));
+  return SMX_OK;
+}
+
+int smx_codebook_accumulate(const float* r, int64_t n, int32_t dim, const uint8_t* codes,
+                            int32_t nb, int32_t dpb, double scale, uint64_t* sums,
+                            uint32_t* counts, void* stream) {
+  if (int e = CheckBlocks(n, dim, nb, dpb)) return e;
+  if (!(scale > 0.0)) return Fail(SMX_INVALID_ARGUMENT, "scale must be > 0");
+  if (n == 0) return SMX_OK;
+  if (!r || !codes || !sums || !counts) return Fail(SMX_INVALID_ARGUMENT, "null buffer");
+  if (smx::CodebookAccumulateLds(nb, dpb) > 65536)
+    return Fail(SMX_INVALID_ARGUMENT, "num_blocks * dims_per_block too large for the kernel");
+  SMX_HIP(smx::LaunchCodebookAccumulate(r, n, dim, codes, nb, dpb, scale,
+                                        reinterpret_cast<unsigned long long*>(sums), counts,
+                                        static_cast<hipStream_t>(stream)));
+  return SMX_OK;
+}
+
+int smx_group_by_leaf(const int32_t* labels, const uint32_t* ids, int64_t m, int32_t k,
+                      void* temp, size_t* temp_bytes, uint64_t* keys, uint64_t* offsets,
+                      uint32_t* members, int32_t* member_leaf, void* stream) {
+  if (m < 0 || k <= 0 || !temp_bytes) return Fail(SMX_INVALID_ARGUMENT, "need m >= 0, k > 0");
+  if (m > 0xFFFFFFFFll) return Fail(SMX_INVALID_ARGUMENT, "at most 2^32 - 1 members");
+  if (temp && (!keys || !offsets || !members || !member_leaf || (m > 0 && (!labels || !ids))))
+    return Fail(SMX_INVALID_ARGUMENT, "null buffer");
+  SMX_HIP(smx::GroupByLeaf(labels, ids, m, k, temp, temp_bytes, keys, offsets, members,
+                           member_leaf, static_cast<hipStream_t>(stream)));
+  return SMX_OK;
+}
+
+int smx_gather_residuals(const float* x, int32_t d, const uint32_t* rows, const int32_t* leaf,
+                         const float* centers, int64_t m, int64_t row_base, float* out,
+                         void* stream) {
+  if (d <= 0 || m < 0) return Fail(SMX_INVALID_ARGUMENT, "need d > 0, m >= 0");
+  if (m == 0) return SMX_OK;
+  if (!x || !rows || !out || (centers && !leaf)) return Fail(SMX_INVALID_ARGUMENT, "null buffer");
+  SMX_HIP(smx::LaunchGatherResiduals(x, d, rows, leaf, centers, m, row_base, out,
+                                     static_cast<hipStream_t>(stream)));
+  return SMX_OK;
+}
+
 int smx_search_batched(smx_index* h, const float* queries, int32_t nq, int32_t dim,
                        const smx_search_params* p, uint32_t* out_idx, float* out_dist,
                        int32_t* out_count) {
@@ -1269,9 +1365,10 @@ int smx_set_tuning(smx_index* h, int32_t candidates_per_query, int32_t seed_leav
   if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
 #ifdef SMX_SCAN_DIAGNOSTICS
   if (scan_variant != 0 && scan_variant != 2 && scan_variant != 4 && scan_variant != 8 &&
-      scan_variant != 16 && scan_variant != 32)
+      scan_variant != 16 && scan_variant != 32 && scan_variant != 64 &&
+      scan_variant != 68)
     return Fail(SMX_INVALID_ARGUMENT,
-                "scan_variant is 0 (scan), 2 / 4 / 16 / 32 (timing ablations) or 8 (diagnostic stamps)");
+                "scan_variant is 0 (scan), 2 / 4 / 16 / 32 / 64 / 68 (timing ablations) or 8 (diagnostic stamps)");
 #else
   if (scan_variant != 0)
     return Fail(SMX_INVALID_ARGUMENT,

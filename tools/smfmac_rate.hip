@@ -29,6 +29,8 @@ constexpr int TILES = 4096;
 // MODE 0: one long chain over the KS B fragments (no per-tile work)
 // MODE 1: per tile: zero the accumulator, KS steps, min of the 16 sums + ballot
 // MODE 2: as 1 with two accumulators (tile t+1's chain beside tile t's test)
+// MODE 3: as 1 with the operands read from the scan's two 16-entry LDS
+//         tables by random code bytes (3 reads in flight), as in the scan
 template <int MODE>
 __global__ void __launch_bounds__(768) rate(const int* __restrict__ rnd, long long* cycles,
                                             int* sink) {
@@ -42,13 +44,49 @@ __global__ void __launch_bounds__(768) rate(const int* __restrict__ rnd, long lo
   int ix = rnd[128 + lane];
   v16i acc = v16i{0}, acc2 = v16i{0};
   unsigned long long hits = 0;
+  __shared__ __align__(256) v4i grp_tab[16];
+  __shared__ int pos_tab[16];
+  if (threadIdx.x < 16) {
+    const uint32_t g0 = threadIdx.x & 3u, g1 = threadIdx.x >> 2;
+    v4i tt = {0, 0, 0, 0};
+    tt[g0 >> 1] = int(1u << (16 * (g0 & 1u)));
+    tt[2 + (g1 >> 1)] = int(1u << (16 * (g1 & 1u)));
+    grp_tab[threadIdx.x] = tt;
+    pos_tab[threadIdx.x] = int((threadIdx.x & 3u) * 0x5555u | ((threadIdx.x >> 2) * 0x5555u) << 16);
+  }
+  __syncthreads();
+  uint32_t codes[4] = {uint32_t(rnd[lane]), uint32_t(rnd[64 + lane]), uint32_t(rnd[128 + lane]),
+                       uint32_t(rnd[192 + lane])};
   const long long t0 = __builtin_amdgcn_s_memtime();
   for (int t = 0; t < TILES; ++t) {
     if (MODE >= 1) acc = v16i{0};
+    if (MODE == 3) {
+      constexpr int R = 3;
+      auto grp = [&](int q) { return (codes[q >> 2] >> ((q & 3) * 8)) & 0xFu; };
+      auto pos = [&](int q) { return (codes[q >> 2] >> ((q & 3) * 8 + 4)) & 0xFu; };
+      v4i o[R];
+      int ixr[R];
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        o[q] = grp_tab[grp(q)];
+        ixr[q] = pos_tab[pos(q)];
+      }
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        acc = __builtin_amdgcn_smfmac_i32_32x32x64_i8(o[s % R], b[s], acc, ixr[s % R], 0, 0);
+        if (s + R < KS) {
+          o[s % R] = grp_tab[grp(s + R)];
+          ixr[s % R] = pos_tab[pos(s + R)];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) codes[q] = codes[q] * 1664525u + 1013904223u;
+    } else {
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       acc = __builtin_amdgcn_smfmac_i32_32x32x64_i8(a, b[s], acc, ix, 0, 0);
       a[0] += 0x00010000;
+    }
     }
     if (MODE >= 1) {
       int m = acc[0];
@@ -111,6 +149,7 @@ int main() {
   for (int w = 1; w <= 3; ++w) {
     run<0>(d_rnd, w, "chain, 13 random B");
     run<1>(d_rnd, w, "per-tile zero + min test");
+    run<3>(d_rnd, w, "+ LDS operand tables (scan)");
   }
   return 0;
 }
