@@ -65,6 +65,7 @@ CONFIGS = {
     # range split; at N=1 this GPU holds rank 0's shard of the `split`-way split
     "soar100m": dict(n=100_000_000, leaves=10000, leaves_to_search=100, metric=0, seed=4,
                      generated=True, split=8, soar=1.5, dim=96, components=4096,
+                     train_sample=250_000, sweep=[20, 40, 60, 100],
                      workload="configs[3]: synthetic 100M x 96 dot product + SOAR (lambda 1.5, "
                               "overretrieve 2), tree-AH 10000 leaves, LUT16 AH 48 blocks x 2 "
                               "dims, leaves_to_search=100, reorder 100, k=10, batch=1000, "
@@ -76,6 +77,7 @@ CONFIGS = {
                                  "dot + SOAR, 10000 leaves, 8-way split), batch=1000"),
     "deep1b": dict(n=1_000_000_000, leaves=50000, leaves_to_search=400, metric=0, seed=5,
                    generated=True, split=8, soar=None, dim=96, components=1 << 17,
+                   train_sample=5_000_000, train_iterations=10, sweep=[400, 800, 1200, 2000],
                    workload="configs[4]: Deep1B shape 1e9 x 96 dot product, tree-AH 50000 "
                             "leaves, LUT16 AH 48 blocks x 2 dims, leaves_to_search=400, reorder "
                             "100, k=10, batch=1000, dataset sharded 8 ways: one rank's shard "
@@ -513,10 +515,17 @@ def main_generated(args, rank, world, local, dist, dev):
     t = time.time()
     ds = generate.GeneratedDataset(n, CFG["dim"], CFG["seed"], components=CFG["components"],
                                    device=dev)
+    torch.cuda.synchronize()
+    t_build = time.perf_counter()
     ix = generate.build_generated_shard(
         ds, LEAVES, shard_rank, split, soar_lambda=CFG["soar"], seed=CFG["seed"],
-        training_sample_size=max(250_000, 20 * LEAVES), counts_from_all_ranks=False, log=log)
-    log(f"shard {shard_rank}/{split} built in {time.time() - t:.1f}s: {ix.num_members} members")
+        training_sample_size=CFG.get("train_sample", max(250_000, 20 * LEAVES)),
+        training_iterations=CFG.get("train_iterations", 8),
+        counts_from_all_ranks=False, log=log)
+    torch.cuda.synchronize()
+    build_s = time.perf_counter() - t_build
+    log(f"shard {shard_rank}/{split} built in {build_s:.1f}s (generation included): "
+        f"{ix.num_members} members")
     q = ds.queries(NQ, CFG["seed"] + 1000)
     eng = NativeShardEngine(ix, device=local)
     qd = torch.from_numpy(q).to(dev)
@@ -588,6 +597,37 @@ def main_generated(args, rank, world, local, dist, dev):
     r0, r1 = c0 * generate.CHUNK, min(c1 * generate.CHUNK, n)
     truth = _generated_truth(ds, q, r0, r1, dev)
     recall = synthetic.recall_at_k(gidx, truth, FINAL_NN)
+    # QPS-recall operating points over leaves_to_search (the headline value
+    # stays at the configured one): search + merge timed as above, recall of
+    # this rank's merged result
+    points = []
+    if not args.no_sweep:
+        for lv in CFG.get("sweep", []):
+            if lv > LEAVES:
+                continue
+            kl = eng.shard_width(lv, PRE_NN, FINAL_NN, True)
+            le = torch.empty((NQ, kl, 2), dtype=torch.int64, device=dev)
+            gl = torch.empty((split, NQ, kl, 2), dtype=torch.int64, device=dev)
+
+            def sweep_step():
+                eng.search_shard(qd, lv, PRE_NN, FINAL_NN, True, le)
+                if world == split:
+                    g = all_gather_entries(le, world)
+                else:
+                    gl.copy_(le.unsqueeze(0).expand_as(gl))
+                    g = gl
+                return eng.merge(split, g, NQ, lv, PRE_NN, FINAL_NN, True)
+
+            for _ in range(2):
+                sweep_step()
+            el = timed(sweep_step, max(2, args.sweep_steps // 2))
+            eng.search_shard(qd, lv, PRE_NN, FINAL_NN, True, le)
+            own = eng.merge(1, le.unsqueeze(0), NQ, lv, PRE_NN, FINAL_NN, True)
+            r = synthetic.recall_at_k(own[0].cpu().numpy().astype(np.int64), truth, FINAL_NN)
+            points.append({"leaves_to_search": lv,
+                           "qps": round(NQ * max(2, args.sweep_steps // 2) / el, 1),
+                           "recall_at_10": round(r, 4)})
+            del le, gl
     avg_scan_ms = float(np.mean(scan_ms))
     bytes_per_launch = float(np.mean(scan_bytes))
     roof = scan_roofline(bytes_per_launch, avg_scan_ms, stages, ix.num_blocks)
@@ -609,6 +649,15 @@ def main_generated(args, rank, world, local, dist, dev):
             "recall_at_10": round(recall, 4),
             "recall_reference": ("exact brute force over the shard's rows" if world == 1
                                  else "exact brute force over the whole dataset"),
+            "operating_points": points,
+            "qps_at_recall_0.95": next(({"leaves_to_search": p["leaves_to_search"],
+                                         "qps": p["qps"], "recall_at_10": p["recall_at_10"]}
+                                        for p in points if p["recall_at_10"] >= 0.95), None),
+            "build_s": round(build_s, 2),
+            "build": ("generation + the whole shard build on this GPU in the HIP build kernels "
+                      "(k-means on a %d-row sample, tokenization%s, grouping, codebook, codes)"
+                      % (CFG.get("train_sample", max(250_000, 20 * LEAVES)),
+                         " + SOAR" if CFG["soar"] else "")),
             "shard_search_ms": round(search_s * 1000.0 / args.steps, 4),
             "merge_ms": round(merge_s * 1000.0 / args.steps, 4),
             "merge_input": (f"all-gather of {split} ranks" if world == split else

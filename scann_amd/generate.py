@@ -21,11 +21,15 @@ keeps only its shard.
 * Per-leaf counts of the other ranks come from an all-gather when
   torch.distributed is initialised, otherwise from a counting pass over
   their rows on this GPU (assign only; nothing kept).
-* Centers: k-means (index_builder.kmeans) on the first `training_sample_size`
-  rows of the dataset; codebook: per-block k-means on the residuals of the
-  first `ah_training_sample_size` rows -- the same samples on every rank.
-* Codes: nearest codebook center per block; SOAR secondary leaves with
-  index_builder's loss; all on the GPU.
+* Centers: k-means (device_builder.kmeans) on the first
+  `training_sample_size` rows of the dataset; codebook: per-block k-means
+  (device_builder.train_codebook) on the residuals of the first
+  `ah_training_sample_size` rows -- the same samples on every rank.
+* Tokens, SOAR secondary leaves, the (leaf, row) grouping, residuals and
+  codes: the hand-written HIP build kernels (smx_nearest_centers,
+  smx_group_by_leaf, smx_gather_residuals, smx_block_encode) -- every step
+  of the build runs in them; torch only generates the rows and holds the
+  buffers.
 """
 from __future__ import annotations
 
@@ -35,7 +39,7 @@ from typing import Optional
 import numpy as np
 import torch
 
-from . import index_builder
+from . import device_builder as dbuild
 from .index import METRIC_DOT, TreeAHIndex
 
 CHUNK = 1 << 16
@@ -92,47 +96,40 @@ class GeneratedDataset:
 
 
 def _assign(x: torch.Tensor, c: torch.Tensor, cn: torch.Tensor) -> torch.Tensor:
-    """argmin_c ||x - c||^2 (the index_builder formula, one GEMM per chunk)."""
-    return (cn[None, :] - 2.0 * (x @ c.T)).argmin(1)
+    """Nearest center of every row (smx_nearest_centers)."""
+    return dbuild.nearest_centers(x, c)
 
 
 def _soar(x: torch.Tensor, c: torch.Tensor, cn: torch.Tensor, p: torch.Tensor,
           lam: float) -> torch.Tensor:
-    """index_builder.soar_assign's loss on one chunk (never the primary leaf)."""
-    r = x - c[p]
-    rn = (r * r).sum(1).clamp_min(1e-30)
-    d2 = (x * x).sum(1, keepdim=True) - 2.0 * (x @ c.T) + cn[None, :]
-    proj = (r * x).sum(1, keepdim=True) - r @ c.T
-    loss = d2 + lam * proj * proj / rn[:, None]
-    loss[torch.arange(x.shape[0], device=x.device), p] = float("inf")
-    return loss.argmin(1)
+    """The SOAR secondary leaf of every row, never the primary
+    (smx_nearest_centers with the primary centers)."""
+    return dbuild.nearest_centers(x, c, primary=p, lam=float(lam))
 
 
 def _tokens(ds: GeneratedDataset, c0: int, c1: int, c: torch.Tensor, cn: torch.Tensor,
             soar_lambda: Optional[float], keep: bool):
-    """(leaf, row) entries of chunks [c0, c1); per-leaf counts always."""
+    """(leaf, row) entries of chunks [c0, c1) (int32 leaves, rows as int32
+    storage of uint32 ids); per-leaf counts always."""
     L = c.shape[0]
     counts = torch.zeros(L, dtype=torch.int64, device=ds.device)
     leaves, rows = [], []
-    sub = max(1024, min(CHUNK, (1 << 27) // max(1, L)))
     for ch in range(c0, c1):
         x = ds.chunk(ch)
-        for s in range(0, x.shape[0], sub):
-            xs = x[s:s + sub]
-            p = _assign(xs, c, cn)
-            parts = [p]
-            if soar_lambda is not None and L > 1:
-                parts.append(_soar(xs, c, cn, p, float(soar_lambda)))
-            rid = torch.arange(ch * CHUNK + s, ch * CHUNK + s + xs.shape[0],
-                               dtype=torch.int64, device=ds.device)
-            for t in parts:
-                counts += torch.bincount(t, minlength=L)
-                if keep:
-                    leaves.append(t)
-                    rows.append(rid)
+        p = _assign(x, c, cn)
+        parts = [p]
+        if soar_lambda is not None and L > 1:
+            parts.append(_soar(x, c, cn, p, float(soar_lambda)))
+        rid = torch.arange(ch * CHUNK, ch * CHUNK + x.shape[0], dtype=torch.int64,
+                           device=ds.device).to(torch.int32)
+        for t in parts:
+            counts += torch.bincount(t, minlength=L)
+            if keep:
+                leaves.append(t)
+                rows.append(rid)
     if keep:
         if not leaves:   # a rank without chunks (n < world chunks)
-            e = torch.zeros(0, dtype=torch.int64, device=ds.device)
+            e = torch.zeros(0, dtype=torch.int32, device=ds.device)
             return counts, e, e.clone()
         return counts, torch.cat(leaves), torch.cat(rows)
     return counts, None, None
@@ -156,19 +153,23 @@ def build_generated_shard(ds: GeneratedDataset, num_leaves: int, rank: int = 0, 
     dim = ds.dim
     residual = metric == METRIC_DOT
     # partitioner: the same sample on every rank
-    samp = ds.rows(0, min(training_sample_size, ds.n)).cpu().numpy()
-    centers = index_builder.kmeans(samp, num_leaves, training_iterations, seed)
+    samp = ds.rows(0, min(training_sample_size, ds.n))
+    c = dbuild.kmeans(samp, num_leaves, training_iterations, seed)
     say(f"centers: k-means {num_leaves} on {samp.shape[0]} rows")
-    c = torch.from_numpy(centers).to(dev)
-    cn = (c * c).sum(1)
+    del samp
+    centers = c.cpu().numpy()
+    cn = None
     L = centers.shape[0]
     num_blocks = int(math.ceil(dim / dims_per_block))
     # codebook: residuals of the first rows' primary leaves
     asamp = ds.rows(0, min(ah_training_sample_size, ds.n))
     ap = _assign(asamp, c, cn)
-    ares = (asamp - c[ap]) if residual else asamp
-    codebook = index_builder.train_codebook(ares.cpu().numpy(), num_blocks, dims_per_block,
-                                            ah_training_iterations, seed + 2)
+    ares = dbuild.gather_residuals(asamp, torch.arange(asamp.shape[0], dtype=torch.int32,
+                                                       device=dev), ap,
+                                   c if residual else None)
+    cb = dbuild.train_codebook(ares, num_blocks, dims_per_block, ah_training_iterations,
+                               seed + 2)
+    codebook = cb.cpu().numpy()
     say(f"codebook: {num_blocks} blocks x 16 on {asamp.shape[0]} residuals")
     del asamp, ap, ares
 
@@ -199,40 +200,33 @@ def build_generated_shard(ds: GeneratedDataset, num_leaves: int, rank: int = 0, 
         before = torch.zeros_like(counts)
         total = counts * world
 
-    # members by (leaf, row)
-    key = leaves * (1 << 32) + rows
-    order = torch.argsort(key)
-    leaves, rows = leaves[order], rows[order]
+    # members by (leaf, row): smx_group_by_leaf
+    _, rows, leaves = dbuild.group_by_leaf(leaves, rows, L)
     offsets = np.zeros(L + 1, np.uint64)
     offsets[1:] = np.cumsum(counts.cpu().numpy())
     spilled = soar_lambda is not None and L > 1
     inner = 32 - int(math.ceil(math.log2(L))) if L > 1 else 32
     shift = inner if (residual and L > 1 and int(total.max()) <= (1 << inner)) else 0
 
-    # codes (nearest codebook center per block) and the members' float rows
-    cb = torch.from_numpy(codebook).to(dev)
+    # the members' float rows and codes (nearest codebook center per block)
     m = rows.numel()
-    codes = np.empty((m, num_blocks), np.uint8)
-    member_rows = np.empty((m, dim), np.float32)
-    pad = num_blocks * dims_per_block - dim
     row0 = c0 * CHUNK
     nrows = min(c1 * CHUNK, ds.n) - row0
     x_all = ds.rows(row0, nrows)
-    step = 1 << 18
-    for s in range(0, m, step):
-        rr = rows[s:s + step] - row0
-        x = x_all[rr]
-        r = (x - c[leaves[s:s + step]]) if residual else x
-        if pad:
-            r = torch.cat([r, torch.zeros(r.shape[0], pad, device=dev)], 1)
-        r = r.view(r.shape[0], num_blocks, dims_per_block)
-        d = ((r[:, :, None, :] - cb[None]) ** 2).sum(-1)
-        codes[s:s + step] = d.argmin(-1).to(torch.uint8).cpu().numpy()
-        member_rows[s:s + step] = x.cpu().numpy()
+    codes = np.empty((m, num_blocks), np.uint8)
+    member_rows = np.empty((m, dim), np.float32)
+    step = 1 << 23
+    for s0 in range(0, m, step):
+        rr, ll = rows[s0:s0 + step], leaves[s0:s0 + step]
+        xr = dbuild.gather_residuals(x_all, rr, None, None, row_base=row0)
+        member_rows[s0:s0 + rr.numel()] = xr.cpu().numpy()
+        res = dbuild.gather_residuals(x_all, rr, ll, c, row_base=row0) if residual else xr
+        codes[s0:s0 + rr.numel()] = dbuild.block_encode(res, cb).cpu().numpy()
+        del xr, res
     del x_all
     say(f"codes: {m} members encoded; largest leaf {int(total.max())} (whole index"
         f"{', estimated' if world > 1 and not counts_from_all_ranks else ''}), shift {shift}")
-    members = rows.to(torch.int64).cpu().numpy().astype(np.uint32)
+    members = rows.cpu().numpy().view(np.uint32)
     if world == 1:
         dataset = np.empty((ds.n, dim), np.float32)
         dataset[members] = member_rows   # a SOAR copy writes the same row twice

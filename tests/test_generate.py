@@ -1,7 +1,8 @@
-"""The on-device generator of BASELINE configs 4/5 (scann_amd/generate.py) on
-the CPU: chunks regenerate bit for bit, and the W shards a rank-by-rank build
-produces are exactly the range split of the whole index (members of every
-leaf contiguous from leaf_row_base, identical codes, whole-index shift)."""
+"""The on-device generator of BASELINE configs 4/5 (scann_amd/generate.py):
+chunks regenerate bit for bit (CPU), and -- on the GPU, where the build's HIP
+kernels run -- the W shards a rank-by-rank build produces are exactly the
+range split of the whole index (members of every leaf contiguous from
+leaf_row_base, identical codes, whole-index shift)."""
 import numpy as np
 import pytest
 import torch
@@ -9,8 +10,8 @@ import torch
 from scann_amd import generate
 
 
-def _ds(n=150_000, dim=24, seed=4):
-    return generate.GeneratedDataset(n, dim, seed, components=64, device=torch.device("cpu"))
+def _ds(n=150_000, dim=24, seed=4, device="cpu"):
+    return generate.GeneratedDataset(n, dim, seed, components=64, device=torch.device(device))
 
 
 def test_chunks_regenerate_and_rows_are_unit():
@@ -22,9 +23,10 @@ def test_chunks_regenerate_and_rows_are_unit():
     assert ds.num_chunks == 3
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("soar", [None, 1.5])
 def test_rank_shards_are_the_range_split_of_the_whole_index(soar):
-    ds = _ds()
+    ds = _ds(device="cuda")
     kw = dict(soar_lambda=soar, training_sample_size=20_000, training_iterations=3,
               ah_training_sample_size=10_000, ah_training_iterations=3, seed=1)
     whole = generate.build_generated_shard(ds, 40, 0, 1, **kw)
@@ -49,8 +51,9 @@ def test_rank_shards_are_the_range_split_of_the_whole_index(soar):
     np.testing.assert_array_equal(sh.member_rows, whole.dataset[sh.leaf_members])
 
 
+@pytest.mark.gpu
 def test_rank_without_chunks_is_an_empty_shard():
-    ds = _ds(n=100_000)   # 2 chunks, 3 ranks
+    ds = _ds(n=100_000, device="cuda")   # 2 chunks, 3 ranks
     sh = generate.build_generated_shard(ds, 8, 0, 3, training_sample_size=5000,
                                         training_iterations=2, ah_training_sample_size=5000,
                                         ah_training_iterations=2)
