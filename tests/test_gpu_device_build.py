@@ -39,8 +39,9 @@ def test_avq_kernel_matches_oracle(oracle, n, dim, dpb, thr):
     want = oracle.avq_encode(r, x, cb, thr)
     np.testing.assert_array_equal(got, want)
     plain = db.block_encode(_dev(r), _dev(cb)).cpu().numpy()
-    eta = (thr * thr) / ((1.0 - thr * thr) / (dim - 1.0))   # unit rows
-    if eta > 1.0:
+    # unit rows: eta = t^2 / ((1 - t^2) / (dim - 1)); at t >= 1 the parallel
+    # cost multiplier is infinite or negative (still bit-equal above)
+    if thr < 1.0 and (thr * thr) / ((1.0 - thr * thr) / (dim - 1.0)) > 1.0:
         assert (got != plain).any()     # noise shaping moved some codes
 
 
