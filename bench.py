@@ -78,7 +78,7 @@ CONFIGS = {
     "deep1b": dict(n=1_000_000_000, leaves=50000, leaves_to_search=400, metric=0, seed=5,
                    generated=True, split=8, soar=None, dim=96, components=1 << 17,
                    train_sample=5_000_000, train_iterations=10,
-                   sweep=[400, 800, 1200, 2000, [800, 400], [2000, 400], [4000, 1000]],
+                   sweep=[400, 800, 1200, 2000, [800, 256], [2000, 256], [4000, 256]],
                    workload="configs[4]: Deep1B shape 1e9 x 96 dot product, tree-AH 50000 "
                             "leaves, LUT16 AH 48 blocks x 2 dims, leaves_to_search=400, reorder "
                             "100, k=10, batch=1000, dataset sharded 8 ways: one rank's shard "

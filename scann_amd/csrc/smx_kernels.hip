@@ -1203,10 +1203,10 @@ __device__ __forceinline__ void LoadCodes(const uint8_t* p, uint32_t* codes) {
 // exact k'-th value.
 // ---------------------------------------------------------------------------
 #ifndef SMX_SEED_U
-#define SMX_SEED_U 8
+#define SMX_SEED_U 4
 #endif
 #ifndef SMX_SEED_PER_THREAD
-#define SMX_SEED_PER_THREAD 32
+#define SMX_SEED_PER_THREAD 16
 #endif
 constexpr int kSeedPerThread = SMX_SEED_PER_THREAD;
 constexpr uint32_t kSeedCap = 256u * kSeedPerThread;
