@@ -220,7 +220,25 @@ __global__ void __launch_bounds__(256) kmeans_finalize_kernel(
 // The codebook's k-means mean step for all blocks at once: sums[(b*16 +
 // code) * dpb + i] += r[row][b*dpb + i] (fixed point), counts[b*16 + code]++.
 // The block's partial sums are kept in LDS (ds_add_u64) and flushed with one
-// global atomic per entry.  256 threads, each a run of rows.
+// global atomic per entry; shapes whose sums exceed 64 KB of LDS add to the
+// global sums directly (codebook_accumulate_global_kernel).  256 threads,
+// each a run of rows.
+__global__ void __launch_bounds__(256) codebook_accumulate_global_kernel(
+    const float* __restrict__ r, int64_t n, int dim, const uint8_t* __restrict__ codes, int nb,
+    int dpb, double scale, unsigned long long* __restrict__ sums, uint32_t* __restrict__ counts) {
+  const int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (e >= n * nb) return;
+  const int64_t row = e / nb;
+  const int b = int(e - row * nb);
+  const int c = codes[e];
+  for (int i = 0; i < dpb; ++i) {
+    const int j = b * dpb + i;
+    const float v = j < dim ? r[row * dim + j] : 0.0f;
+    atomicAdd(&sums[(b * 16 + c) * dpb + i], (unsigned long long)llrint(double(v) * scale));
+  }
+  atomicAdd(&counts[b * 16 + c], 1u);
+}
+
 __global__ void __launch_bounds__(256) codebook_accumulate_kernel(
     const float* __restrict__ r, int64_t n, int dim, const uint8_t* __restrict__ codes, int nb,
     int dpb, double scale, unsigned long long* __restrict__ sums, uint32_t* __restrict__ counts) {
@@ -439,6 +457,11 @@ hipError_t LaunchCodebookAccumulate(const float* r, int64_t n, int dim, const ui
                                     uint32_t* counts, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const int64_t total = n * nb;
+  if (CodebookAccumulateLds(nb, dpb) > 65536) {
+    hipLaunchKernelGGL(codebook_accumulate_global_kernel, dim3(unsigned((total + 255) / 256)),
+                       dim3(256), 0, s, r, n, dim, codes, nb, dpb, scale, sums, counts);
+    return hipGetLastError();
+  }
   const unsigned grid = unsigned(std::min<int64_t>(2048, (total + 255) / 256));
   hipLaunchKernelGGL(codebook_accumulate_kernel, dim3(grid), dim3(256),
                      CodebookAccumulateLds(nb, dpb), s, r, n, dim, codes, nb, dpb, scale, sums,

@@ -2316,7 +2316,9 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
           LoadCodes<K>(tile_ptr(more ? tn : t), cb);
           tile(codes, t);
           ++tiles_done;
+#ifndef SMX_COPY_LATE
           if (pending) copy_prev();   // after the segment's first tile: the atomic has returned
+#endif
           if (!more) break;
           drain_mid();
           advance(t, tn);
@@ -2331,6 +2333,10 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
           t = tn;
         }
       }
+#ifdef SMX_COPY_LATE
+      // the previous segment's list-slot atomics had this whole segment to return
+      if (pending) copy_prev();
+#endif
       if (whits) {
         drain();
         whits = 0;

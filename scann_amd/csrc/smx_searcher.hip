@@ -1092,8 +1092,6 @@ int smx_codebook_accumulate(const float* r, int64_t n, int32_t dim, const uint8_
   if (!(scale > 0.0)) return Fail(SMX_INVALID_ARGUMENT, "scale must be > 0");
   if (n == 0) return SMX_OK;
   if (!r || !codes || !sums || !counts) return Fail(SMX_INVALID_ARGUMENT, "null buffer");
-  if (smx::CodebookAccumulateLds(nb, dpb) > 65536)
-    return Fail(SMX_INVALID_ARGUMENT, "num_blocks * dims_per_block too large for the kernel");
   SMX_HIP(smx::LaunchCodebookAccumulate(r, n, dim, codes, nb, dpb, scale,
                                         reinterpret_cast<unsigned long long*>(sums), counts,
                                         static_cast<hipStream_t>(stream)));

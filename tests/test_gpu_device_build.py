@@ -140,3 +140,37 @@ def test_device_built_index_search_parity(oracle, soar, avq):
     np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
     truth = synthetic.brute_force_topk(x, q, 10, 0)
     assert synthetic.recall_at_k(gi.astype(np.int64), truth, 10) > 0.8
+
+
+@pytest.mark.parametrize("dim,dpb", [(100, 2), (900, 2)])
+def test_codebook_accumulate_sums(dim, dpb):
+    """Every block's 16-center sums and counts at once, LDS-privatised (100
+    dims) or straight to global memory (900 dims: 450 blocks); the means equal
+    float64 means."""
+    from scann_amd import _native
+    from scann_amd import device_builder as db
+    rng = np.random.default_rng(dim)
+    n, nb = 3000, -(-dim // dpb)
+    r = rng.standard_normal((n, dim)).astype(np.float32)
+    codes = rng.integers(0, 16, (n, nb)).astype(np.uint8)
+    scale = db.fixed_point_scale(float(np.abs(r).max()), n)
+    sums = torch.zeros(nb * 16 * dpb, dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(nb * 16, dtype=torch.int32, device="cuda")
+    cen = torch.zeros((nb * 16, dpb), dtype=torch.float32, device="cuda")
+    rd, cd = _dev(r), _dev(codes)
+    lib = _native.load()
+    _native.check(lib.smx_codebook_accumulate(db._p(rd), n, dim, db._p(cd), nb, dpb, scale,
+                                              db._p(sums), db._p(cnt), None), "acc")
+    _native.check(lib.smx_kmeans_finalize(db._p(sums), db._p(cnt), nb * 16, dpb, scale,
+                                          db._p(cen), None), "fin")
+    torch.cuda.synchronize()
+    pad = np.zeros((n, nb * dpb))
+    pad[:, :dim] = r
+    want = np.zeros((nb, 16, dpb))
+    wc = np.zeros((nb, 16), np.int64)
+    for b in range(nb):
+        np.add.at(want[b], codes[:, b], pad[:, b * dpb:(b + 1) * dpb])
+        wc[b] = np.bincount(codes[:, b], minlength=16)
+    np.testing.assert_array_equal(cnt.cpu().numpy().reshape(nb, 16), wc)
+    np.testing.assert_allclose(cen.cpu().numpy().reshape(nb, 16, dpb),
+                               want / np.maximum(wc, 1)[..., None], rtol=2e-6, atol=1e-6)
