@@ -1615,8 +1615,6 @@ template <int K, int R, bool NOLDS = false>
 __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)[K / 2],
                                            const v4i* grp_tab, const int* pos_tab) {
   constexpr int KS = K / 2;
-  auto grp = [&](int t) { return (codes[t >> 2] >> ((t & 3) * 8)) & 0xFu; };
-  auto pos = [&](int t) { return (codes[t >> 2] >> ((t & 3) * 8 + 4)) & 0xFu; };
   v4i o[R];
   int ix[R];
   // NOLDS (timing ablation, results invalid): operands straight from the
@@ -1627,8 +1625,26 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
       o[slot] = v4i{w & 0x00010001, 0, w & 0x01000100, 0};
       ix[slot] = w;
     } else {
-      o[slot] = grp_tab[grp(t)];
-      ix[slot] = pos_tab[pos(t)];
+      // both table offsets in one SDWA op each: the group table (v4i
+      // entries at LDS 0) at 16 * (byte & 0xF) = (byte << 4) truncated to its
+      // low byte; the position table (one index word per 16 bytes) at
+      // byte & 0xF0 = 16 * (byte >> 4)
+      const uint32_t w = codes[t >> 2];
+      uint32_t og, op;
+#define SMX_SDWA_OFFS(B)                                                                        \
+  asm("v_lshlrev_b32_sdwa %0, 4, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD "        \
+      "src1_sel:BYTE_" #B "\n\tv_and_b32_sdwa %1, %3, %2 dst_sel:DWORD dst_unused:UNUSED_PAD "   \
+      "src0_sel:DWORD src1_sel:BYTE_" #B                                                         \
+      : "=&v"(og), "=&v"(op) : "v"(w), "v"(0xF0u))
+      switch (t & 3) {
+        case 0: SMX_SDWA_OFFS(0); break;
+        case 1: SMX_SDWA_OFFS(1); break;
+        case 2: SMX_SDWA_OFFS(2); break;
+        default: SMX_SDWA_OFFS(3); break;
+      }
+#undef SMX_SDWA_OFFS
+      o[slot] = *reinterpret_cast<const v4i*>(reinterpret_cast<const char*>(grp_tab) + og);
+      ix[slot] = *reinterpret_cast<const int*>(reinterpret_cast<const char*>(pos_tab) + op);
     }
   };
 #pragma unroll
@@ -1939,7 +1955,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   static_assert(K % 2 == 0, "the sparse scan takes two code nibbles per step");
   __shared__ ScanWaveLds wl_[NWAVES];
   __shared__ __align__(256) v4i grp_tab[16];   // 256-aligned: base | (x & 0xF0)
-  __shared__ int pos_tab[16];
+  __shared__ __align__(16) int pos_tab[64];   // entry p at word 4 p (16-byte stride)
   __shared__ uint32_t s_item[kMaxSegs], s_end[kMaxSegs], s_next[kMaxSegs];
   __shared__ SegDesc s_desc[kMaxSegs];
   __shared__ uint32_t s_nseg, s_claim, s_sw, s_su, s_sp;
@@ -1956,7 +1972,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
     t[2 + (g1 >> 1)] = int(1u << (16 * (g1 & 1u)));
     grp_tab[threadIdx.x] = t;
     // position nibble p0 | p1 << 2: p0 in index fields 0..7, p1 in 8..15
-    pos_tab[threadIdx.x] = int((threadIdx.x & 3u) * 0x5555u | ((threadIdx.x >> 2) * 0x5555u) << 16);
+    pos_tab[4 * threadIdx.x] = int((threadIdx.x & 3u) * 0x5555u | ((threadIdx.x >> 2) * 0x5555u) << 16);
   }
   const uint32_t worker = blockIdx.x * NWAVES + wv;
   // this workgroup's share: `units` tiles from tile jfirst of item w on
@@ -2316,9 +2332,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
           LoadCodes<K>(tile_ptr(more ? tn : t), cb);
           tile(codes, t);
           ++tiles_done;
-#ifndef SMX_COPY_LATE
           if (pending) copy_prev();   // after the segment's first tile: the atomic has returned
-#endif
           if (!more) break;
           drain_mid();
           advance(t, tn);
@@ -2333,10 +2347,6 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
           t = tn;
         }
       }
-#ifdef SMX_COPY_LATE
-      // the previous segment's list-slot atomics had this whole segment to return
-      if (pending) copy_prev();
-#endif
       if (whits) {
         drain();
         whits = 0;
