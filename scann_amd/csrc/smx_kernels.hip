@@ -1954,8 +1954,12 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   constexpr int R = SMX_SCAN_R;   // one-hot reads in flight ahead of their MFMA
   static_assert(K % 2 == 0, "the sparse scan takes two code nibbles per step");
   __shared__ ScanWaveLds wl_[NWAVES];
-  __shared__ __align__(256) v4i grp_tab[16];   // 256-aligned: base | (x & 0xF0)
-  __shared__ __align__(16) int pos_tab[64];   // entry p at word 4 p (16-byte stride)
+  // the two operand tables in one 512-byte array at LDS 0 (256-aligned, the
+  // largest alignment is placed first): group entries [0, 256), position
+  // entries at 256 + 16 p, so both offsets fold into the ds_read's immediate
+  __shared__ __align__(256) v4i opnd_tab[32];
+  v4i* const grp_tab = opnd_tab;
+  int* const pos_tab = reinterpret_cast<int*>(opnd_tab + 16);
   __shared__ uint32_t s_item[kMaxSegs], s_end[kMaxSegs], s_next[kMaxSegs];
   __shared__ SegDesc s_desc[kMaxSegs];
   __shared__ uint32_t s_nseg, s_claim, s_sw, s_su, s_sp;
