@@ -94,6 +94,11 @@ def load(path: str = LIB_PATH):
         raise ImportError(
             f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
             " (the MI355X search path has no CPU fallback)")
+    # torch first: it brings its own HIP/HSA runtime, which the library then
+    # binds by soname.  Loaded the other way round, /opt/rocm's runtime comes
+    # in first and torch's later device init fails ("No HIP GPUs are
+    # available") -- one process, one runtime.
+    import torch  # noqa: F401
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -148,24 +148,25 @@ __device__ __forceinline__ uint32_t RankStable(const uint64_t* keys, uint32_t n,
 
 // Block-wide bitonic sort (ascending) of n (power of two) keys in LDS.
 __device__ void BitonicSort(uint64_t* keys, uint32_t n) {
+  // every thread a compare-exchange pair per step (pair p -> the index with a
+  // zero inserted at bit log2(j), and its partner i | j): no idle half
+  const uint32_t half = n >> 1;
   for (uint32_t k = 2; k <= n; k <<= 1) {
     for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint32_t ixj = i ^ j;
-        if (ixj > i) {
-          const uint64_t a = keys[i], b = keys[ixj];
-          const bool up = (i & k) == 0;
-          if ((a > b) == up) {
-            keys[i] = b;
-            keys[ixj] = a;
-          }
+      for (uint32_t p = threadIdx.x; p < half; p += blockDim.x) {
+        const uint32_t i = ((p & ~(j - 1u)) << 1) | (p & (j - 1u));
+        const uint32_t ixj = i | j;
+        const uint64_t a = keys[i], b = keys[ixj];
+        const bool up = (i & k) == 0;
+        if ((a > b) == up) {
+          keys[i] = b;
+          keys[ixj] = a;
         }
       }
       __syncthreads();
     }
   }
 }
-
 
 // Exact k smallest of n keys (u64, LDS) into out[0..m) sorted ascending,
 // m = min(k, n).  Keys are binned linearly on their high word between its
@@ -454,12 +455,28 @@ struct TopLTail {
 
 __device__ void TopLFinish(int qi, int L, uint32_t m, const uint64_t* sel, int32_t* out_leaf,
                            float* out_dist, const TopLTail& tail) {
-  for (int i = threadIdx.x; i < L; i += blockDim.x) {
-    const bool has = uint32_t(i) < m;
-    const int32_t leaf = has ? int32_t(sel[i] & 0xFFFFFFFFu) : -1;
-    out_leaf[size_t(qi) * L + i] = leaf;
-    out_dist[size_t(qi) * L + i] = has ? FromOrdered(uint32_t(sel[i] >> 32)) : __int_as_float(0x7fc00000);
-    if (tail.leaf_count && has) tail.rank[size_t(qi) * L + i] = atomicAdd(&tail.leaf_count[size_t(leaf) * kCounterStride], 1u);
+  // eight pairs per thread per round, their count atomics all in flight
+  // before the first returned rank is stored (one round trip per round, not
+  // per pair: L = 2000 is eight of them)
+  constexpr int U = 8;
+  for (int i0 = threadIdx.x; i0 < L; i0 += U * blockDim.x) {
+    uint32_t rk[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * int(blockDim.x);
+      if (i >= L) break;
+      const bool has = uint32_t(i) < m;
+      const int32_t leaf = has ? int32_t(sel[i] & 0xFFFFFFFFu) : -1;
+      out_leaf[size_t(qi) * L + i] = leaf;
+      out_dist[size_t(qi) * L + i] = has ? FromOrdered(uint32_t(sel[i] >> 32)) : __int_as_float(0x7fc00000);
+      if (tail.leaf_count && has) rk[u] = atomicAdd(&tail.leaf_count[size_t(leaf) * kCounterStride], 1u);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * int(blockDim.x);
+      if (i >= L) break;
+      if (tail.leaf_count && uint32_t(i) < m) tail.rank[size_t(qi) * L + i] = rk[u];
+    }
   }
   if (tail.lut.lut) {
     __syncthreads();
@@ -470,7 +487,7 @@ __device__ void TopLFinish(int qi, int L, uint32_t m, const uint64_t* sel, int32
 // Exact top-L by (score, center index) with one NT-thread block per query,
 // the row in registers (VPT scores per thread, nl <= NT * VPT; a block per
 // query, not a wave: 1000 queries must fill 1024 SIMDs several waves deep;
-// NT = 1024 for 10^4 - 6.5 * 10^4 leaves).  Linear 256-bin histograms of the
+// NT = 1024 for 10^4 - 1.6 * 10^4 leaves; above, topl_sample_kernel).  Linear 256-bin histograms of the
 // ordered score bits between the boundary set's [LO, HI] (radix digits of
 // nearby floats would all hit one bin) narrow down to the bin holding the
 // L-th score until at most 256 keys are left.  The boundary set is always a
@@ -683,13 +700,9 @@ constexpr int kLdsSelectLeaves = 16384;
 // below T plus the lowest-index ties (the reference's (distance, index)
 // order) are compacted into LDS and bitonic-sorted.  Same output as
 // topl_select_kernel.  LDS: lcap = NextPow2(min(L, nl)) u64 keys.
-__global__ void __launch_bounds__(256) topl_select_global_kernel(const float* __restrict__ scores,
-                                                                 int nl, int L, uint32_t lcap,
-                                                                 int32_t* __restrict__ out_leaf,
-                                                                 float* __restrict__ out_dist,
-                                                                 TopLTail tail) {
-  extern __shared__ uint64_t lds64[];
-  uint64_t* sel = lds64;
+__device__ void TopLGlobalSelect(const float* __restrict__ scores, int nl, int L, uint32_t lcap,
+                                 uint64_t* sel, int32_t* __restrict__ out_leaf,
+                                 float* __restrict__ out_dist, const TopLTail& tail) {
   __shared__ uint32_t hist[256];
   __shared__ uint32_t s_prefix, s_need, s_eq, s_cnt, s_tie;
   __shared__ uint32_t s_wave[4];
@@ -761,6 +774,251 @@ __global__ void __launch_bounds__(256) topl_select_global_kernel(const float* __
   __syncthreads();
   BitonicSort(sel, lcap);
   TopLFinish(qi, L, m, sel, out_leaf, out_dist, tail);
+}
+
+__global__ void __launch_bounds__(256) topl_select_global_kernel(const float* __restrict__ scores,
+                                                                 int nl, int L, uint32_t lcap,
+                                                                 int32_t* __restrict__ out_leaf,
+                                                                 float* __restrict__ out_dist,
+                                                                 TopLTail tail) {
+  extern __shared__ uint64_t lds64[];
+  TopLGlobalSelect(scores, nl, L, lcap, lds64, out_leaf, out_dist, tail);
+}
+
+// Exact top-L for many leaves (configs[4]: 50000) by a sampled threshold:
+// the k-th smallest of 2048 sampled scores (k = 1.5 L * 2048 / nl + 16,
+// found exactly by histogram rounds over 8 values per thread) is a value T at
+// or below which ~1.5 L + nl / 128 keys lie; one pass over the row compacts
+// every key with score <= T into LDS, and -- when at least L and at most cap
+// of them arrived (the L smallest keys are then all among them: at least L
+// keys have score <= T) -- a histogram select keeps the ~L smallest, a
+// counting sort by bin orders them, and the first L are the result.  Otherwise the radix select from
+// global memory (TopLGlobalSelect) runs instead; the result is the same
+// exact top-L either way.  No per-thread row in registers (the
+// register kernel spilled 56 VGPRs at 52 scores per thread).
+constexpr int kSampleVals = 8;          // samples per thread (2048 per query)
+constexpr uint32_t kSampleCap = 16384;   // most LDS keys (128 KB)
+
+__device__ uint32_t BlockKthOfSamples(const uint32_t (&v)[kSampleVals], uint32_t kk) {
+  __shared__ uint32_t hist[256], wsum[4], s_lo[4], s_hi[4], s_bin, s_below;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  uint32_t lo = 0xFFFFFFFFu, hi = 0;
+#pragma unroll
+  for (int i = 0; i < kSampleVals; ++i) {
+    lo = min(lo, v[i]);
+    hi = max(hi, v[i]);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = min(lo, uint32_t(__shfl_xor(int(lo), off)));
+    hi = max(hi, uint32_t(__shfl_xor(int(hi), off)));
+  }
+  if (lane == 0) { s_lo[wid] = lo; s_hi[wid] = hi; }
+  __syncthreads();
+  lo = min(min(s_lo[0], s_lo[1]), min(s_lo[2], s_lo[3]));
+  hi = max(max(s_hi[0], s_hi[1]), max(s_hi[2], s_hi[3]));
+  uint32_t below = 0;
+  while (lo < hi) {   // block-uniform; each round shrinks [lo, hi] ~256-fold
+    const uint64_t scale = ((uint64_t(255) << 32) + 0xFFFFFFFFull) / uint64_t(hi - lo);
+    hist[tid] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kSampleVals; ++i)
+      if (v[i] >= lo && v[i] <= hi) atomicAdd(&hist[uint32_t((uint64_t(v[i] - lo) * scale) >> 32)], 1u);
+    __syncthreads();
+    const uint32_t hv = hist[tid];
+    const uint32_t inc = BlockInclusiveScan256(hv, wsum);
+    if (below + inc - hv < kk && below + inc >= kk) {
+      s_bin = uint32_t(tid);
+      s_below = below + inc - hv;
+    }
+    __syncthreads();
+    const uint32_t b = s_bin;
+    below = s_below;
+    const uint32_t blo = lo + uint32_t(((uint64_t(b) << 32) + scale - 1) / scale);
+    const uint32_t bhi = lo + uint32_t(((uint64_t(b + 1) << 32) + scale - 1) / scale) - 1u;
+    lo = blo;
+    hi = min(bhi, hi);
+    __syncthreads();   // hist, wsum and s_bin are rewritten by the next round
+  }
+  return hi;
+}
+
+__global__ void __launch_bounds__(256) topl_sample_kernel(const float* __restrict__ scores, int nl,
+                                                          int L, uint32_t lcap, uint32_t cap,
+                                                          int32_t* __restrict__ out_leaf,
+                                                          float* __restrict__ out_dist,
+                                                          TopLTail tail) {
+  extern __shared__ uint64_t lds64[];
+  uint64_t* sel = lds64;   // [max(cap, lcap)]
+  __shared__ uint32_t s_cnt;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int qi = blockIdx.x;
+  SMX_PHASE(0, qi, 0);
+  const float* row = scores + size_t(qi) * nl;
+  const uint32_t m = min(uint32_t(L), uint32_t(nl));
+  constexpr uint32_t kSamples = 256u * kSampleVals;
+  // the samples: 64 runs of 32 consecutive scores (one 128-byte line each)
+  // at evenly spaced offsets -- a strided sample would touch every line of
+  // the row; leaf order carries no score order, and a skewed sample only
+  // costs the fallback, never exactness
+  uint32_t v[kSampleVals];
+#pragma unroll
+  for (int i = 0; i < kSampleVals; ++i) {
+    const uint32_t j = uint32_t(tid) + 256u * uint32_t(i);
+    const uint32_t run = ((uint64_t(j >> 5) * uint32_t(nl)) / (kSamples / 32u)) & ~31u;
+    v[i] = OrderedBits(row[run + (j & 31u)]);
+  }
+  const uint32_t kk = min(kSamples, uint32_t((uint64_t(3 * m) * kSamples) / (2u * uint32_t(nl))) + 16u);
+  SMX_PHASE(0, qi, 1);
+  uint32_t T = 0;   // the threshold, set below once the first chunk's loads are issued
+  // One sweep of the row, 16 scores per thread per chunk with the next chunk's
+  // loads in flight; a wave reserves its chunk's slots with one LDS atomic
+  // (per-lane counts up to 16 prefix-summed over five ballots).
+  constexpr int kPass = 16;
+  constexpr int kChunk = 256 * kPass;
+  const uint64_t below = (1ull << lane) - 1ull;
+  auto load = [&](uint32_t (&x)[kPass], int c0) {
+    // clamped, unconditional loads (a guarded load becomes a branch with its
+    // own vmcnt(0) wait); take() masks the positions past nl
+#pragma unroll
+    for (int i = 0; i < kPass; ++i) x[i] = OrderedBits(row[min(c0 + 256 * i + tid, nl - 1)]);
+  };
+  auto take = [&](const uint32_t (&x)[kPass], int c0) {
+    uint32_t mask = 0;
+#pragma unroll
+    for (int i = 0; i < kPass; ++i)
+      if (c0 + 256 * i + tid < nl && x[i] <= T) mask |= 1u << i;
+    const uint32_t n_in = uint32_t(__popc(mask));
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+      const uint64_t bb = __ballot((n_in >> b) & 1u);
+      pre += uint32_t(__popcll(bb & below)) << b;
+      tot += uint32_t(__popcll(bb)) << b;
+    }
+    if (tot == 0) return;   // (wave-uniform)
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&s_cnt, tot);
+    uint32_t pos = uint32_t(__shfl(int(base), 0)) + pre;
+#pragma unroll
+    for (int i = 0; i < kPass; ++i)
+      if ((mask >> i) & 1u) {
+        if (pos < cap) sel[pos] = (uint64_t(x[i]) << 32) | uint32_t(c0 + 256 * i + tid);
+        ++pos;
+      }
+  };
+  uint32_t xa[kPass], xb[kPass];
+  load(xa, 0);   // (independent of T: in flight during the threshold rounds)
+  T = BlockKthOfSamples(v, kk);
+  SMX_PHASE(0, qi, 2);
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < nl; c0 += 2 * kChunk) {
+    if (c0 + kChunk < nl) load(xb, c0 + kChunk);
+    take(xa, c0);
+    if (c0 + kChunk >= nl) break;
+    if (c0 + 2 * kChunk < nl) load(xa, c0 + 2 * kChunk);
+    take(xb, c0 + kChunk);
+  }
+  __syncthreads();
+  SMX_PHASE(0, qi, 3);
+  const uint32_t cnt = s_cnt;
+  if (cnt < m || cnt > cap) {   // (block-uniform) the sample missed: exact radix select
+    __syncthreads();
+    TopLGlobalSelect(scores, nl, L, lcap, sel, out_leaf, out_dist, tail);
+    return;
+  }
+  // Exact select and order inside LDS: 2048 linear bins of the score bits
+  // between the smallest compacted score and T.  The keys of the bins up to
+  // the one holding the m-th key (m plus about one bin) are scattered after
+  // the compacted keys in bin order (a counting sort), then each is ranked
+  // among the few keys of its own bin -- O(keys), no sorting network.  A
+  // crowded bin (more than kBinRankMax keys: near-ties) bitonic-sorts them
+  // instead; if they do not fit, all cnt keys are sorted in place.
+  constexpr uint32_t kBinRankMax = 256;
+  __shared__ uint32_t hist[kSelBins], wsum[4], s_min, s_bsel, s_c, s_maxbin;
+  if (tid == 0) { s_min = 0xFFFFFFFFu; s_bsel = kSelBins - 1; s_c = cnt; s_maxbin = 0; }
+  for (uint32_t b = tid; b < kSelBins; b += 256) hist[b] = 0;
+  uint32_t lo = 0xFFFFFFFFu;
+  for (uint32_t i = tid; i < cnt; i += 256) lo = min(lo, uint32_t(sel[i] >> 32));
+  for (int off = 32; off > 0; off >>= 1) lo = min(lo, uint32_t(__shfl_xor(int(lo), off)));
+  __syncthreads();
+  if (lane == 0) atomicMin(&s_min, lo);
+  __syncthreads();
+  lo = s_min;
+  // bin(v) = ((v - lo) * scale) >> 32 < kSelBins, monotone; (v - lo) < span
+  // keeps the product below 2^43
+  const uint64_t span = uint64_t(T - lo) + 1;
+  const uint64_t scale = ((uint64_t(kSelBins) << 32) - 1) / span;
+  auto bin_of = [&](uint64_t key) {
+    return uint32_t((uint64_t(uint32_t(key >> 32) - lo) * scale) >> 32);
+  };
+  for (uint32_t i = tid; i < cnt; i += 256) atomicAdd(&hist[bin_of(sel[i])], 1u);
+  __syncthreads();
+  constexpr uint32_t per = kSelBins / 256;
+  uint32_t h[per], local = 0;
+#pragma unroll
+  for (uint32_t u = 0; u < per; ++u) {
+    h[u] = hist[tid * per + u];
+    local += h[u];
+  }
+  const uint32_t incl = BlockInclusiveScan256(local, wsum);
+  uint32_t run = incl - local, mx = 0;
+  const bool owner = run < m && incl >= m;
+#pragma unroll
+  for (uint32_t u = 0; u < per; ++u) {   // bins -> exclusive offsets, in place
+    hist[tid * per + u] = run;
+    if (owner && run < m && run + h[u] >= m) { s_bsel = tid * per + u; s_c = run + h[u]; }
+    run += h[u];
+  }
+  __syncthreads();
+  const uint32_t bsel = s_bsel, c = s_c;
+#pragma unroll
+  for (uint32_t u = 0; u < per; ++u)
+    if (tid * per + u <= bsel) mx = max(mx, h[u]);
+  for (int off = 32; off > 0; off >>= 1) mx = max(mx, uint32_t(__shfl_xor(int(mx), off)));
+  if (lane == 0) atomicMax(&s_maxbin, mx);
+  uint64_t* out = sel + cnt;
+  const uint32_t out_cap = cap - cnt;
+  const uint64_t* res = sel;
+  if (c > out_cap) {   // (block-uniform) no room after the keys: sort them all in place
+    const uint32_t np2 = NextPow2(cnt);
+    for (uint32_t i = cnt + tid; i < np2; i += 256) sel[i] = ~0ull;
+    __syncthreads();
+    BitonicSort(sel, np2);
+  } else {
+    for (uint32_t i = tid; i < cnt; i += 256) {   // counting-sort scatter by bin
+      const uint64_t key = sel[i];
+      const uint32_t b = bin_of(key);
+      if (b <= bsel) out[atomicAdd(&hist[b], 1u)] = key;
+    }
+    __syncthreads();   // hist[b] = end of bin b = start of bin b + 1
+    if (s_maxbin <= kBinRankMax) {
+      for (uint32_t p = tid; p < c; p += 256) {
+        const uint64_t key = out[p];
+        const uint32_t b = bin_of(key);
+        const uint32_t s0 = b ? hist[b - 1] : 0u, e0 = hist[b];
+        uint32_t r = 0;
+        for (uint32_t q = s0; q < e0; ++q) r += out[q] < key ? 1u : 0u;   // keys are unique
+        sel[s0 + r] = key;
+      }
+      __syncthreads();
+    } else if (NextPow2(c) <= out_cap) {
+      const uint32_t np2 = NextPow2(c);
+      for (uint32_t i = c + tid; i < np2; i += 256) out[i] = ~0ull;
+      __syncthreads();
+      BitonicSort(out, np2);
+      res = out;
+    } else {
+      const uint32_t np2 = NextPow2(cnt);
+      for (uint32_t i = cnt + tid; i < np2; i += 256) sel[i] = ~0ull;
+      __syncthreads();
+      BitonicSort(sel, np2);
+    }
+  }
+  SMX_PHASE(0, qi, 4);
+  TopLFinish(qi, L, m, res, out_leaf, out_dist, tail);
+  SMX_PHASE(0, qi, 5);
 }
 
 constexpr int kGroups = kWorkGroups;   // XCD groups of the work list
@@ -3281,9 +3539,20 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   } else if (L <= kWaveTopL && ix.nl <= 1024 * 16) {
     hipLaunchKernelGGL((topl_block_kernel<16, 1024>), dim3(nq), dim3(1024), 0, s, scores, ix.nl,
                        L, out_leaf, out_dist, tail);
-  } else if (L <= kWaveTopL && ix.nl <= 1024 * 52) {
-    hipLaunchKernelGGL((topl_block_kernel<52, 1024>), dim3(nq), dim3(1024), 0, s, scores, ix.nl,
-                       L, out_leaf, out_dist, tail);
+  } else if (ix.nl > 1024 * 16 && L <= 4096) {
+    // many leaves (configs[4]): the sampled threshold, exact
+    uint32_t lcap = 1;
+    while (lcap < uint32_t(std::min(L, ix.nl))) lcap <<= 1;
+    // LDS keys: the compacted keys (expected 1.5 L + 16 nl / 2048, room for
+    // 1.3x that) plus the appended select output (~L), a power of two from
+    // 2048 up to kSampleCap; more keys take the exact fallback
+    const uint64_t m = uint64_t(std::min(L, ix.nl));
+    const uint64_t expect = (3ull * m) / 2 + (16ull * uint64_t(ix.nl)) / 2048;
+    uint32_t cap = 2048;
+    while (cap < kSampleCap && cap < (13 * expect) / 10 + m + m / 16 + 64) cap <<= 1;
+    const size_t lds_s = size_t(std::max(cap, lcap)) * 8;
+    hipLaunchKernelGGL(topl_sample_kernel, dim3(nq), dim3(256), lds_s, s, scores, ix.nl, L, lcap,
+                       cap, out_leaf, out_dist, tail);
   } else if (ix.nl <= kLdsSelectLeaves && lds + kStaticLds <= 160 * 1024) {
     hipLaunchKernelGGL(topl_select_kernel, dim3(nq), dim3(256), lds, s, scores, ix.nl, L, kcap,
                        out_leaf, out_dist, tail);

@@ -59,18 +59,19 @@ def test_partition_topl_many_leaves(native, oracle, nl, metric):
         np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
 
 
-@pytest.mark.parametrize("nl", [1000, 5000, 20000])
+@pytest.mark.parametrize("nl", [1000, 5000, 20000, 50000])
 def test_partition_topl_all_ties(native, oracle, nl):
     """Every center identical: the L lowest leaf indices, in index order
-    (wave select, block select and global-memory select)."""
+    (wave select, block select, global-memory select, and the sampled
+    threshold's fallback: every key ties the sampled threshold)."""
     ix, q = _random_index(nl, 30000, 16, 0, seed=5, dup=False)
     ix.centers[:] = ix.centers[0]
     n = native.NativeIndex(ix)
-    for L in (1, 37, 300, 700):
+    for L in (1, 37, 300, 700, 4096):
         gl, gd = n.partition_topl(q, L)
         ol, od = oracle.partition_topl(q, ix.centers, ix.metric, L)
         np.testing.assert_array_equal(gl, ol)
-        np.testing.assert_array_equal(gl[0], np.arange(L))
+        np.testing.assert_array_equal(gl[0][:min(L, nl)], np.arange(min(L, nl)))
         np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
 
 
@@ -89,4 +90,22 @@ def test_search_many_leaves_matches_oracle(native, oracle, nl, metric):
         gi, gd, gc = n.search_batched(q, leaves, pre, 10, True)
         oi, od, oc = oracle.search(ix, q, leaves, pre, 10, True, oracle.MODE_IDEAL)
         np.testing.assert_array_equal(gi, oi)
+        np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+
+
+@pytest.mark.parametrize("ntie", [100, 600, 3000])
+def test_partition_topl_crowded_ties(native, oracle, ntie):
+    """50000 leaves of which `ntie` share one center next to every query: the
+    L nearest are (mostly) one tie group, ordered by leaf index -- the sampled
+    kernel's crowded-bin and in-place sort paths."""
+    ix, q = _random_index(50000, 60000, 16, 0, seed=11 + ntie, dup=False)
+    rng = np.random.default_rng(ntie)
+    tied = rng.choice(50000, ntie, replace=False)
+    ix.centers[tied] = ix.centers[tied[0]]
+    q[:] = ix.centers[tied[0]] + 0.01 * rng.standard_normal(q.shape).astype(np.float32)
+    n = native.NativeIndex(ix)
+    for L in (50, 400, 2000):
+        gl, gd = n.partition_topl(q, L)
+        ol, od = oracle.partition_topl(q, ix.centers, ix.metric, L)
+        np.testing.assert_array_equal(gl, ol)
         np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
