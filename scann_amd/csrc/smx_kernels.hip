@@ -252,6 +252,84 @@ __device__ uint32_t SelectSmallest(uint64_t* keys, uint32_t n, uint32_t k, uint6
   return m;
 }
 
+// Orders the m smallest of the n unique keys keys[0..n) (u64 in LDS, high
+// words in [?, hi]) into res[0..m) ascending, in O(n): NBINS linear bins of
+// the high word between the keys' minimum and hi; the keys of the bins up to
+// the one holding the m-th are scattered to tmp in bin order (a counting
+// sort) and each is then ranked among the keys of its own bin.  res may alias
+// keys (keys are not read after the scatter).  Returns false, with res
+// unwritten, when those keys exceed tmp_cap or a bin holds more than
+// kBinRankMax of them (near-ties): the caller orders the keys another way.
+// 256 threads; all call; block-uniform result.
+constexpr uint32_t kBinRankMax = 256;
+
+template <uint32_t NBINS>
+__device__ bool OrderSmallestByBins(const uint64_t* keys, uint32_t n, uint32_t m, uint32_t hi,
+                                    uint64_t* tmp, uint32_t tmp_cap, uint64_t* res) {
+  static_assert(NBINS % 256 == 0, "bins per thread");
+  __shared__ uint32_t hist[NBINS], wsum[4], s_min, s_bsel, s_c, s_maxbin;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  if (tid == 0) { s_min = 0xFFFFFFFFu; s_bsel = NBINS - 1; s_c = n; s_maxbin = 0; }
+  for (uint32_t b = tid; b < NBINS; b += 256) hist[b] = 0;
+  uint32_t lo = 0xFFFFFFFFu;
+  for (uint32_t i = tid; i < n; i += 256) lo = min(lo, uint32_t(keys[i] >> 32));
+  for (int off = 32; off > 0; off >>= 1) lo = min(lo, uint32_t(__shfl_xor(int(lo), off)));
+  __syncthreads();
+  if (lane == 0) atomicMin(&s_min, lo);
+  __syncthreads();
+  lo = s_min;
+  // bin(v) = ((v - lo) * scale) >> 32 < NBINS, monotone; (v - lo) < span keeps
+  // the product below 2^(32 + log2 NBINS)
+  const uint64_t span = uint64_t(hi - lo) + 1;
+  const uint64_t scale = ((uint64_t(NBINS) << 32) - 1) / span;
+  auto bin_of = [&](uint64_t key) {
+    return uint32_t((uint64_t(uint32_t(key >> 32) - lo) * scale) >> 32);
+  };
+  for (uint32_t i = tid; i < n; i += 256) atomicAdd(&hist[bin_of(keys[i])], 1u);
+  __syncthreads();
+  constexpr uint32_t per = NBINS / 256;
+  uint32_t h[per], local = 0;
+#pragma unroll
+  for (uint32_t u = 0; u < per; ++u) {
+    h[u] = hist[tid * per + u];
+    local += h[u];
+  }
+  const uint32_t incl = BlockInclusiveScan256(local, wsum);
+  uint32_t run = incl - local, mx = 0;
+  const bool owner = run < m && incl >= m;
+#pragma unroll
+  for (uint32_t u = 0; u < per; ++u) {   // bins -> exclusive offsets, in place
+    hist[tid * per + u] = run;
+    if (owner && run < m && run + h[u] >= m) { s_bsel = tid * per + u; s_c = run + h[u]; }
+    run += h[u];
+  }
+  __syncthreads();
+  const uint32_t bsel = s_bsel, c = s_c;
+#pragma unroll
+  for (uint32_t u = 0; u < per; ++u)
+    if (tid * per + u <= bsel) mx = max(mx, h[u]);
+  for (int off = 32; off > 0; off >>= 1) mx = max(mx, uint32_t(__shfl_xor(int(mx), off)));
+  if (lane == 0) atomicMax(&s_maxbin, mx);
+  __syncthreads();
+  if (c > tmp_cap || s_maxbin > kBinRankMax) return false;   // (block-uniform)
+  for (uint32_t i = tid; i < n; i += 256) {   // counting-sort scatter by bin
+    const uint64_t key = keys[i];
+    const uint32_t b = bin_of(key);
+    if (b <= bsel) tmp[atomicAdd(&hist[b], 1u)] = key;
+  }
+  __syncthreads();   // hist[b] = end of bin b = start of bin b + 1
+  for (uint32_t p = tid; p < c; p += 256) {
+    const uint64_t key = tmp[p];
+    const uint32_t b = bin_of(key);
+    const uint32_t s0 = b ? hist[b - 1] : 0u, e0 = hist[b];
+    uint32_t r = s0;
+    for (uint32_t q = s0; q < e0; ++q) r += tmp[q] < key ? 1u : 0u;   // keys are unique
+    if (r < m) res[r] = key;
+  }
+  __syncthreads();
+  return true;
+}
+
 // ---------------------------------------------------------------------------
 // Query tokenization on the f32 MFMA.  v_mfma_f32_32x32x2_f32 computes
 // D = fma(a_k1, b_k1, fma(a_k0, b_k0, C)) with one rounding per step, so
@@ -928,94 +1006,17 @@ __global__ void __launch_bounds__(256) topl_sample_kernel(const float* __restric
     TopLGlobalSelect(scores, nl, L, lcap, sel, out_leaf, out_dist, tail);
     return;
   }
-  // Exact select and order inside LDS: 2048 linear bins of the score bits
-  // between the smallest compacted score and T.  The keys of the bins up to
-  // the one holding the m-th key (m plus about one bin) are scattered after
-  // the compacted keys in bin order (a counting sort), then each is ranked
-  // among the few keys of its own bin -- O(keys), no sorting network.  A
-  // crowded bin (more than kBinRankMax keys: near-ties) bitonic-sorts them
-  // instead; if they do not fit, all cnt keys are sorted in place.
-  constexpr uint32_t kBinRankMax = 256;
-  __shared__ uint32_t hist[kSelBins], wsum[4], s_min, s_bsel, s_c, s_maxbin;
-  if (tid == 0) { s_min = 0xFFFFFFFFu; s_bsel = kSelBins - 1; s_c = cnt; s_maxbin = 0; }
-  for (uint32_t b = tid; b < kSelBins; b += 256) hist[b] = 0;
-  uint32_t lo = 0xFFFFFFFFu;
-  for (uint32_t i = tid; i < cnt; i += 256) lo = min(lo, uint32_t(sel[i] >> 32));
-  for (int off = 32; off > 0; off >>= 1) lo = min(lo, uint32_t(__shfl_xor(int(lo), off)));
-  __syncthreads();
-  if (lane == 0) atomicMin(&s_min, lo);
-  __syncthreads();
-  lo = s_min;
-  // bin(v) = ((v - lo) * scale) >> 32 < kSelBins, monotone; (v - lo) < span
-  // keeps the product below 2^43
-  const uint64_t span = uint64_t(T - lo) + 1;
-  const uint64_t scale = ((uint64_t(kSelBins) << 32) - 1) / span;
-  auto bin_of = [&](uint64_t key) {
-    return uint32_t((uint64_t(uint32_t(key >> 32) - lo) * scale) >> 32);
-  };
-  for (uint32_t i = tid; i < cnt; i += 256) atomicAdd(&hist[bin_of(sel[i])], 1u);
-  __syncthreads();
-  constexpr uint32_t per = kSelBins / 256;
-  uint32_t h[per], local = 0;
-#pragma unroll
-  for (uint32_t u = 0; u < per; ++u) {
-    h[u] = hist[tid * per + u];
-    local += h[u];
-  }
-  const uint32_t incl = BlockInclusiveScan256(local, wsum);
-  uint32_t run = incl - local, mx = 0;
-  const bool owner = run < m && incl >= m;
-#pragma unroll
-  for (uint32_t u = 0; u < per; ++u) {   // bins -> exclusive offsets, in place
-    hist[tid * per + u] = run;
-    if (owner && run < m && run + h[u] >= m) { s_bsel = tid * per + u; s_c = run + h[u]; }
-    run += h[u];
-  }
-  __syncthreads();
-  const uint32_t bsel = s_bsel, c = s_c;
-#pragma unroll
-  for (uint32_t u = 0; u < per; ++u)
-    if (tid * per + u <= bsel) mx = max(mx, h[u]);
-  for (int off = 32; off > 0; off >>= 1) mx = max(mx, uint32_t(__shfl_xor(int(mx), off)));
-  if (lane == 0) atomicMax(&s_maxbin, mx);
-  uint64_t* out = sel + cnt;
-  const uint32_t out_cap = cap - cnt;
-  const uint64_t* res = sel;
-  if (c > out_cap) {   // (block-uniform) no room after the keys: sort them all in place
+  // Exact select and order inside LDS (OrderSmallestByBins: the ~L smallest
+  // counting-sorted by bin after the compacted keys, ranked inside their
+  // bins, written back over the keys); near-ties or no room after the keys:
+  // a bitonic sort of all cnt keys in place (cap is a power of two)
+  if (!OrderSmallestByBins<kSelBins>(sel, cnt, m, T, sel + cnt, cap - cnt, sel)) {
     const uint32_t np2 = NextPow2(cnt);
     for (uint32_t i = cnt + tid; i < np2; i += 256) sel[i] = ~0ull;
     __syncthreads();
     BitonicSort(sel, np2);
-  } else {
-    for (uint32_t i = tid; i < cnt; i += 256) {   // counting-sort scatter by bin
-      const uint64_t key = sel[i];
-      const uint32_t b = bin_of(key);
-      if (b <= bsel) out[atomicAdd(&hist[b], 1u)] = key;
-    }
-    __syncthreads();   // hist[b] = end of bin b = start of bin b + 1
-    if (s_maxbin <= kBinRankMax) {
-      for (uint32_t p = tid; p < c; p += 256) {
-        const uint64_t key = out[p];
-        const uint32_t b = bin_of(key);
-        const uint32_t s0 = b ? hist[b - 1] : 0u, e0 = hist[b];
-        uint32_t r = 0;
-        for (uint32_t q = s0; q < e0; ++q) r += out[q] < key ? 1u : 0u;   // keys are unique
-        sel[s0 + r] = key;
-      }
-      __syncthreads();
-    } else if (NextPow2(c) <= out_cap) {
-      const uint32_t np2 = NextPow2(c);
-      for (uint32_t i = c + tid; i < np2; i += 256) out[i] = ~0ull;
-      __syncthreads();
-      BitonicSort(out, np2);
-      res = out;
-    } else {
-      const uint32_t np2 = NextPow2(cnt);
-      for (uint32_t i = cnt + tid; i < np2; i += 256) sel[i] = ~0ull;
-      __syncthreads();
-      BitonicSort(sel, np2);
-    }
   }
+  const uint64_t* res = sel;
   SMX_PHASE(0, qi, 4);
   TopLFinish(qi, L, m, res, out_leaf, out_dist, tail);
   SMX_PHASE(0, qi, 5);
