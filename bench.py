@@ -13,10 +13,16 @@ dedupe, exact reorder and sort all inside the step).
 `--config sift` measures BASELINE.json configs[2] (SIFT1M shape, squared L2,
 2000 leaves) as a secondary line; the default is the metric's configuration.
 
-For N > 1 the driver starts one rank per GPU with torch.distributed.run;
-every rank holds a replica of the index and searches its own batch of 1000
-queries (queries shard with no collective: "weak" scaling), the step time is
-the max over ranks.  Prints ONE JSON line on rank 0.
+`--gpus N` runs N ranks, one process per GPU.  Started under a launcher
+(torch.distributed.run sets WORLD_SIZE), WORLD_SIZE must equal N; started
+directly with N > 1, bench.py relaunches itself under
+`python -m torch.distributed.run --nproc-per-node N` before anything touches
+the GPU and exits with the launcher's status (`launch_plan`).  For glove /
+SIFT every rank holds a replica of the index and searches its own batch of
+1000 queries (queries shard with no collective: "weak" scaling); for
+soar100m / deep1b the N = 8 ranks hold the 8 shards of the range split and
+search one batch jointly (RangeSplitSearcher: shard search, one all-gather,
+merge).  The step time is the max over ranks.  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -32,6 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 NQ = 1000
+PARITY_QUERIES = 64
 LEAVES = 1000
 LEAVES_TO_SEARCH = 100
 PRE_NN = 100
@@ -66,6 +73,7 @@ CONFIGS = {
     "soar100m": dict(n=100_000_000, leaves=10000, leaves_to_search=100, metric=0, seed=4,
                      generated=True, split=8, soar=1.5, dim=96, components=4096,
                      train_sample=250_000, sweep=[20, 40, 60, 100],
+                     parity_points=[(100, 100), (1000, 256)],
                      workload="configs[3]: synthetic 100M x 96 dot product + SOAR (lambda 1.5, "
                               "overretrieve 2), tree-AH 10000 leaves, LUT16 AH 48 blocks x 2 "
                               "dims, leaves_to_search=100, reorder 100, k=10, batch=1000, "
@@ -79,6 +87,7 @@ CONFIGS = {
                    generated=True, split=8, soar=None, dim=96, components=1 << 17,
                    train_sample=5_000_000, train_iterations=10,
                    sweep=[400, 800, 1200, 2000, [800, 256], [2000, 256], [4000, 256]],
+                   parity_points=[(400, 100), (2000, 256)],
                    workload="configs[4]: Deep1B shape 1e9 x 96 dot product, tree-AH 50000 "
                             "leaves, LUT16 AH 48 blocks x 2 dims, leaves_to_search=400, reorder "
                             "100, k=10, batch=1000, dataset sharded 8 ways: one rank's shard "
@@ -312,7 +321,42 @@ def cpu_baseline_restatement(ix, q, gpu_idx, threads):
                 id_mismatch_vs_gpu=float((out[0] != gpu_idx).mean()))
 
 
+def launch_plan(gpus, env, argv, port=None):
+    """What `bench.py --gpus N` does before touching the GPU:
+    ("run", world) -- run as one rank of `world` (WORLD_SIZE, or 1);
+    ("relaunch", cmd) -- N > 1 with no launcher: start N ranks with
+    torch.distributed.run (rendezvous on 127.0.0.1) and exit with its status;
+    ("error", message) -- --gpus disagrees with the launcher's WORLD_SIZE."""
+    if gpus < 1:
+        return ("error", f"--gpus must be >= 1 (got {gpus})")
+    world_env = env.get("WORLD_SIZE")
+    if world_env is None:
+        if gpus == 1:
+            return ("run", 1)
+        if port is None:
+            import socket
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+        return ("relaunch", [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                             f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1",
+                             f"--master-port={port}", os.path.abspath(__file__)] + list(argv))
+    if int(world_env) != gpus:
+        return ("error", f"--gpus {gpus} but the launcher started WORLD_SIZE={world_env} ranks")
+    return ("run", gpus)
+
+
 def main():
+    plan = launch_plan(_peek_gpus(sys.argv[1:]), os.environ, sys.argv[1:])
+    if plan[0] == "error":
+        print(f"bench.py: {plan[1]}", file=sys.stderr)
+        sys.exit(2)
+    if plan[0] == "relaunch":
+        # a child process, not exec: this process has not touched the GPU
+        import subprocess
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        sys.exit(subprocess.call(plan[1], env=env))
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -324,6 +368,8 @@ def main():
     ap.add_argument("--no-sweep", action="store_true",
                     help="skip the leaves_to_search QPS-recall operating points")
     ap.add_argument("--sweep-steps", type=int, default=20)
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the oracle check of the generated-shard lines")
     args = ap.parse_args()
     global CFG, LEAVES, LEAVES_TO_SEARCH
     CFG = CONFIGS[args.config]
@@ -362,7 +408,7 @@ def main():
         nat.search_batched_device(qd.data_ptr(), NQ, leaves, PRE_NN, FINAL_NN, True,
                                   out_idx.data_ptr(), out_dist.data_ptr(), out_cnt.data_ptr())
 
-    # timed steps: the library replays its captured hipGraph of the pipeline
+    # timed steps: eager launches of the six pipeline kernels per step
     nat.set_profiling(False)
     for _ in range(args.warmup):
         step()
@@ -507,7 +553,7 @@ def main_generated(args, rank, world, local, dist, dev):
     itself is not in the single-GPU step)."""
     import torch
     from scann_amd import generate, synthetic
-    from scann_amd.distributed import NativeShardEngine, all_gather_entries
+    from scann_amd.distributed import NativeShardEngine, RangeSplitSearcher, all_gather_entries
     split = CFG["split"]
     if world not in (1, split):
         raise SystemExit(f"--config {args.config}: run with 1 or {split} ranks")
@@ -565,9 +611,16 @@ def main_generated(args, rank, world, local, dist, dev):
             el = float(tt.item())
         return el
 
+    # the N-rank step is the searcher the distributed module exports
+    # (RangeSplitSearcher: shard search, one all-gather, merge on every rank)
+    searcher = RangeSplitSearcher(eng, world) if world == split else None
+
     def step():
-        search()
-        merge()
+        if searcher is not None:
+            res["out"] = searcher.search_batched(qd, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True)
+        else:
+            search()
+            merge()
 
     for _ in range(args.warmup):
         step()
@@ -671,6 +724,9 @@ def main_generated(args, rank, world, local, dist, dev):
                          ("partition_ms", "invert_ms", "seed_scan_ms", "scan_ms", "select_ms",
                           "total_ms")},
         }
+        if not args.no_parity:
+            result["parity_vs_oracle"] = shard_parity(
+                ix, eng, q, CFG["parity_points"], args.cpu_threads or host_threads()[0], local)
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline_shard(ix, q, args.cpu_threads or host_threads()[0])
         print(json.dumps(result), flush=True)
@@ -698,20 +754,61 @@ def _generated_truth(ds, q, r0, r1, dev):
     return best_i.cpu().numpy()
 
 
+def shard_parity(ix, eng, q, points, threads, device):
+    """parity_vs_oracle of a shard line at workload size: rank 0's shard as a
+    standalone index (TreeAHIndex.standalone: the same leaves, codes, ties
+    and float rows) searched on the GPU and by the oracle (ideal mode) on
+    PARITY_QUERIES queries, per (leaves_to_search, pre_reorder_nn) point:
+    ids and distance bits must be equal.  For a disjoint index the shard
+    engine's own list (search_shard + merge of the one list) must give the
+    same neighbors by global id."""
+    import torch
+    from oracle import binding as oracle
+    from scann_amd import _native
+    oracle.build()
+    view = ix.standalone()
+    sub = q[:PARITY_QUERIES]
+    nv = _native.NativeIndex(view, device=device)
+    out = []
+    try:
+        for lv, pre in points:
+            t = time.perf_counter()
+            gi, gd, gc = nv.search_batched(sub, lv, pre, FINAL_NN, True)
+            oi, od, oc = oracle.search(view, sub, lv, pre, FINAL_NN, True, oracle.MODE_IDEAL,
+                                       threads)
+            ent = {"leaves_to_search": lv, "pre_reorder_nn": pre, "queries": int(sub.shape[0]),
+                   "id_mismatch": float((gi != oi).mean()),
+                   "dist_bits_mismatch": float((gd.view(np.uint32) != od.view(np.uint32)).mean()),
+                   "count_mismatch": int((gc != oc).sum()),
+                   "max_rel_dist_err": float(np.max(np.abs(gd - od) /
+                                                    np.maximum(np.abs(od), 1e-30)))}
+            if ix.disjoint:
+                qd = torch.from_numpy(sub).to(eng.device)
+                k = eng.shard_width(lv, pre, FINAL_NN, True)
+                le = torch.empty((sub.shape[0], k, 2), dtype=torch.int64, device=eng.device)
+                eng.search_shard(qd, lv, pre, FINAL_NN, True, le)
+                si, sd, _ = eng.merge(1, le.unsqueeze(0), sub.shape[0], lv, pre, FINAL_NN, True)
+                torch.cuda.synchronize()
+                ent["shard_engine_id_mismatch"] = float(
+                    (si.cpu().numpy().astype(np.uint32) != ix.leaf_members[oi]).mean())
+            ent["oracle_s"] = round(time.perf_counter() - t, 2)
+            log(f"parity L={lv} pre={pre}: {ent}")
+            out.append(ent)
+    finally:
+        nv.close()
+    return {"index": "rank 0's shard as a standalone index (TreeAHIndex.standalone)",
+            "mode": "oracle ideal mode (oracle/scann_oracle.cc) vs the GPU, bit-exact ids and "
+                    "distances", "points": out}
+
+
 def cpu_baseline_shard(ix, q, threads):
     """The AVX2 port over this rank's shard viewed as a standalone index
     (members renumbered 0..M-1, their float rows as the dataset): the
     reference's per-rank work, timed on a bounded sample of the batch."""
     from oracle import binding as oracle
-    from scann_amd.index import TreeAHIndex
     oracle.build()
     m = ix.num_members
-    view = TreeAHIndex(metric=ix.metric, dim=ix.dim, num_blocks=ix.num_blocks,
-                       dims_per_block=ix.dims_per_block, residual=ix.residual,
-                       centers=ix.centers, codebook=ix.codebook, leaf_offsets=ix.leaf_offsets,
-                       leaf_members=np.arange(m, dtype=np.uint32), member_codes=ix.member_codes,
-                       num_datapoints=m, dataset=ix.member_rows,
-                       spilling_overretrieve_factor=ix.spilling_overretrieve_factor)
+    view = ix.standalone()
     port = oracle.Avx2Port(view)
     model, isa = cpu_info()
     sub = q[:max(threads, 250)]
@@ -727,6 +824,13 @@ def cpu_baseline_shard(ix, q, threads):
                 sample=f"median of 3 runs of {sub.shape[0]} queries through the AVX2 port over "
                        f"this rank's shard as a standalone index ({m} members renumbered, "
                        f"emulate-mode pipeline A), {threads} threads; no merge")
+
+
+def _peek_gpus(argv):
+    """--gpus from the command line (argparse proper runs in main())."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    return ap.parse_known_args(argv)[0].gpus
 
 
 if __name__ == "__main__":

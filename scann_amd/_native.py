@@ -97,8 +97,12 @@ def load(path: str = LIB_PATH):
     # torch first: it brings its own HIP/HSA runtime, which the library then
     # binds by soname.  Loaded the other way round, /opt/rocm's runtime comes
     # in first and torch's later device init fails ("No HIP GPUs are
-    # available") -- one process, one runtime.
-    import torch  # noqa: F401
+    # available") -- one process, one runtime (load order).
+    # Without torch the library binds /opt/rocm's runtime by itself.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -66,6 +66,10 @@ struct DeviceIndex {
   float* dataset = nullptr;     // [num_datapoints][dim] or null
   uint32_t* row_base = nullptr; // [nl] shard's first row in each whole leaf, or null
   float* member_rows = nullptr; // [num_members][dim] shard rows for the reorder, or null
+  // with member_rows: [num_datapoints] global id -> a member slot holding it
+  // (0xFFFFFFFF: not in this shard); the reorder row of a candidate known by
+  // its global id (ties by global id, shift 0; the block select's gid space)
+  uint32_t* row_of = nullptr;
 };
 
 // smx_shard_entry (include/scann_mi355x.h)
@@ -113,17 +117,6 @@ struct ItemLane {
 };
 constexpr uint32_t kNoQuery = 0xFFFFFFFFu;     // ItemLane::qid of an empty slot
 
-// One leaf position of the work order (the fused front end's work list: the
-// scan derives its work items from these instead of a materialized list):
-// the position's first work item, its leaf, size, pair count and layout.
-struct PosDesc {
-  uint32_t item0;
-  uint32_t leaf;
-  uint32_t n;
-  uint32_t cnt;
-  uint64_t tile_off;
-  uint64_t member_off;
-};
 constexpr int32_t kNoSum = -2147483647 - 1;   // the sum limit of an empty slot
 
 struct ScanArgs {
@@ -131,12 +124,8 @@ struct ScanArgs {
   const uint32_t* members;
   const int8_t* lut;          // [nq][2K][16]
   const float* inv;           // [nq]
-  const WorkItem* work;       // [work items] (materialized list; null with pos)
-  const ItemLane* lanes;      // [work items][32] or [nl][slot_stride] (leaf slots, with pos)
-  const PosDesc* pos;         // [nl] fused front end: items derived from the positions
-  const uint32_t* pos_unit0;  // [nl + 1] (with pos) each position's first unit
-  const uint32_t* gunits;     // [9] (with pos) the XCD groups' unit boundaries
-  uint32_t slot_stride;       // leaf slots per leaf (with pos)
+  const WorkItem* work;       // [work items]
+  const ItemLane* lanes;      // [work items][32]
   uint32_t chunk_tiles;
   const uint4* wave_start;    // [grid] {first item, first tile, tiles, first position}
   uint32_t num_items;
@@ -161,8 +150,6 @@ struct SeedArgs {
   const uint32_t* rank;       // [nq][L] position inside the leaf's list
   const uint32_t* leaf_item0; // [nl] the leaf's first work item
   ItemLane* lanes;            // [work items][32]
-  ItemLane* leaf_slots;       // fused front end: [nl][slot_stride], slot = rank
-  uint32_t slot_stride;
   uint32_t chunk_tiles;
   const int8_t* lut;          // [nq][2K][16]
   const float* inv;
@@ -198,8 +185,6 @@ struct WorklistArgs {
   WorkItem* work;
   ItemLane* lanes;
   uint4* wave_start;           // [grid]
-  PosDesc* pos;                // [nl] (fused front end)
-  uint32_t* done;              // top-L blocks finished (fused front end; zeroed per call)
   Bounds bd;                  // debug-build index checks
 };
 // Up to this many leaves the work list is built by one extra block of the
@@ -258,6 +243,7 @@ struct SelectArgs {
   ShardEntry* shard_out;      // shard mode: [nq][kk] local top-k' entries (or NULL)
   const uint32_t* row_base;   // shard: whole-leaf row of each leaf's first shard row
   const float* member_rows;   // shard: [members][dim] rows for the exact distances
+  const uint32_t* row_of;     // shard with member_rows: global id -> member slot
   Bounds bd;                  // debug-build index checks
 };
 
@@ -303,15 +289,7 @@ struct FrontArgs {
 hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int nq,
                                int L, int32_t* out_leaf, float* out_dist,
                                float* scores /*[nq][nl] scratch*/, hipStream_t s,
-                               const FrontArgs* front = nullptr,
-                               const SeedArgs* seed = nullptr, const WorklistArgs* wl = nullptr,
-                               bool* fused = nullptr);
-// (With `seed` and `wl`: when the index's top-L runs in one 256-thread block
-// per query (nl <= 2048, L <= 512), the same launch (topl_seed_kernel) also
-// computes each query's seed threshold, writes its pairs' records into the
-// leaf slots (seed->leaf_slots) and, in the block that finishes last, the
-// positions and scan shares of the work list (wl->pos, wl->wave_start,
-// totals); *fused is set and the scan reads those directly.)
+                               const FrontArgs* front = nullptr);
 hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq,
                           int8_t* lut, float* mult, float* inv, uint8_t* lut_u8,
                           hipStream_t s);
@@ -392,6 +370,8 @@ hipError_t SetPhaseStamps(unsigned long long* p);
 // the device since the last call (reset to 0); always 0 in the product build.
 hipError_t TakeCheckFailures(unsigned int* out);
 hipError_t LaunchFill64(uint64_t* p, uint64_t v, size_t n, hipStream_t s);
+// row_of[members[m]] = m for every member slot m (row_of pre-filled).
+hipError_t LaunchRowOf(const uint32_t* members, uint64_t m, uint32_t* row_of, hipStream_t s);
 
 }  // namespace smx
 

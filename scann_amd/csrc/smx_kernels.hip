@@ -1701,155 +1701,6 @@ __global__ void __launch_bounds__(256) pair_scatter_kernel(SeedArgs a, int nq) {
   PairScatter(a, size_t(blockIdx.x) * blockDim.x + threadIdx.x, nq, a.leaf_item0);
 }
 
-// The fused front end's work list, built by the one block of the top-L launch
-// that finishes last (every leaf's pair count is final then): per position in
-// work order its first item and units (the exclusive prefixes of
-// WorklistFusedBlock), the PosDesc the scan derives its items from, the 8 XCD
-// groups' unit boundaries and the totals.  No item, lane record or share
-// start is written: each scan workgroup finds its share's start
-// (ShareStart) and computes its items' (leaf, query tile, chunk) from the
-// positions, and reads their records from the leaf slots.  256 threads, nl <=
-// 2048 (FusedFrontShape).
-constexpr int kPosPerThread = 8;   // BuildPositions: nl <= 2048 (FusedFrontShape)
-
-__device__ void BuildPositions(const WorklistArgs& w) {
-  __shared__ uint32_t wsum[4], s_gunits[kGroups + 1], s_last_un[256];
-  __shared__ unsigned long long red[4][2];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int nl = w.nl, p0 = tid * kPosPerThread;
-  uint32_t leafv[kPosPerThread], cv[kPosPerThread], nv[kPosPerThread];
-#pragma unroll
-  for (int k = 0; k < kPosPerThread; ++k) leafv[k] = p0 + k < nl ? w.order[p0 + k] : 0u;
-#pragma unroll
-  for (int k = 0; k < kPosPerThread; ++k) {
-    cv[k] = nv[k] = 0;
-    if (p0 + k < nl) {
-      // the count as the atomic unit holds it (every block's rank atomics
-      // have returned before it counted itself done)
-      cv[k] = atomicAdd(const_cast<uint32_t*>(&w.cnt[size_t(leafv[k]) * kCounterStride]), 0u);
-      nv[k] = w.leaf_size[leafv[k]];
-    }
-  }
-  uint32_t ti = 0, tu = 0, it, un = 0;
-  unsigned long long tp = 0, tb = 0;
-#pragma unroll
-  for (int k = 0; k < kPosPerThread; ++k) {
-    un = LeafUnits(cv[k], nv[k], w.chunk_tiles, it);
-    tp += cv[k];
-    tb += 16ull * w.nb * ((nv[k] + 31u) / 32u) * cv[k];   // algorithmic code bytes
-    ti += it;
-    tu += un;
-  }
-  s_last_un[tid] = un;
-  const uint32_t inc_i = BlockInclusiveScan256(ti, wsum);
-  __syncthreads();   // wsum is reused
-  const uint32_t inc_u = BlockInclusiveScan256(tu, wsum);
-  const uint32_t total_w = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-  {
-    unsigned long long v[2] = {tp, tb};
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
-      if (lane == 0) red[wid][k] = v[k];
-    }
-  }
-  __syncthreads();   // s_last_un, red
-  if (tid == 255) {
-    w.totals[0] = uint32_t(red[0][0] + red[1][0] + red[2][0] + red[3][0]);
-    w.totals[1] = inc_i;
-    w.totals[2] = total_w;
-    w.code_bytes[0] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
-  }
-  const uint64_t wdiv = max(1u, total_w);
-  auto group_of = [&](uint32_t excl_w) {
-    return int(min<uint64_t>(kGroups - 1, (uint64_t(kGroups) * excl_w) / wdiv));
-  };
-  uint32_t ei = inc_i - ti, eu = inc_u - tu;
-  uint32_t prev_un = tid > 0 ? s_last_un[tid - 1] : 0u;
-#pragma unroll
-  for (int k = 0; k < kPosPerThread; ++k) {
-    const int p = p0 + k;
-    un = LeafUnits(cv[k], nv[k], w.chunk_tiles, it);
-    if (p < nl) {
-      PosDesc d;
-      d.item0 = ei;
-      d.leaf = leafv[k];
-      d.n = nv[k];
-      d.cnt = cv[k];
-      d.tile_off = w.tile_off[leafv[k]];
-      d.member_off = w.member_off[leafv[k]];
-      w.pos[p] = d;
-      w.pos_unit0[p] = eu;
-      const int gp = group_of(eu);
-      const int prev = p > 0 ? group_of(eu - prev_un) : -1;
-      for (int gg = prev + 1; gg <= gp; ++gg) s_gunits[gg] = eu;
-      if (p == nl - 1) {
-        for (int gg = gp + 1; gg <= kGroups; ++gg) s_gunits[gg] = total_w;
-        w.pos_unit0[nl] = total_w;
-      }
-    }
-    ei += it;
-    eu += un;
-    prev_un = un;
-  }
-  __syncthreads();   // s_gunits
-  if (tid <= kGroups) w.gunits[tid] = s_gunits[tid];
-}
-
-// Partition top-L (TopLBlock: the leaves, their ranks in the leaves' lists
-// and the query's LUT) and the query's seed threshold (SeedTau) in one block
-// per query: the seed reads only this query's LUT, leaves and distances,
-// which this block has just written (visible to the block after a barrier).
-// With leaf slots (the fused front end), each pair's record {query, bias,
-// 1/multiplier, sum limit} goes to slot `rank` of its leaf, and the block
-// that finishes last builds the work list's positions (BuildPositions):
-// every block releases its rank atomics (device-scope fence) before counting
-// itself done, and the last one acquires before reading the counts.
-template <int VPT, int K>
-__global__ void __launch_bounds__(256, 4) topl_seed_kernel(const float* __restrict__ scores, int nl,
-                                                        int L, int32_t* __restrict__ out_leaf,
-                                                        float* __restrict__ out_dist,
-                                                        TopLTail tail, SeedArgs sa, WorklistArgs wl) {
-  __shared__ uint32_t s_last;
-  const int qi = int(blockIdx.x);
-  TopLBlock<VPT, 256>(scores, nl, L, out_leaf, out_dist, tail);
-  __syncthreads();
-  const uint64_t T = SeedTau<K>(sa, qi);
-  if (threadIdx.x == 0) sa.tau_key[qi] = T;
-  if (!sa.leaf_slots) return;   // block-uniform
-  {
-    const float inv = sa.inv[qi];
-    const float td = T == kNoThreshold ? 0.0f : FromOrdered(uint32_t(T >> 32));
-    for (int i = threadIdx.x; i < L; i += 256) {
-      const int32_t leaf = out_leaf[size_t(qi) * L + i];
-      if (leaf < 0) continue;
-      const uint32_t r = tail.rank[size_t(qi) * L + i];
-      ItemLane v;
-      v.qid = uint32_t(qi);
-      v.bias = sa.residual ? out_dist[size_t(qi) * L + i] : 0.0f;
-      v.inv = inv;
-      // the slot's sum limit: the largest LUT16 sum whose distance can pass
-      // the query's threshold (PairScatter's)
-      v.amax = T == kNoThreshold ? 128 * sa.nb
-                                 : SumLimit(td, inv, v.bias, -128 * sa.nb, 128 * sa.nb);
-      SMX_CHECK(size_t(leaf) * sa.slot_stride + r, sa.bd.recs, "leaf slot");
-      sa.leaf_slots[size_t(leaf) * sa.slot_stride + r] = v;
-    }
-  }
-  // The last block to finish builds the work list.  It needs only the pair
-  // counts, which every block changed by returning atomics whose results it
-  // has consumed (the ranks) before this barrier, and which the last block
-  // reads back through the atomic unit: no cache write-back or invalidation
-  // (a device-scope fence per block cost ~100 us here).  The records and
-  // positions reach the scan through the kernel boundary.
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(wl.done, 1u) == gridDim.x - 1 ? 1u : 0u;
-  __syncthreads();
-  if (!s_last) return;
-  BuildPositions(wl);
-}
-
-
 // One tile: S[dp][q] for 32 datapoints x 32 queries with the item's B
 // fragments (LUT rows) held in registers, on the 2:4 structured-sparse MFMA
 // (v_smfmac_i32_32x32x64_i8:
@@ -1903,7 +1754,15 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
       }
 #undef SMX_SDWA_OFFS
       o[slot] = *reinterpret_cast<const v4i*>(reinterpret_cast<const char*>(grp_tab) + og);
-      ix[slot] = *reinterpret_cast<const int*>(reinterpret_cast<const char*>(pos_tab) + op);
+      // the index word read as the low half of a ds_read_b64: its bank is
+      // (a/4) mod 64, so the 16 entries 16 bytes apart sit on 16 distinct
+      // bank pairs (a ds_read_b32 banks (a/4) mod 32: entries p and p + 8
+      // collided, 2.97M conflict cycles per launch).  The empty asm takes
+      // the high half as an input so that the load is not narrowed to b32.
+      const uint2 pw = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(pos_tab) + op);
+      int xw;
+      asm("; pos word %1" : "=v"(xw) : "v"(pw.y), "0"(pw.x));
+      ix[slot] = xw;
     }
   };
 #pragma unroll
@@ -2051,116 +1910,14 @@ struct SegDesc {
 // tile, end tile, descriptor) into the LDS table, 64 items per step (a prefix
 // of their tiles), at most kMaxSegs; the share's remainder stays in s_sw /
 // s_su.
-// The fused front end's items come from the positions instead of a list: lane
-// l holds position sp + l's descriptor, item idx = sw + lane lies in the last
-// of those positions whose first item is <= idx (a 6-step search over the
-// lanes), and its (query tile, chunk) follow from the offset inside the
-// position (items are query-tile-major, chunk-minor, as WorklistFusedBlock
-// numbers them).  Items past the 64 positions loaded are left to the next
-// step (`valid` is a prefix of the lanes).
-// The fused front end: workgroup b's share start {item, first tile, units,
-// position}, as WaveStarts assigns it -- group g = b % 8, k = b / 8 of the
-// group's nw, units [U0 + span * k / nw, U0 + span * (k + 1) / nw) -- found
-// by one wave: the position holding the first unit is the last one whose
-// unit prefix is <= it (a 64-ary search over a.pos_unit0 in two rounds of
-// lane loads; nl <= 2048), then its query tile, tile and chunk.
-__device__ uint4 ShareStart(const ScanArgs& a, int lane) {
-  const uint32_t b = blockIdx.x, grid = gridDim.x;
-  const uint32_t g = b & (kGroups - 1), k = b / kGroups;
-  const uint32_t nw = (grid - g + kGroups - 1) / kGroups;
-  const uint32_t U0 = a.gunits[g], span = a.gunits[g + 1] - U0;
-  const uint32_t us = U0 + uint32_t((uint64_t(span) * k) / nw);
-  const uint32_t ue = U0 + uint32_t((uint64_t(span) * (k + 1)) / nw);
-  if (us >= ue) return make_uint4(0, 0, 0, 0);
-  const uint32_t nl = uint32_t(a.nl);
-  // round 1: positions 32 l; round 2: positions 32 L1 + l, l < 32
-  const uint32_t p1 = min(uint32_t(lane) * 32u, nl);
-  const uint64_t b1 = __ballot(p1 < nl && a.pos_unit0[p1] <= us);
-  const uint32_t l1 = 63u - uint32_t(__clzll(b1));   // lane 0 always qualifies
-  const uint32_t p2 = l1 * 32u + uint32_t(lane);
-  const uint64_t b2 = __ballot(lane < 32 && p2 < nl && a.pos_unit0[p2] <= us);
-  const uint32_t p = l1 * 32u + (63u - uint32_t(__clzll(b2)));
-  SMX_CHECK(p, a.bd.nl, "share position");
-  const PosDesc d = a.pos[p];
-  const uint32_t tiles = (d.n + 31u) / 32u;
-  const uint32_t off = us - a.pos_unit0[p], tq = off / tiles, rem = off % tiles;
-  const uint32_t chunks = LeafChunks(d.n, a.chunk_tiles);
-  uint32_t ch = 0;
-  while (ChunkTiles(d.n, a.chunk_tiles, ch).y <= rem) ++ch;
-  return make_uint4(d.item0 + tq * chunks + ch, rem, ue - us, p);
-}
-
-struct PosItem {
-  WorkItem it;
-  uint32_t slot0, nslots, pos;
-  bool valid;
-};
-
-__device__ __forceinline__ PosItem ItemFromPositions(const ScanArgs& a, int lane, uint32_t sp,
-                                                     uint32_t idx) {
-  PosDesc d;
-  const uint32_t p = sp + uint32_t(lane);
-  if (p < uint32_t(a.nl)) {
-    d = a.pos[p];
-  } else {
-    d.item0 = ~0u;   // never <= an item index
-    d.leaf = d.n = d.cnt = 0;
-    d.tile_off = d.member_off = 0;
-  }
-  const uint32_t chunks_l = LeafChunks(d.n, a.chunk_tiles);
-  const uint32_t qt_l = (d.cnt + kQueriesPerTile - 1) / kQueriesPerTile;
-  const uint32_t end_l = d.item0 == ~0u ? ~0u : d.item0 + qt_l * chunks_l;
-  int q = 0;
-#pragma unroll
-  for (int st = 32; st > 0; st >>= 1) {
-    const uint32_t v = uint32_t(__shfl(int(d.item0), q + st));
-    if (v <= idx) q += st;
-  }
-  PosItem r;
-  const uint32_t item0 = uint32_t(__shfl(int(d.item0), q));
-  const uint32_t end = uint32_t(__shfl(int(end_l), q));
-  r.valid = idx >= item0 && idx < end;
-  r.pos = sp + uint32_t(q);
-  r.it.leaf = uint32_t(__shfl(int(d.leaf), q));
-  r.it.n = uint32_t(__shfl(int(d.n), q));
-  const uint32_t cnt = uint32_t(__shfl(int(d.cnt), q));
-  r.it.tile_off = (uint64_t(uint32_t(__shfl(int(uint32_t(d.tile_off >> 32)), q))) << 32) |
-                  uint32_t(__shfl(int(uint32_t(d.tile_off)), q));
-  r.it.member_off = (uint64_t(uint32_t(__shfl(int(uint32_t(d.member_off >> 32)), q))) << 32) |
-                    uint32_t(__shfl(int(uint32_t(d.member_off)), q));
-  const uint32_t chunks = max(1u, LeafChunks(r.it.n, a.chunk_tiles));
-  const uint32_t u = r.valid ? idx - item0 : 0u;
-  const uint32_t tq = u / chunks;
-  const uint2 cr = ChunkTiles(r.it.n, a.chunk_tiles, u - tq * chunks);
-  r.it.j0 = cr.x;
-  r.it.jend = r.valid ? cr.y : 0u;
-  r.slot0 = r.it.leaf * a.slot_stride + tq * kQueriesPerTile;
-  r.nslots = min(uint32_t(kQueriesPerTile), cnt - min(cnt, tq * kQueriesPerTile));
-  return r;
-}
-
 __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32_t& sj,
                                              uint32_t* s_item, uint32_t* s_end, uint32_t* s_next,
                                              SegDesc* s_desc, uint32_t& s_sw, uint32_t& s_su,
-                                             uint32_t& s_sp, uint32_t& s_nseg, uint32_t& s_claim) {
-  uint32_t sw = s_sw, su = s_su, sp = s_sp, nseg = 0;
+                                             uint32_t& s_nseg, uint32_t& s_claim) {
+  uint32_t sw = s_sw, su = s_su, nseg = 0;
   while (su > 0 && nseg + 64 <= uint32_t(kMaxSegs)) {
     const uint32_t idx = sw + uint32_t(lane);
-    WorkItem it;
-    uint32_t slot0, nslots, ipos = 0;
-    bool valid = true;
-    if (a.pos) {   // (uniform)
-      const PosItem pi = ItemFromPositions(a, lane, sp, idx);
-      it = pi.it;
-      slot0 = pi.slot0;
-      nslots = pi.nslots;
-      valid = pi.valid;
-      ipos = pi.pos;
-    } else {
-      it = a.work[min(idx, a.num_items - 1)];
-      slot0 = idx * uint32_t(kQueriesPerTile);
-      nslots = kQueriesPerTile;
-    }
+    const WorkItem it = a.work[min(idx, a.num_items - 1)];
     const uint32_t j0 = (lane == 0 && sj) ? sj : it.j0;
     const uint32_t t = it.jend > j0 ? min(it.jend - j0, su) : 0u;
     uint32_t incl = t;
@@ -2169,7 +1926,7 @@ __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32
       if (lane >= off) incl += y;
     }
     const uint32_t excl = incl - t;
-    const bool used = valid && excl < su;   // a prefix of the lanes
+    const bool used = excl < su;   // a prefix of the lanes, lane 0 always
     const bool take = used && t > 0;
     if (take) SMX_CHECK(idx, a.bd.items, "listed item");
     const uint64_t bt = __ballot(take);
@@ -2183,14 +1940,12 @@ __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32
       dsc.member_off = it.member_off;
       dsc.n = it.n;
       dsc.leaf = it.leaf;
-      dsc.slot0 = slot0;
-      dsc.nslots = nslots;
+      dsc.slot0 = idx * uint32_t(kQueriesPerTile);
+      dsc.nslots = kQueriesPerTile;
       s_desc[pos] = dsc;
     }
     const uint32_t nused = uint32_t(__popcll(__ballot(used)));
-    if (nused == 0) break;   // (cannot happen: lane 0's item is in position sp)
     const uint32_t last_incl = uint32_t(__shfl(int(incl), int(nused) - 1));
-    sp = uint32_t(__shfl(int(ipos), int(nused) - 1));   // the next item is there or later
     sw += nused;
     su -= min(su, last_incl);
     nseg += uint32_t(__popcll(bt));
@@ -2199,7 +1954,6 @@ __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32
   if (lane == 0) {
     s_sw = sw;
     s_su = su;
-    s_sp = sp;
     s_nseg = nseg;
     s_claim = 0;
   }
@@ -2221,7 +1975,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   int* const pos_tab = reinterpret_cast<int*>(opnd_tab + 16);
   __shared__ uint32_t s_item[kMaxSegs], s_end[kMaxSegs], s_next[kMaxSegs];
   __shared__ SegDesc s_desc[kMaxSegs];
-  __shared__ uint32_t s_nseg, s_claim, s_sw, s_su, s_sp;
+  __shared__ uint32_t s_nseg, s_claim, s_sw, s_su;
   // wave-uniform values in scalar registers (the B fragments need the VGPRs)
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -2240,12 +1994,10 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   const uint32_t worker = blockIdx.x * NWAVES + wv;
   // this workgroup's share: `units` tiles from tile jfirst of item w on
   // (wave 0 lists the segments; only its copy is used)
-  const uint4 ws = wv != 0 ? make_uint4(0, 0, 0, 0)
-                   : a.pos ? ShareStart(a, lane) : a.wave_start[blockIdx.x];
+  const uint4 ws = wv != 0 ? make_uint4(0, 0, 0, 0) : a.wave_start[blockIdx.x];
   if (threadIdx.x == 0) {
     s_sw = ws.x;
     s_su = ws.z;
-    s_sp = ws.w;   // (fused front end) the position of item ws.x
   }
   uint32_t sj = ws.y;   // the share's first tile inside its first item
   bool pending = false;   // the previous segment's survivors await their copy
@@ -2300,8 +2052,8 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
 
   for (;;) {   // rounds of at most kMaxSegs segments (block-uniform)
     __syncthreads();   // s_sw / s_su / the segment table are free
-    if (wv == 0) ListSegments(a, lane, sj, s_item, s_end, s_next, s_desc, s_sw, s_su, s_sp,
-                                 s_nseg, s_claim);
+    if (wv == 0) ListSegments(a, lane, sj, s_item, s_end, s_next, s_desc, s_sw, s_su, s_nseg,
+                                 s_claim);
     __syncthreads();
     const uint32_t nseg = s_nseg;
     if (nseg == 0) break;
@@ -2834,6 +2586,17 @@ __global__ void __launch_bounds__(256) partition_scores_a8_kernel(
 // (distance, id) sort of SortAndDropResults.
 // LDS: keys[cap_pow2] u64 | q[dim] f32 | gid/dist scratch.
 // ---------------------------------------------------------------------------
+// The float row of a candidate known by its global id: the shard's own copy
+// (member_rows[row_of[gid]]) or the dataset's row.
+__device__ __forceinline__ const float* RowOfId(const SelectArgs& a, uint32_t gid) {
+  if (a.member_rows) {
+    const uint32_t slot = a.row_of[gid];
+    SMX_CHECK(slot, a.bd.members, "row_of slot");
+    return a.member_rows + uint64_t(slot) * uint64_t(a.dim);
+  }
+  return a.dataset + uint64_t(gid) * uint64_t(a.dim);
+}
+
 __device__ void FinalSelectQuery(const SelectArgs& a, int qi) {
   extern __shared__ uint64_t lds[];
   uint32_t raw_n = a.cand_count[size_t(qi) * kCounterStride];
@@ -2888,7 +2651,7 @@ __device__ void FinalSelectQuery(const SelectArgs& a, int qi) {
       e.exact = 0.0f;
       if (i < m) {
         uint64_t key = keys[i];
-        const float* x = a.dataset ? a.dataset + size_t(gid[i]) * a.dim : nullptr;
+        const float* x = a.reorder ? RowOfId(a, gid[i]) : nullptr;
         if (a.shift > 0) {
           const uint32_t tie = uint32_t(key & 0xFFFFFFFFu);
           const uint32_t leaf = tie >> a.shift;
@@ -2949,7 +2712,7 @@ __device__ void FinalSelectQuery(const SelectArgs& a, int qi) {
   }
   if (a.reorder && !a.pre_only) {
     for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
-      dist[i] = ExactDistance(q, a.dataset + size_t(gid[i]) * a.dim, a.dim, a.metric);
+      dist[i] = ExactDistance(q, RowOfId(a, gid[i]), a.dim, a.metric);
     __syncthreads();
   }
   // Sort by (distance, global id) and keep the output width.
@@ -3202,6 +2965,8 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
       if (a.shard_out && a.row_base)   // whole-index tie for the merge
         out[tid] = (key & 0xFFFFFFFF00000000ull) |
                    ((leaf << a.shift) | (local + a.row_base[leaf]));
+    } else if (a.member_rows) {   // ties by global id (no global top-N): its slot
+      rid = a.row_of[tie];
     }
     SMX_CHECK(rid, a.member_rows ? a.bd.members : uint64_t(a.bd.datapoints), "select row");
     gid[tid] = tie;
@@ -3462,6 +3227,12 @@ __global__ void exact_distances_kernel(const float* __restrict__ queries, const 
   }
 }
 
+__global__ void row_of_kernel(const uint32_t* __restrict__ members, uint64_t m,
+                              uint32_t* __restrict__ row_of) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < m) row_of[members[i]] = uint32_t(i);
+}
+
 __global__ void fill64_kernel(uint64_t* p, uint64_t v, size_t n) {
   const size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
@@ -3474,9 +3245,7 @@ __global__ void fill64_kernel(uint64_t* p, uint64_t v, size_t n) {
 // ---------------------------------------------------------------------------
 hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int nq, int L,
                                int32_t* out_leaf, float* out_dist, float* scores, hipStream_t s,
-                               const FrontArgs* front, const SeedArgs* seed,
-                               const WorklistArgs* wl, bool* fused) {
-  if (fused) *fused = false;
+                               const FrontArgs* front) {
   if (nq == 0) return hipSuccess;
   uint32_t kcap = 1;
   while (kcap < uint32_t(ix.nl)) kcap <<= 1;
@@ -3505,33 +3274,7 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   // static LDS of the kernel besides the dynamic key buffers: the LUT build's
   // raw table and reduction (~5 KB) and the selection's words
   constexpr size_t kStaticLds = 6 * 1024;
-  if (seed && wl && fused && seed->leaf_slots && wl->pos && L <= kWaveTopL && ix.nl <= 256 * 8) {
-    const bool v4 = ix.nl <= 256 * 4;
-#define SMX_TOPL_SEED_CASE(KV)                                                               \
-  case KV:                                                                                   \
-    if (v4)                                                                                  \
-      hipLaunchKernelGGL((topl_seed_kernel<4, KV>), dim3(nq), dim3(256), 0, s, scores, ix.nl, \
-                         L, out_leaf, out_dist, tail, *seed, *wl);                            \
-    else                                                                                     \
-      hipLaunchKernelGGL((topl_seed_kernel<8, KV>), dim3(nq), dim3(256), 0, s, scores, ix.nl, \
-                         L, out_leaf, out_dist, tail, *seed, *wl);                            \
-    break;
-    switch (ix.ksteps) {
-      SMX_TOPL_SEED_CASE(4)
-      SMX_TOPL_SEED_CASE(8)
-      SMX_TOPL_SEED_CASE(12)
-      SMX_TOPL_SEED_CASE(16)
-      SMX_TOPL_SEED_CASE(20)
-      SMX_TOPL_SEED_CASE(24)
-      SMX_TOPL_SEED_CASE(26)
-      SMX_TOPL_SEED_CASE(28)
-      SMX_TOPL_SEED_CASE(32)
-      default:
-        return hipErrorInvalidValue;
-    }
-#undef SMX_TOPL_SEED_CASE
-    *fused = true;
-  } else if (L <= kWaveTopL && ix.nl <= 256 * 4) {
+  if (L <= kWaveTopL && ix.nl <= 256 * 4) {
     hipLaunchKernelGGL((topl_block_kernel<4, 256>), dim3(nq), dim3(256), 0, s, scores, ix.nl, L,
                        out_leaf, out_dist, tail);
   } else if (L <= kWaveTopL && ix.nl <= 256 * 8) {
@@ -3600,8 +3343,6 @@ WorklistArgs MakeWorklistArgs(const DeviceIndex& ix, const uint32_t* leaf_count,
   w.work = work;
   w.lanes = lanes;
   w.wave_start = wave_start;
-  w.pos = nullptr;
-  w.done = nullptr;
   return w;
 }
 
@@ -3852,6 +3593,13 @@ hipError_t TakeCheckFailures(unsigned int* out) {
   *out = 0;
   return hipSuccess;
 #endif
+}
+
+hipError_t LaunchRowOf(const uint32_t* members, uint64_t m, uint32_t* row_of, hipStream_t s) {
+  if (m == 0) return hipSuccess;
+  hipLaunchKernelGGL(row_of_kernel, dim3(unsigned((m + 255) / 256)), dim3(256), 0, s, members, m,
+                     row_of);
+  return hipGetLastError();
 }
 
 hipError_t LaunchFill64(uint64_t* p, uint64_t v, size_t n, hipStream_t s) {

@@ -86,9 +86,14 @@ struct CounterLayout {
 };
 
 struct Workspace {
-  int nq = 0, L = 0, kk = 0, dim = 0, width = 0;
+  // allocated sizes, each the largest of its own quantity over past calls
+  // (never a product of per-dimension maxima: nq = 10^4 at L = 20 followed
+  // by nq = 10 at L = 2000 keeps 2 * 10^5 pairs, not 2 * 10^7)
+  int nq = 0, dim = 0;
+  size_t pairs = 0, cand_words = 0, out_words = 0;
   uint64_t gen = 0;                 // bumped on every (re)allocation
-  uint32_t cap = 0, max_items = 0;
+  uint32_t max_items = 0;
+  uint32_t cap = 0;                 // this call's list capacity = its [nq][cap] stride
   float* queries = nullptr;
   int32_t* topl_leaf = nullptr;
   float* topl_dist = nullptr;
@@ -103,9 +108,6 @@ struct Workspace {
   smx::ItemLane* lanes = nullptr;   // [max_items][32]
   uint4* wave_start = nullptr;      // [grid] each scan wave's static share
   uint32_t* pos_unit0 = nullptr;    // [nl+1] work units before each leaf (work order)
-  smx::PosDesc* pos = nullptr;      // [nl] fused front end: the work order's positions
-  smx::ItemLane* leaf_slots = nullptr;   // fused front end: [nl][slot_stride] pair records
-  uint32_t slot_stride = 0;         // nq rounded up to 32 (0: no leaf slots)
   uint32_t* gunits = nullptr;       // [16] the XCD groups' unit boundaries
   unsigned long long* wl_part = nullptr;   // [4 * ceil(nl / 256)] work-list block sums
   uint64_t* tau = nullptr;          // [nq]
@@ -119,12 +121,12 @@ struct Workspace {
     DFree(queries); DFree(topl_leaf); DFree(topl_dist); DFree(scores); DFree(lut); DFree(mult);
     DFree(inv);
     DFree(counters); DFree(rank); DFree(leaf_item0); DFree(lanes); DFree(wave_start);
-    DFree(pos_unit0); DFree(gunits); DFree(wl_part); DFree(pos); DFree(leaf_slots);
-    slot_stride = 0;
+    DFree(pos_unit0); DFree(gunits); DFree(wl_part);
     DFree(work); DFree(tau); DFree(cand); DFree(cand_count); DFree(out_idx);
     DFree(out_dist);
     DFree(out_count);
-    nq = L = kk = dim = width = 0;
+    nq = dim = 0;
+    pairs = cand_words = out_words = 0;
     cap = max_items = 0;
   }
 };
@@ -141,13 +143,6 @@ struct smx_index {
   int seed_leaves = 4;
   int scan_variant = 0;            // see smx::LaunchScan
   int fused_worklist_leaves = smx::kFusedWorklistLeaves;   // 0: always the side stream
-  // SMX_FUSED_FRONT=1: the top-L launch also computes the seed thresholds, the
-  // pairs' leaf-slot records and the work list's positions (four launches a
-  // call instead of six); measured 2% slower than the separate launches at
-  // glove shape (the seed blocks' LDS pair-table lookups, not the launches,
-  // bound the front end), so off by default
-  bool fused_front = false;
-  bool front_fused_last = false;   // the last call ran the fused front end (timings)
   uint32_t chunk_tiles = 20;       // tiles per work item (tools/tune.py: 16-20 best at glove)
   int grid = 0;                    // scan grid: resident one-wave workgroups (occupancy API)
   bool profiling = false;
@@ -224,8 +219,6 @@ int UploadIndex(const smx_index_desc* d, smx_index* h) {
     for (int l = 0; l < nl; ++l)
       if (ix.shift > 0 && uint64_t(d->leaf_row_base[l]) + size[l] > (1ull << ix.shift))
         return Fail(SMX_INVALID_ARGUMENT, "shard rows exceed the whole index's leaf range");
-    if (d->member_rows && ix.shift == 0)
-      return Fail(SMX_INVALID_ARGUMENT, "member_rows needs a global top-N (residual) index");
   }
 
   // Code tiles: lane l = h*32 + r of tile j of a leaf holds, as nibbles
@@ -278,6 +271,11 @@ int UploadIndex(const smx_index_desc* d, smx_index* h) {
       if ((rc = DAlloc(&ix.member_rows, size_t(M) * dim))) return rc;
       SMX_HIP(hipMemcpy(ix.member_rows, d->member_rows, sizeof(float) * size_t(M) * dim,
                         hipMemcpyHostToDevice));
+      // global id -> member slot, for the candidates known by global id (the
+      // non-global-top-N fallback: ties are global ids, shift 0; and the
+      // block select).  A SOAR id held twice keeps either slot: same row.
+      if ((rc = DAlloc(&ix.row_of, size_t(d->num_datapoints)))) return rc;
+      SMX_HIP(hipMemset(ix.row_of, 0xFF, sizeof(uint32_t) * size_t(d->num_datapoints)));
     }
   }
   SMX_HIP(hipMemcpy(ix.centers, d->centers, sizeof(float) * nl * dim, hipMemcpyHostToDevice));
@@ -290,6 +288,10 @@ int UploadIndex(const smx_index_desc* d, smx_index* h) {
   SMX_HIP(hipMemcpy(ix.leaf_size, size.data(), 4 * nl, hipMemcpyHostToDevice));
   SMX_HIP(hipMemcpy(ix.member_off, d->leaf_offsets, 8 * (nl + 1), hipMemcpyHostToDevice));
   if (M) SMX_HIP(hipMemcpy(ix.members, d->leaf_members, 4 * M, hipMemcpyHostToDevice));
+  if (ix.row_of) {
+    SMX_HIP(smx::LaunchRowOf(ix.members, M, ix.row_of, nullptr));
+    SMX_HIP(hipDeviceSynchronize());
+  }
   // Work order: the leaves by descending size dealt to the 8 XCD groups in a
   // snake (0..7, 7..0, ...), each group's leaves contiguous and largest
   // first.  The worklist cuts the order into 8 groups of equal MFMA work, so
@@ -318,7 +320,7 @@ void FreeIndex(smx::DeviceIndex& ix) {
   DFree(ix.centers); DFree(ix.centers_t); DFree(ix.cnorm); DFree(ix.codebook);
   DFree(ix.tiles); DFree(ix.tile_off); DFree(ix.leaf_size); DFree(ix.member_off);
   DFree(ix.members); DFree(ix.leaf_order); DFree(ix.dataset); DFree(ix.row_base);
-  DFree(ix.member_rows);
+  DFree(ix.member_rows); DFree(ix.row_of);
 }
 
 int ValidateDesc(const smx_index_desc* d) {
@@ -366,71 +368,67 @@ uint32_t AutoCap(int L, int kk, int seed) {
   return cap;
 }
 
-uint32_t RoundUp32(int n) { return (uint32_t(n) + 31u) & ~31u; }
-
-// The index shapes the fused front end takes (one 256-thread top-L block per
-// query, the work list's positions built by one block): nl <= 2048, L <= 512.
-bool FusedFrontShape(const smx::DeviceIndex& ix, int L) { return ix.nl <= 2048 && L <= 512; }
+// Work items the workspace holds for `pairs` (query, leaf) pairs: one per
+// (leaf, 32-query tile, chunk of >= 8 tiles).
+uint32_t MaxItems(const smx::DeviceIndex& ix, size_t pairs) {
+  const uint32_t chunks = (uint32_t((ix.max_leaf + 31) / 32) + 7) / 8 + 1;  // chunk >= 8
+  return uint32_t((pairs / smx::kQueriesPerTile + ix.nl + 1) * chunks);
+}
 
 int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
   Workspace& w = h->ws;
   const smx::DeviceIndex& ix = h->ix;
   // cap >= 2 k': when a list overflows, its k'-th stored key is strictly
   // below the threshold (keys are unique and all <= it), so every
-  // tightening pass drops at least cap - k' keys
+  // tightening pass drops at least cap - k' keys.  The lists of a call are
+  // [nq][cap] with this call's own cap (the kernels' stride), inside a
+  // buffer that may be larger.
   const uint32_t base = h->cap_per_query ? h->cap_per_query
                                          : AutoCap(L, kk, std::min(h->seed_leaves, L));
-  uint32_t cap = std::max<uint32_t>(base, 2u * uint32_t(kk));
-  // a larger list than this call needs is reused as it is (w.cap is the
-  // stride every kernel uses): varying leaves_to_search never frees and
-  // reallocates the workspace (hipFree synchronises the device) unless it
-  // has to grow, and then it grows to cover both shapes
-  // (an explicit capacity, smx_set_tuning, is used exactly)
-  const bool cap_ok = h->cap_per_query ? cap == w.cap : cap <= w.cap;
-  if (nq <= w.nq && L <= w.L && kk <= w.kk && width <= w.width && cap_ok && ix.dim == w.dim)
+  const uint32_t cap = std::max<uint32_t>(base, 2u * uint32_t(kk));
+  const size_t pairs = size_t(nq) * L;
+  const size_t cand_words = size_t(nq) * cap, out_words = size_t(nq) * width;
+  if (nq <= w.nq && pairs <= w.pairs && cand_words <= w.cand_words && out_words <= w.out_words &&
+      ix.dim == w.dim) {
+    w.cap = cap;
     return SMX_OK;
-  if (w.nq) {
-    nq = std::max(nq, w.nq);
-    L = std::max(L, w.L);
-    kk = std::max(kk, w.kk);
-    width = std::max(width, w.width);
-    if (!h->cap_per_query) cap = std::max(cap, w.cap);
   }
+  // grow each quantity to cover this call and the earlier ones, so that
+  // alternating shapes (leaves_to_search sweeps) settle after one growth
+  // (hipFree synchronises the device)
+  const int anq = std::max(nq, w.nq);
+  const size_t apairs = std::max(pairs, w.pairs);
+  const size_t acand = std::max(cand_words, w.cand_words);
+  const size_t aout = std::max(out_words, w.out_words);
   w.Release();
   const int nl = ix.nl;
-  const size_t pairs = size_t(nq) * L;
-  const uint32_t chunks = (uint32_t((ix.max_leaf + 31) / 32) + 7) / 8 + 1;  // chunk >= 8
-  const uint32_t max_items = uint32_t((pairs / smx::kQueriesPerTile + nl + 1) * chunks);
+  const uint32_t max_items = MaxItems(ix, apairs);
   int rc;
-  if ((rc = DAlloc(&w.queries, size_t(nq) * ix.dim)) || (rc = DAlloc(&w.topl_leaf, pairs)) ||
-      (rc = DAlloc(&w.topl_dist, pairs)) || (rc = DAlloc(&w.scores, size_t(nq) * nl)) ||
-      (rc = DAlloc(&w.lut, size_t(nq) * 2 * ix.ksteps * 16)) || (rc = DAlloc(&w.mult, nq)) ||
-      (rc = DAlloc(&w.inv, nq)) || (rc = DAlloc(&w.counters, CounterLayout(nl).words)) ||
-      (rc = DAlloc(&w.rank, pairs)) || (rc = DAlloc(&w.leaf_item0, size_t(nl))) ||
+  if ((rc = DAlloc(&w.queries, size_t(anq) * ix.dim)) || (rc = DAlloc(&w.topl_leaf, apairs)) ||
+      (rc = DAlloc(&w.topl_dist, apairs)) || (rc = DAlloc(&w.scores, size_t(anq) * nl)) ||
+      (rc = DAlloc(&w.lut, size_t(anq) * 2 * ix.ksteps * 16)) || (rc = DAlloc(&w.mult, anq)) ||
+      (rc = DAlloc(&w.inv, anq)) || (rc = DAlloc(&w.counters, CounterLayout(nl).words)) ||
+      (rc = DAlloc(&w.rank, apairs)) || (rc = DAlloc(&w.leaf_item0, size_t(nl))) ||
       (rc = DAlloc(&w.lanes, size_t(max_items) * smx::kQueriesPerTile)) ||
       (rc = DAlloc(&w.wave_start, size_t(std::max(h->grid, 1)))) ||
       (rc = DAlloc(&w.pos_unit0, size_t(nl + 1))) || (rc = DAlloc(&w.gunits, 16)) ||
       (rc = DAlloc(&w.wl_part, size_t(4) * ((nl + 255) / 256))) ||
-      (rc = DAlloc(&w.work, max_items)) || (rc = DAlloc(&w.tau, nq)) ||
-      (rc = DAlloc(&w.cand, size_t(nq) * cap)) || (rc = DAlloc(&w.cand_count, size_t(nq) * smx::kCounterStride)) ||
-      (rc = DAlloc(&w.out_idx, size_t(nq) * width)) ||
-      (rc = DAlloc(&w.out_dist, size_t(nq) * width)) || (rc = DAlloc(&w.out_count, nq))) {
+      (rc = DAlloc(&w.work, max_items)) || (rc = DAlloc(&w.tau, anq)) ||
+      (rc = DAlloc(&w.cand, acand)) ||
+      (rc = DAlloc(&w.cand_count, size_t(anq) * smx::kCounterStride)) ||
+      (rc = DAlloc(&w.out_idx, aout)) || (rc = DAlloc(&w.out_dist, aout)) ||
+      (rc = DAlloc(&w.out_count, anq))) {
     w.Release();
     return rc;
   }
-  // leaf slots of the fused front end (smx::LaunchPartitionTopL): one record
-  // per possible (leaf, query) pair, at most 1 GiB
-  if (FusedFrontShape(ix, L) && uint64_t(nl) * RoundUp32(nq) * sizeof(smx::ItemLane) <= (1ull << 30)) {
-    if ((rc = DAlloc(&w.pos, size_t(nl))) ||
-        (rc = DAlloc(&w.leaf_slots, size_t(nl) * RoundUp32(nq)))) {
-      w.Release();
-      return rc;
-    }
-    w.slot_stride = RoundUp32(nq);
-  }
-  w.nq = nq; w.L = L; w.kk = kk; w.width = width; w.dim = ix.dim;
+  w.nq = anq;
+  w.pairs = apairs;
+  w.cand_words = acand;
+  w.out_words = aout;
+  w.dim = ix.dim;
   w.gen = ++h->ws_generation;
-  w.cap = cap; w.max_items = max_items;
+  w.cap = cap;
+  w.max_items = max_items;
   return SMX_OK;
 }
 
@@ -484,11 +482,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   bd.datapoints = ix.num_datapoints;
   bd.members = ix.num_members;
   bd.tiles = ix.num_tiles;
-  // the fused front end (top-L + seed + pair records + work-list positions in
-  // one launch; the scan derives its items from the positions)
-  const bool fuse = h->fused_front && w.slot_stride >= uint32_t(nq) && w.leaf_slots &&
-                    FusedFrontShape(ix, L);
-  bd.recs = fuse ? uint32_t(nl) * w.slot_stride : w.max_items * uint32_t(smx::kQueriesPerTile);
+  bd.recs = w.max_items * uint32_t(smx::kQueriesPerTile);
   smx::SeedArgs sa{};
   sa.bd = bd;
   sa.topl_leaf = w.topl_leaf;
@@ -508,8 +502,6 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sa.seed = seed;
   sa.kk = kk;
   sa.residual = ix.residual;
-  sa.leaf_slots = fuse ? w.leaf_slots : nullptr;
-  sa.slot_stride = w.slot_stride;
 
   smx::ScanArgs a{};
   a.bd = bd;
@@ -518,11 +510,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   a.lut = w.lut;
   a.inv = w.inv;
   a.work = w.work;
-  a.lanes = fuse ? w.leaf_slots : w.lanes;
-  a.pos = fuse ? w.pos : nullptr;
-  a.pos_unit0 = w.pos_unit0;
-  a.gunits = w.gunits;
-  a.slot_stride = w.slot_stride;
+  a.lanes = w.lanes;
   a.chunk_tiles = h->chunk_tiles;
   a.wave_start = w.wave_start;
   a.num_items = w.max_items;   // bound of the one-ahead descriptor prefetch
@@ -592,6 +580,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sel.shard_out = shard_out;
   sel.row_base = ix.row_base;
   sel.member_rows = ix.member_rows;
+  sel.row_of = ix.row_of;
   if (!smx::FinalSelectFits(sel))
     return Fail(SMX_INVALID_ARGUMENT,
                 "the candidate list capacity, k' and dim exceed the final selection's 160 KiB of "
@@ -618,29 +607,8 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     f.mult = w.mult;
     f.inv = w.inv;
     f.one_to_many = single ? 1 : 0;
-    // Fused front end: the seed thresholds, the pairs' slot records and the
-    // work list's positions in the top-L launch -- four launches in all
-    smx::WorklistArgs fwl = smx::MakeWorklistArgs(
-        ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes, w.wave_start, h->grid,
-        stats + 3, code_bytes, h->chunk_tiles, bd);
-    fwl.pos = w.pos;
-    fwl.done = stats + 16;   // zeroed by the state reset above
-    bool fused = false;
-    SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s, &f,
-                                     fuse ? &sa : nullptr, fuse ? &fwl : nullptr,
-                                     fuse ? &fused : nullptr));
+    SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s, &f));
     Mark(h, 1, s);
-    h->front_fused_last = fused;
-    if (fuse && !fused)
-      return Fail(SMX_INTERNAL, "fused front end not taken for a shape that selected it");
-    if (fused) {
-      Mark(h, 5, s);
-      SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s));
-      Mark(h, 6, s);
-      SMX_HIP(smx::LaunchFinalSelect(sel, nq, s));
-      Mark(h, 7, s);
-      return SMX_OK;
-    }
     if (ix.nl <= h->fused_worklist_leaves) {
       // the work list is built by extra blocks of the seed launch (one
       // stream: a fork/join costs 5-10 us per cross-queue edge)
@@ -801,15 +769,8 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     // stream) and the seed overlap, each timed from the fork
     t.partition_ms = Elapsed(h, 0, 1);
     t.lut_ms = 0.0f;
-    if (h->front_fused_last) {
-      // the seed, the pair records and the work list ran inside the top-L
-      // launch (partition_ms)
-      t.invert_ms = Elapsed(h, 1, 5);
-      t.seed_scan_ms = 0.0f;
-    } else {
-      t.invert_ms = Elapsed(h, 1, 3);
-      t.seed_scan_ms = Elapsed(h, 1, 4);
-    }
+    t.invert_ms = Elapsed(h, 1, 3);
+    t.seed_scan_ms = Elapsed(h, 1, 4);
     t.seed_select_ms = 0.0f;
     t.scan_ms = Elapsed(h, 5, 6);
     t.select_ms = Elapsed(h, 6, 7);
@@ -914,7 +875,6 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
   }
   if (const char* fw = std::getenv("SMX_FUSED_WORKLIST"))
     h->fused_worklist_leaves = std::min(std::atoi(fw), smx::kFusedWorklistLeaves);
-  if (const char* ff = std::getenv("SMX_FUSED_FRONT")) h->fused_front = ff[0] != '0';
   const char* ng = std::getenv("SMX_NO_GRAPH");
   // Eager launches by default: six kernels a call queue back to back on the
   // stream, while consecutive replays of a captured graph left ~13 us

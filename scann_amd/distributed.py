@@ -40,9 +40,13 @@ def all_gather_entries(local: torch.Tensor, world: int, group=None) -> torch.Ten
         return out
     if dist.get_backend(group) == "nccl":
         dist.all_gather_into_tensor(out, local.contiguous(), group=group)
-    else:   # gloo (CPU tests): list form
+    elif local.device.type == "cpu":   # gloo (CPU tests): list form
         parts = list(out.unbind(0))
         dist.all_gather(parts, local.contiguous(), group=group)
+    else:   # gloo with device tensors (multi-process tests on one GPU): via host memory
+        host = torch.empty((world,) + tuple(local.shape), dtype=local.dtype)
+        dist.all_gather(list(host.unbind(0)), local.cpu(), group=group)
+        out.copy_(host)
     return out
 
 

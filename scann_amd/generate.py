@@ -235,29 +235,14 @@ def build_generated_shard(ds: GeneratedDataset, num_leaves: int, rank: int = 0, 
                            codebook=codebook, leaf_offsets=offsets, leaf_members=members,
                            member_codes=codes, num_datapoints=ds.n, dataset=dataset,
                            spilling_overretrieve_factor=float(overretrieve_factor))
-    if shift == 0 and ds.n * dim * 4 > (16 << 30):
-        # without the global top-N path ties are global ids and the reorder
-        # reads rows by global id: every rank would need the whole dataset
-        raise ValueError(
-            f"generated shard: a leaf exceeds {1 << inner} members (the global top-N limit "
-            f"for {L} leaves), so the shard would need the whole {ds.n}-row dataset; use "
-            f"more leaves or a more uniform mixture")
+    # shift 0 (a leaf above the global top-N limit, the reference's fallback
+    # to global-id ties): the shard still reorders from its own rows (the
+    # device maps a candidate's global id to its member slot)
     return TreeAHIndex(metric=metric, dim=dim, num_blocks=num_blocks,
                        dims_per_block=dims_per_block, residual=residual, centers=centers,
                        codebook=codebook, leaf_offsets=offsets, leaf_members=members,
                        member_codes=codes, num_datapoints=ds.n,
-                       dataset=None if shift > 0 else _rows_by_id(ds, dim),
                        spilling_overretrieve_factor=float(overretrieve_factor),
                        leaf_row_base=before.cpu().numpy().astype(np.uint32),
                        global_topn_shift=shift, global_spilled=spilled,
-                       member_rows=member_rows if shift > 0 else None)
-
-
-def _rows_by_id(ds: GeneratedDataset, dim: int) -> np.ndarray:
-    """The whole dataset on the host (shards without the global top-N path
-    reorder by global id; small configurations only)."""
-    out = np.empty((ds.n, dim), np.float32)
-    for ch in range(ds.num_chunks):
-        x = ds.chunk(ch)
-        out[ch * CHUNK:ch * CHUNK + x.shape[0]] = x.cpu().numpy()
-    return out
+                       member_rows=member_rows)

@@ -124,8 +124,11 @@ class TreeAHIndex:
         """Rank `rank` of a `world`-way range split: rows [n*r/W, n*(r+1)/W) of
         every leaf (balanced whatever the query popularity).
         Ties stay the whole index's (leaf << shift | row) through
-        leaf_row_base.  With own_rows (global top-N indexes) the shard carries
-        only its members' float rows for the reorder instead of the dataset."""
+        leaf_row_base (or are global ids when a leaf exceeds the global top-N
+        limit: shift 0, the reference's fallback, tree_ah_hybrid_residual.h:
+        234-247).  With own_rows the shard carries only its members' float
+        rows for the reorder instead of the dataset (the device finds a
+        candidate's row from its tie, or from its global id at shift 0)."""
         if self.is_shard:
             raise ValueError("already a shard")
         if not 0 <= rank < world:
@@ -142,7 +145,7 @@ class TreeAHIndex:
         members = self.leaf_members[take]
         rows = None
         dataset = self.dataset
-        if own_rows and shift > 0 and self.dataset is not None:
+        if own_rows and self.dataset is not None:
             rows = self.dataset[members]
             dataset = None
         return TreeAHIndex(
@@ -153,6 +156,31 @@ class TreeAHIndex:
             dataset=dataset, spilling_overretrieve_factor=self.spilling_overretrieve_factor,
             leaf_row_base=lo.astype(np.uint32), global_topn_shift=shift,
             global_spilled=not self.disjoint, member_rows=rows)
+
+    def standalone(self) -> "TreeAHIndex":
+        """This shard as a whole index of its own: members renumbered
+        0..M-1 (member m <-> global id leaf_members[m]) with their float rows
+        as the dataset.  Its ties (leaf << shift | row) order every leaf's
+        rows as the shard's whole-index ties do, so for a disjoint index the
+        shard's local top-k' is this index's top-k' mapped through
+        leaf_members; a SOAR shard's spilled copies become distinct members
+        (no dedupe).  The per-rank work of a range split as an index the
+        oracle and the CPU port can run (bench.py's shard lines)."""
+        if not self.is_shard:
+            raise ValueError("standalone() is for a shard")
+        rows = self.member_rows
+        if rows is None:
+            if self.dataset is None:
+                raise ValueError("the shard has neither member rows nor a dataset")
+            rows = self.dataset[self.leaf_members]
+        m = self.num_members
+        return TreeAHIndex(metric=self.metric, dim=self.dim, num_blocks=self.num_blocks,
+                           dims_per_block=self.dims_per_block, residual=self.residual,
+                           centers=self.centers, codebook=self.codebook,
+                           leaf_offsets=self.leaf_offsets,
+                           leaf_members=np.arange(m, dtype=np.uint32),
+                           member_codes=self.member_codes, num_datapoints=m, dataset=rows,
+                           spilling_overretrieve_factor=self.spilling_overretrieve_factor)
 
     def leaf_sizes(self) -> np.ndarray:
         return np.diff(self.leaf_offsets).astype(np.int64)

@@ -19,16 +19,13 @@ def medium():
 
 
 # eager (the default), graph replay; the work list from the fused seed-launch blocks (the
-# default at <= 4096 leaves), from the side-stream fork/join path, and the fused front end
-# (top-L + seed + leaf slots + the work list's positions in one launch)
+# default at <= 4096 leaves) and from the side-stream fork/join path
 @pytest.mark.parametrize("env", [{}, {"SMX_GRAPH": "1"}, {"SMX_FUSED_WORKLIST": "0"},
-                                 {"SMX_FUSED_WORKLIST": "0", "SMX_GRAPH": "1"},
-                                 {"SMX_FUSED_FRONT": "1"}, {"SMX_FUSED_FRONT": "1", "SMX_GRAPH": "1"}])
+                                 {"SMX_FUSED_WORKLIST": "0", "SMX_GRAPH": "1"}])
 def test_replays_see_new_queries(oracle, medium, env):
     from scann_amd import _native, synthetic
     ix, db, _ = medium
-    old = {k: os.environ.get(k) for k in ("SMX_GRAPH", "SMX_NO_GRAPH", "SMX_FUSED_WORKLIST",
-                                          "SMX_FUSED_FRONT")}
+    old = {k: os.environ.get(k) for k in ("SMX_GRAPH", "SMX_NO_GRAPH", "SMX_FUSED_WORKLIST")}
     try:
         for k in old:
             os.environ.pop(k, None)

@@ -344,33 +344,3 @@ def _nat_env(native, ix, env):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
-
-
-@pytest.mark.parametrize("leaves,pre,final", [(1, 10, 5), (4, 60, 10), (12, 200, 25), (40, 100, 10)])
-def test_fused_front_matches_oracle(native, oracle, small_dot, small_l2, leaves, pre, final):
-    """The fused front end (seed, leaf-slot records and the work list's
-    positions in the top-L launch; the scan deriving its items and shares
-    from the positions) against the oracle, dot product and L2, and equal to
-    the separate-launch pipeline."""
-    for ix, db, q in (small_dot, small_l2):
-        nf = _nat_env(native, ix, {"SMX_FUSED_FRONT": "1"})
-        ns = _nat_env(native, ix, {"SMX_FUSED_FRONT": "0"})
-        try:
-            gi, gd, gc = nf.search_batched(q, leaves, pre, final, True)
-            si, sd, sc = ns.search_batched(q, leaves, pre, final, True)
-            oi, od, oc = oracle.search(ix, q, leaves, pre, final, True, oracle.MODE_IDEAL)
-            np.testing.assert_array_equal(gc, oc)
-            np.testing.assert_array_equal(gi, oi)
-            np.testing.assert_array_equal(np.nan_to_num(gd).view(np.uint32),
-                                          np.nan_to_num(od).view(np.uint32))
-            np.testing.assert_array_equal(gi, si)
-            np.testing.assert_array_equal(np.nan_to_num(gd).view(np.uint32),
-                                          np.nan_to_num(sd).view(np.uint32))
-            # pre-reorder output (the scan's candidates themselves)
-            gi, gd, gc = nf.search_pre_reorder(q, leaves, pre)
-            oi, od, oc = oracle.search_pre_reorder(ix, q, leaves, pre, oracle.MODE_IDEAL)
-            np.testing.assert_array_equal(gi, oi)
-            np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
-        finally:
-            nf.close()
-            ns.close()

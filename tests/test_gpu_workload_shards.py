@@ -1,0 +1,97 @@
+"""configs[3] / configs[4] at their per-rank workload density, against the oracle.
+
+The bench's shard lines search rank 0's shard of an 8-way range split whose
+leaves hold hundreds to thousands of rows each (configs[4]: ~2,500 per
+rank-leaf at 125M rows / 50000 leaves).  The stand-ins of test_gpu_configs.py
+hold ~2-10 rows per rank-leaf, so multi-chunk work items, the candidate-list
+autocap, overflow rescans at K = 24 and the L = 2000 / pre_reorder_nn = 256
+operating point that reaches recall >= 0.95 for configs[4] (bench.py sweep)
+only run at this density.  Here rank 0's shard is generated and built on the
+GPU as bench.py builds it (scann_amd/generate.py), then:
+
+  * the shard as a standalone index (TreeAHIndex.standalone) on the GPU ==
+    the oracle (ideal mode) on the same index, ids and distance bits, at the
+    bench's operating points (tree_ah_hybrid_residual.cc:631-846);
+  * the same with a 512-entry candidate list, so that lists overflow and are
+    rescanned on the device (the timings report the rescan passes);
+  * (disjoint index) the shard engine's own list -- search_shard + merge of
+    that one list, the bench's N = 1 path -- gives the same neighbors by
+    global id.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+NQ = 64
+
+
+def _shard(n, leaves, components, soar, seed, train):
+    from scann_amd import generate
+    ds = generate.GeneratedDataset(n, 96, seed, components=components,
+                                   device=torch.device("cuda"))
+    ix = generate.build_generated_shard(
+        ds, leaves, 0, 8, soar_lambda=soar, seed=seed, training_sample_size=train,
+        training_iterations=4, ah_training_sample_size=100_000, ah_training_iterations=4,
+        counts_from_all_ranks=False)
+    return ix, ds.queries(NQ, seed + 1000)
+
+
+def _check_points(oracle, ix, q, points, min_rows_per_leaf, multi_chunk_leaves):
+    from scann_amd import _native
+    from scann_amd.distributed import NativeShardEngine
+    sizes = ix.leaf_sizes()
+    assert sizes.mean() >= min_rows_per_leaf, sizes.mean()
+    # leaves with more than one work-item chunk (20 tiles of 32 rows)
+    assert int((sizes > 20 * 32).sum()) >= multi_chunk_leaves, int((sizes > 640).sum())
+    view = ix.standalone()
+    nv = _native.NativeIndex(view)
+    eng = NativeShardEngine(ix) if ix.disjoint else None
+    try:
+        for lv, pre in points:
+            oi, od, oc = oracle.search(view, q, lv, pre, 10, True, oracle.MODE_IDEAL, 16)
+            for cap in (0, 512):   # sized per call (autocap); small: overflow rescans
+                nv.set_tuning(candidates_per_query=cap)
+                nv.set_profiling(True)
+                gi, gd, gc = nv.search_batched(q, lv, pre, 10, True)
+                t = nv.timings()
+                nv.set_profiling(False)
+                np.testing.assert_array_equal(gc, oc)
+                np.testing.assert_array_equal(gi, oi, err_msg=f"L={lv} pre={pre} cap={cap}")
+                np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+                if cap:
+                    assert t["overflow_retries"] > 0, t
+            if eng is not None:
+                qd = torch.from_numpy(q).cuda()
+                k = eng.shard_width(lv, pre, 10, True)
+                le = torch.empty((NQ, k, 2), dtype=torch.int64, device="cuda")
+                eng.search_shard(qd, lv, pre, 10, True, le)
+                si, sd, sc = eng.merge(1, le.unsqueeze(0), NQ, lv, pre, 10, True)
+                torch.cuda.synchronize()
+                np.testing.assert_array_equal(si.cpu().numpy().astype(np.uint32),
+                                              ix.leaf_members[oi])
+                np.testing.assert_array_equal(sd.cpu().numpy().view(np.uint32),
+                                              od.view(np.uint32))
+    finally:
+        nv.close()
+        if eng is not None:
+            eng.nat.close()
+
+
+def test_deep1b_shard_at_workload_density(oracle):
+    """configs[4]: rank 0 of 8 of a 50000-leaf dot-product index (shift 16),
+    >= 500 rows per rank-leaf, at the bench's headline L = 400 / pre = 100
+    and the recall-gate point L = 2000 / pre = 256."""
+    ix, q = _shard(8 * 50000 * 520, 50000, 1 << 17, None, 5, 1_000_000)
+    assert ix.global_topn_shift == 16 and ix.disjoint
+    _check_points(oracle, ix, q, [(400, 100), (2000, 256)], 500, 100)
+
+
+def test_soar_shard_at_workload_density(oracle):
+    """configs[3]: rank 0 of 8 of a 10000-leaf SOAR index (shift 18, k' =
+    2 x pre), >= 1000 members per rank-leaf, at the bench's L = 100 /
+    pre = 100 and L = 1000 / pre = 256."""
+    ix, q = _shard(8 * 10000 * 520, 10000, 4096, 1.5, 4, 250_000)
+    assert ix.global_topn_shift == 18 and not ix.disjoint
+    _check_points(oracle, ix, q, [(100, 100), (1000, 256)], 1000, 100)

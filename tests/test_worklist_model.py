@@ -32,46 +32,3 @@ def test_shares_cover_items_exactly_once(seed, qtile):
 def test_edge_shapes(sizes, counts):
     for qtile in (32, 64):
         wm.check(sizes, counts, grid=256, qtile=qtile)
-
-
-@pytest.mark.parametrize("seed", range(8))
-def test_position_items_equal_listed_items(seed):
-    """The fused front end's scan derives items from the positions
-    (ItemFromPositions): every workgroup's segments equal the ones it lists
-    from the materialized work list, including positions without pairs and
-    more than 64 positions per share step."""
-    rng = np.random.default_rng(100 + seed)
-    nl = int(rng.integers(1, 400))
-    sizes = rng.integers(0, 2500, nl)
-    sizes[rng.random(nl) < 0.1] = 0
-    counts = rng.poisson(rng.uniform(0.2, 90), nl)
-    counts[rng.random(nl) < 0.3] = 0
-    grid = int(rng.choice([64, 256, 3072]))
-    wl = wm.build([int(x) for x in sizes], [int(x) for x in counts], grid, 32,
-                  int(rng.choice([8, 20, 40])))
-    for b in range(grid):
-        assert wm.list_segments_pos(wl, b) == wm.list_segments(wl, b), f"workgroup {b}"
-
-
-@pytest.mark.parametrize("seed", range(8))
-def test_share_start_equals_wave_start(seed):
-    """ShareStart (each scan workgroup's own search over the positions' unit
-    prefix) gives the share start WaveStarts writes, position included."""
-    rng = np.random.default_rng(200 + seed)
-    nl = int(rng.integers(1, 2049))
-    sizes = rng.integers(0, 3000, nl)
-    sizes[rng.random(nl) < 0.1] = 0
-    counts = rng.poisson(rng.uniform(0.2, 90), nl)
-    counts[rng.random(nl) < 0.3] = 0
-    grid = int(rng.choice([64, 256, 3072]))
-    wl = wm.build([int(x) for x in sizes], [int(x) for x in counts], grid, 32,
-                  int(rng.choice([8, 20, 40])))
-    units = []
-    for d in wl["pos"]:
-        units.append(((d["cnt"] + 31) // 32) * ((d["n"] + 31) // 32))
-    pu = np.concatenate([[0], np.cumsum(units)]).astype(int).tolist()
-    for b in range(grid):
-        ws, p = wm.share_start(wl, b, grid, pu)
-        assert ws == wl["wave_start"][b], f"workgroup {b}"
-        if ws[2] > 0:
-            assert p == wl["wave_pos"][b], f"workgroup {b} position"

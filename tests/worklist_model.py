@@ -104,17 +104,8 @@ def build(sizes, counts, grid, qtile, chunk_tiles):
                 ch += 1
             wave_start[GROUPS * k + g] = (item0 + tq * chunks + ch, rem, ue - us)
             k += 1
-    # the fused front end's positions (BuildPositions): first item, leaf, size,
-    # pair count; wave starts carry the position of their first item
-    pos = [dict(item0=int(ex_i[p]), leaf=order[p], n=sizes[order[p]], cnt=counts[order[p]])
-           for p in range(nl)]
-    wave_pos = [0] * grid
-    for i, ws in enumerate(wave_start):
-        if ws[2] > 0:
-            wave_pos[i] = max(p for p in range(nl)
-                              if pos[p]["item0"] <= ws[0] and items_p[p] > 0)
     return dict(order=order, work=work, wave_start=wave_start, gunits=gunits, total_w=total_w,
-                pos=pos, wave_pos=wave_pos, chunk_tiles=chunk_tiles, qtile=qtile)
+                chunk_tiles=chunk_tiles, qtile=qtile)
 
 
 def list_segments(wl, b, max_segs=512):
@@ -165,75 +156,3 @@ def check(sizes, counts, grid=256, qtile=64, chunk_tiles=20):
             assert (idx, t) in seen, f"tile {t} of item {idx} (leaf {leaf}) never scanned"
     assert len(seen) == wl["total_w"]
     return wl
-
-
-def item_from_positions(wl, sp, idx):
-    """ItemFromPositions: item idx from the 64 positions loaded at sp
-    (None when it lies past them)."""
-    pos, ct, qtile = wl["pos"], wl["chunk_tiles"], wl["qtile"]
-    window = [pos[p] if p < len(pos) else None for p in range(sp, sp + 64)]
-    item0 = [d["item0"] if d else 2**32 - 1 for d in window]
-    q = 0
-    for st in (32, 16, 8, 4, 2, 1):
-        if item0[q + st] <= idx:
-            q += st
-    d = window[q]
-    if d is None or idx < d["item0"]:
-        return None
-    chunks = chunks_of(d["n"], ct)
-    qt = (d["cnt"] + qtile - 1) // qtile
-    if idx >= d["item0"] + qt * chunks:
-        return None
-    u = idx - d["item0"]
-    tq, ch = divmod(u, chunks)
-    j0, j1 = chunk_tiles_range(d["n"], ct, ch)
-    return (d["leaf"], d["n"], j0, j1, tq), sp + q
-
-
-def list_segments_pos(wl, b):
-    """ListSegments over the positions (fused front end)."""
-    sw, sj, su = wl["wave_start"][b]
-    sp = wl["wave_pos"][b]
-    segs = []
-    while su > 0:
-        excl, nused, last_pos = 0, 0, sp
-        for lane in range(64):
-            r = item_from_positions(wl, sp, sw + lane)
-            if r is None or excl >= su:
-                break
-            it, p = r
-            j0 = sj if (lane == 0 and sj) else it[2]
-            t = min(it[3] - j0, su) if it[3] > j0 else 0
-            if t > 0:
-                segs.append((sw + lane, j0, j0 + min(t, su - excl)))
-            excl += t
-            nused += 1
-            last_pos = p
-        assert nused > 0, f"workgroup {b}: no item found from position {sp}"
-        sw += nused
-        su -= min(su, excl)
-        sp = last_pos
-        sj = 0
-    return segs
-
-
-def share_start(wl, b, grid, pos_unit0):
-    """ShareStart: workgroup b's share start from the positions' unit prefix
-    (two rounds of a 64-ary search), as (item, first tile, units), position."""
-    gunits, pos, ct, qtile = wl["gunits"], wl["pos"], wl["chunk_tiles"], wl["qtile"]
-    nl = len(pos)
-    g, k = b % GROUPS, b // GROUPS
-    nw = (grid - g + GROUPS - 1) // GROUPS
-    U0, span = gunits[g], gunits[g + 1] - gunits[g]
-    us, ue = U0 + span * k // nw, U0 + span * (k + 1) // nw
-    if us >= ue:
-        return (0, 0, 0), 0
-    l1 = max(l for l in range(64) if min(32 * l, nl) < nl and pos_unit0[min(32 * l, nl)] <= us)
-    p = max(32 * l1 + l for l in range(32) if 32 * l1 + l < nl and pos_unit0[32 * l1 + l] <= us)
-    d = pos[p]
-    tiles = (d["n"] + 31) // 32
-    tq, rem = divmod(us - pos_unit0[p], tiles)
-    ch = 0
-    while chunk_tiles_range(d["n"], ct, ch)[1] <= rem:
-        ch += 1
-    return (d["item0"] + tq * chunks_of(d["n"], ct) + ch, rem, ue - us), p

@@ -3,9 +3,8 @@
 # repo root); every GPU step under its own time limit, chained with &&.
 #   diag : the -m gpu suite on the diagnostic library (device index checks on
 #          every computed index) + the phase-stamp tool, once;
-#   ab   : fused vs separate front end (tools/ab_front.sh);
 #   prof : the round profile of the bench workload (tools/profile_bench.sh).
-# STEPS="diag ab prof" selects; output under gpurun_out/$TAG.*
+# STEPS="diag prof" selects; output under gpurun_out/$TAG.*
 set -o pipefail
 TAG=${TAG:-rg}
 O=gpurun_out
@@ -13,7 +12,7 @@ mkdir -p $O
 step() { echo "[round_gpu] $(date +%T) $*" >&2; }
 PYTEST="python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread"
 rc=0
-for s in ${STEPS:-diag ab prof}; do
+for s in ${STEPS:-diag prof}; do
   case $s in
     diag)
       step "diag suite" &&
@@ -21,8 +20,6 @@ for s in ${STEPS:-diag ab prof}; do
           > $O/$TAG.diag_tests.log 2>&1 &&
       step "phase stamps" &&
       timeout -k 10 240 python tools/phase_stamps.py > $O/$TAG.phase.log 2>&1 || rc=1 ;;
-    ab)
-      step "front-end A/B" && TAG=$TAG.ab bash tools/ab_front.sh || rc=1 ;;
     prof)
       step "profile" && timeout -k 10 900 bash tools/profile_bench.sh $O/$TAG.prof || rc=1 ;;
     tune)
