@@ -833,10 +833,24 @@ static void PipelineBEmulate(const IndexView& v, const std::vector<int>& leaves,
 // FastTopNeighbors -- with the results scaled by 1.0f / mult; every result,
 // mapped to its global id, pushed into one TopNeighbors<float>(k'); once it
 // is full the next leaf's epsilon is its approx_bottom (:1004-1010).
+// A single token (:926-949) is the leaf searcher's own search with
+// pre_reordering_num_neighbors -- no spilling multiplier, no dedupe -- its
+// results remapped to global ids.
 static void PipelineBGeneric(const IndexView& v, const std::vector<int>& leaves,
-                             const Lut& lut, float inv, int32_t kk, NN* out) {
+                             const Lut& lut, float inv, int32_t kk, int32_t pre_nn, NN* out) {
   const orc_index* ix = v.ix;
   out->clear();
+  if (leaves.size() == 1) {
+    const int leaf = leaves[0];
+    const size_t k1 = size_t(std::max(pre_nn, 0));
+    if (k1 == 0) return;
+    std::vector<std::pair<uint32_t, int16_t>> local;
+    LeafInt16TopN(ix, leaf, lut, k1, LeafInt16Epsilon(kInf, lut.mult), &local);
+    const uint64_t beg = ix->leaf_offsets[leaf];
+    for (const auto& e : local)
+      out->push_back({ix->leaf_members[beg + e.first], static_cast<float>(e.second) * inv});
+    return;
+  }
   const size_t k = size_t(std::max(kk, 0));
   if (k == 0 || leaves.empty()) return;
   TopNeighborsF top(k);
@@ -940,7 +954,7 @@ static void QueryPreReorder(const IndexView& v, const float* q, int L,
     }
     *out = std::move(res);
   } else if (mode == ORC_MODE_EMULATE && !residual && generic) {
-    PipelineBGeneric(v, leaves, lut, inv, kk, out);
+    PipelineBGeneric(v, leaves, lut, inv, kk, pre_nn, out);
   } else if (mode == ORC_MODE_EMULATE && !residual) {
     PipelineBEmulate(v, leaves, lut, inv, kk, out);
   } else {

@@ -189,3 +189,24 @@ def test_emulate_pipeline_b_generic_tight_epsilon(oracle):
     ii, idist, ic = oracle.search_pre_reorder(ix, qq, 32, 5, oracle.MODE_IDEAL)
     assert ec[0] == 5 and len(set(ei[0].tolist())) == 5
     assert set(ei[0].tolist()) == set(ii[0].tolist())
+
+
+def test_emulate_pipeline_b_single_token(oracle):
+    """One token on the generic path (L = 1, tree_x_hybrid_smmd.cc:926-949):
+    the leaf searcher's own search with pre_reordering_num_neighbors, no
+    spilling multiplier and no dedupe; on a SOAR index this is the leaf's
+    exact top pre_nn by (int16 distance, id) = the ideal top pre_nn, ids of
+    one leaf only."""
+    from scann_amd import index_builder, synthetic
+    db = synthetic.mixture(5000, 32, 40, 0.6, 9, normalize=False)
+    q = synthetic.mixture(4, 32, 40, 0.6, 109, normalize=False, means_seed=9)
+    ix = index_builder.build_tree_ah(db, 1, 64, 2, training_iterations=4,
+                                     ah_training_iterations=4, soar_lambda=1.5, seed=9)
+    assert not ix.residual and not ix.disjoint
+    for k in (5, 40):
+        ii, idist, ic = oracle.search_pre_reorder(ix, q, 1, k, oracle.MODE_IDEAL)
+        ei, ed, ec = oracle.search_pre_reorder(ix, q, 1, k, oracle.MODE_EMULATE)
+        np.testing.assert_array_equal(ec, ic)
+        assert (ec <= k).all()
+        for r in range(q.shape[0]):
+            np.testing.assert_array_equal(np.sort(ei[r, :ec[r]]), np.sort(ii[r, :ic[r]]))
