@@ -158,7 +158,17 @@ def scan_roofline(code_bytes, scan_ms, timings, num_blocks):
     sec = scan_ms * 1e-3
     achieved = ops / sec / 1e12
     k = scan_k(num_blocks)
-    smfmac = float(timings.get("scan_item_tiles", 0.0)) * (k // 2)
+    # executed MFMA work: 32-slot tiles x K/2 v_smfmac_i32_32x32x64_i8 (32
+    # cycles each), 16-slot tiles x 2 ceil(K/4) v_smfmac_i32_16x16x128_i8 (16)
+    t32 = float(timings.get("scan_item_tiles", 0.0))
+    t16 = float(timings.get("scan_item_tiles16", 0.0))
+    smfmac = t32 * (k // 2)
+    smfmac16 = t16 * 2 * ((k + 3) // 4)
+    mfma_cycles = smfmac * 32.0 + smfmac16 * 16.0
+    # useful fraction of the executed MFMA work: the algorithmic ops over the
+    # dense-equivalent ops the executed instructions carry (empty query
+    # slots and K padding are the rest)
+    executed_ops = smfmac * 131072.0 + smfmac16 * 65536.0
     return {
         "bound": "mfma", "achieved": round(achieved, 1), "peak": round(SMFMAC_PEAK_TOPS, 1),
         "unit": "TOP/s", "frac": round(achieved / SMFMAC_PEAK_TOPS, 4),
@@ -174,7 +184,10 @@ def scan_roofline(code_bytes, scan_ms, timings, num_blocks):
         "algorithmic_code_bytes_per_launch": code_bytes,
         "avg_launch_ms": round(scan_ms, 5),
         "smfmac_executed_per_launch": smfmac,
-        "smfmac_pipe_frac": round(smfmac * 32.0 / (1024 * 2.4e9 * sec), 4) if smfmac else None,
+        "smfmac16_executed_per_launch": smfmac16,
+        "tiles_32_slot": t32, "tiles_16_slot": t16,
+        "smfmac_pipe_frac": round(mfma_cycles / (1024 * 2.4e9 * sec), 4) if mfma_cycles else None,
+        "useful_mfma_frac": round(ops / executed_ops, 4) if executed_ops else None,
         # SURVEY §8d's byte roofline: algorithmic code bytes / time; above the
         # 8 TB/s HBM peak by design (the query tiles of a leaf re-read its
         # codes from L2), hence the MFMA bound

@@ -135,9 +135,12 @@ typedef struct smx_timings {
   int32_t seed_pairs;
   int32_t overflow_retries; /* candidate-buffer tightening passes            */
   int32_t max_candidates;   /* largest per-query survivor count              */
-  double scan_item_tiles;   /* 32x32 MFMA tiles of the main scan (x K MFMAs)  */
+  double scan_item_tiles;   /* 32-slot tiles of the main scan
+                               (x K/2 v_smfmac_i32_32x32x64_i8)              */
   float mean_candidates;    /* survivors per query (last pass)               */
   int32_t scan_workgroups;  /* persistent scan grid (one wave each)          */
+  double scan_item_tiles16; /* 16-slot tiles of the main scan
+                               (x 2*ceil(K/4) v_smfmac_i32_16x16x128_i8)     */
 } smx_timings;
 
 /* Index lifecycle (ScannNumpy ctor / destructor; scann_npy.cc:57-77). */

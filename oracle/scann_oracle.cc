@@ -630,10 +630,10 @@ static int GlobalShift(const orc_index* ix) {
 
 static void BuildView(const orc_index* ix, IndexView* v) {
   v->ix = ix;
-  v->shift = GlobalShift(ix);
+  v->shift = ix->is_shard ? ix->global_topn_shift : GlobalShift(ix);
   const uint64_t nmem = ix->leaf_offsets[ix->num_leaves];
-  v->disjoint = (nmem == ix->num_datapoints);
-  if (v->disjoint) {
+  v->disjoint = ix->is_shard ? !ix->global_spilled : (nmem == ix->num_datapoints);
+  if (v->disjoint && !ix->is_shard) {
     std::vector<uint8_t> seen(ix->num_datapoints, 0);
     for (uint64_t i = 0; i < nmem; ++i) {
       const uint32_t g = ix->leaf_members[i];

@@ -49,6 +49,15 @@ typedef struct orc_index {
   const float* dataset;      /* [num_datapoints][dim] or NULL (no reorder)  */
   float spilling_overretrieve_factor; /* SOAR over-retrieval (default 2)   */
   int32_t pad_;
+  /* A range-split shard (the tail of smx_index_desc): with is_shard the
+   * whole index's tie shift and spill setting replace the ones this index's
+   * own leaves would give (the rows' order inside a leaf is the same). */
+  int32_t is_shard;
+  int32_t global_topn_shift;
+  int32_t global_spilled;
+  int32_t reserved2;
+  const uint32_t* leaf_row_base;   /* unused by the oracle */
+  const float* member_rows;        /* unused by the oracle (reorders from dataset) */
 } orc_index;
 
 /* Partition scores, transposed many-to-many numerics

@@ -36,7 +36,7 @@ class Timings(ctypes.Structure):
                 ("scan_pairs", ctypes.c_int32), ("seed_pairs", ctypes.c_int32),
                 ("overflow_retries", ctypes.c_int32), ("max_candidates", ctypes.c_int32),
                 ("scan_item_tiles", ctypes.c_double), ("mean_candidates", ctypes.c_float),
-                ("scan_workgroups", ctypes.c_int32)]
+                ("scan_workgroups", ctypes.c_int32), ("scan_item_tiles16", ctypes.c_double)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

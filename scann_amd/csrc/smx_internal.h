@@ -11,6 +11,25 @@ namespace smx {
 // Query-tile width of the LUT16 scan: one MFMA i32_32x32x32_i8 covers 32
 // datapoints x 32 queries x 2 AH blocks.
 constexpr int kQueriesPerTile = 32;
+// A leaf's last query tile with at most this many queries runs on the
+// 16-slot path (v_smfmac_i32_16x16x128_i8); its work item is marked in the
+// leaf field.
+constexpr int kNarrowSlots = 16;
+// WorklistArgs::totals[kTotalsTiles16]: the call's 16-slot tiles (stats[12])
+constexpr int kTotalsTiles16 = 9;
+// The seed scan (the per-query thresholds on MFMA): each leaf lists at most
+// kSeedSlots of the queries it seeds (the top-L kernel claims the slots), each
+// query keeps at most kSeedKeys seed distances -- SeedLeafCap per seed leaf.
+constexpr int kSeedSlots = 32;
+constexpr int kSeedKeys = 4096;
+constexpr int kSeedMaxMfma = 32;   // seed leaves per query (the seed mask's bits)
+__host__ __device__ constexpr int SeedLeafCap(int seed) {
+  return seed <= 0 ? 0 : (kSeedKeys / seed < 1024 ? (kSeedKeys / seed) & ~31 : 1024);
+}
+constexpr uint32_t kItemNarrow = 1u << 31;
+// 16-slot tiles are used when a call averages fewer queries per leaf
+// (nq * L / num_leaves) than this
+constexpr int kNarrowQueriesPerLeaf = 32;
 constexpr int kDpPerTile = 32;
 constexpr int kMaxBlocks = 64;           // LUT16 blocks supported (K <= 32)
 constexpr uint64_t kNoThreshold = ~0ull;
@@ -20,6 +39,11 @@ constexpr int kWorkGroups = 8;        // XCD groups of the scan's work list
 // atomics over 1000 packed counters (32 lines) cost ~12 us where one line per
 // counter costs ~1 us.  counter(i) = base[i * kCounterStride].
 constexpr uint32_t kCounterStride = 32;
+
+// LUT rows (16 int8 entries each) per query: the 2K blocks of the 32-slot
+// scan, padded with zero rows to whole 8-block steps of the 16-slot scan
+// (K = 26, glove: 52 -> 56).  Row b = AH block b; rows >= num_blocks are 0.
+__host__ __device__ constexpr int LutRows(int ksteps) { return 8 * ((ksteps + 3) / 4); }
 
 // Bytes of code data one lane holds per 32-datapoint tile: lane (r, h) keeps
 // the nibbles of datapoint r for blocks h, h+2, h+4, ... (K = ceil(B/2)).
@@ -95,9 +119,10 @@ struct Bounds {
 };
 
 // One work item of the scan: a chunk [j0, jend) of the 32-datapoint tiles of
-// a leaf, for one 32-query tile of that leaf's query list.
+// a leaf, for one query tile (32 slots, or 16 with kItemNarrow set in `leaf`)
+// of that leaf's query list.
 struct WorkItem {
-  uint32_t leaf;
+  uint32_t leaf;         // | kItemNarrow for a 16-slot query tile
   uint32_t n;            // leaf size (datapoints)
   uint32_t j0, jend;     // tile range
   uint64_t tile_off;     // the leaf's first code tile
@@ -145,6 +170,14 @@ struct ScanArgs {
 struct SeedArgs {
   const int32_t* topl_leaf;   // [nq][L]
   const float* topl_dist;     // [nq][L]
+  // the seed scan (mfma != 0): per leaf its seeding queries, per query its
+  // granted seed leaves and their distances
+  int mfma;
+  const uint32_t* seed_count; // [nl] strided (kCounterStride)
+  const uint32_t* seed_list;  // [nl][kSeedSlots] query | seed index << 24
+  const uint32_t* seed_mask;  // [nq] bit i: seed leaf i was scanned
+  uint32_t* seed_keys;        // [nq][kSeedKeys] ordered distances, [i][SeedLeafCap]
+  int nl;
   // the inversion (pair scatter): every (query, leaf) pair's slot in its
   // leaf's work items
   const uint32_t* rank;       // [nq][L] position inside the leaf's list
@@ -177,16 +210,20 @@ struct WorklistArgs {
   int nb;
   uint32_t chunk_tiles;
   int grid;                    // scan workgroups
+  uint32_t narrow;             // 16-slot tiles for remainders of <= 16 queries
   uint32_t* leaf_item0;        // [nl]
   uint32_t* pos_unit0;         // [nl + 1]
   uint32_t* gunits;            // [9]
-  uint32_t* totals;            // [3] pairs, items, units
+  uint32_t* totals;            // [3] pairs, items, units; [kTotalsTiles16] 16-slot tiles
   unsigned long long* code_bytes;
   WorkItem* work;
   ItemLane* lanes;
   uint4* wave_start;           // [grid]
   Bounds bd;                  // debug-build index checks
 };
+// 64-bit words of one work-list block's sums (WorklistPart: items, units,
+// pairs, code bytes, 16-slot tiles).
+constexpr int kWorklistPartWords = 5;
 // Up to this many leaves the work list is built by one extra block of the
 // seed launch (no second stream, no fork/join); above it by three launches.
 constexpr int kFusedWorklistLeaves = 4096;
@@ -285,6 +322,11 @@ struct FrontArgs {
   float* mult = nullptr;            // [nq]
   float* inv = nullptr;             // [nq]
   int one_to_many = 0;              // the single-query partition scores (A.8 order)
+  // the seed scan's claims (NULL: the per-query seed kernel)
+  uint32_t* seed_count = nullptr;   // [nl] strided, zeroed by init
+  uint32_t* seed_list = nullptr;    // [nl][kSeedSlots]
+  uint32_t* seed_mask = nullptr;    // [nq]
+  int seed = 0;                     // seed leaves per query (<= kSeedMaxMfma)
 };
 hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int nq,
                                int L, int32_t* out_leaf, float* out_dist,
@@ -302,12 +344,14 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count,
                           ItemLane* lanes /*[max items][32]*/, uint4* wave_start /*[grid]*/,
                           int grid, uint32_t* totals /*[3]*/,
                           unsigned long long* code_bytes /*[1]*/, uint32_t chunk_tiles,
-                          unsigned long long* part /*[4 * ceil(nl / 256)]*/, const Bounds& bd,
-                          hipStream_t s);
-// variant 0: the LUT16 scan (lut16_scan_kernel); 4: the same without its
-// threshold epilogue (timing ablation, results invalid).
+                          uint32_t narrow,
+                          unsigned long long* part /*[kWorklistPartWords * ceil(nl / 256)]*/,
+                          const Bounds& bd, hipStream_t s);
+// variant 0: the LUT16 scan (lut16_scan_kernel; `narrow`: the work list
+// holds 16-slot items); 4: the same without its threshold epilogue (timing
+// ablation, results invalid; the diagnostic variants take 32-slot items only).
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,
-                      hipStream_t s);
+                      hipStream_t s, bool narrow);
 // Resident scan workgroups per CU (occupancy of the index's instantiation).
 hipError_t ScanBlocksPerCU(const DeviceIndex& ix, int* blocks);
 // The per-query thresholds (tau_key) from the seed leaves.
@@ -315,11 +359,19 @@ WorklistArgs MakeWorklistArgs(const DeviceIndex& ix, const uint32_t* leaf_count,
                               uint32_t* leaf_item0, uint32_t* pos_unit0, uint32_t* gunits,
                               ItemLane* lanes, uint4* wave_start, int grid, uint32_t* totals,
                               unsigned long long* code_bytes, uint32_t chunk_tiles,
-                              const Bounds& bd);
+                              uint32_t narrow, const Bounds& bd);
 // The seed thresholds (one block per query); with `wl`, one more block
 // builds the whole work list (ix.nl <= kFusedWorklistLeaves).
 hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s,
                       const WorklistArgs* wl = nullptr);
+// The seed scan (MFMA): every listed (leaf, seeding query) pair's distances
+// into seed_keys; with `wl`, extra blocks build the whole work list
+// (ix.nl <= kFusedWorklistLeaves).  Needs 1 <= a.seed <= kSeedMaxMfma.
+hipError_t LaunchSeedScan(const DeviceIndex& ix, const SeedArgs& a, hipStream_t s,
+                          const WorklistArgs* wl = nullptr);
+// Per query its threshold from the seed scan's distances, then its pairs'
+// lane records (after the work list: they need leaf_item0).
+hipError_t LaunchSeedSelect(const SeedArgs& a, int nq, hipStream_t s);
 // Every (query, leaf) pair's lane record into its leaf's work items (after
 // LaunchWorklist and the seed thresholds: each record carries its sum limit).
 hipError_t LaunchPairScatter(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s);

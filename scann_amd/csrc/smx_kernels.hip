@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "smx_internal.h"
 
@@ -432,7 +433,7 @@ __global__ void __launch_bounds__(256) partition_scores_kernel(
 // 127 / max(sqrt(FLT_EPSILON), max|raw|); int8 = round(raw * m) (the uint8
 // table minus its bias 128); inv = (float)(1.0/(double)m) for residual
 // indexes (lut16_avx2.inc:427-430), 1.0f/m otherwise (querying.h:450-454).
-// LUT rows are padded to 2*K blocks with zeros.
+// LUT rows are padded to LutRows(K) blocks with zeros.
 // ---------------------------------------------------------------------------
 struct LutParams {
   const float* queries;
@@ -529,7 +530,35 @@ struct TopLTail {
   uint32_t* leaf_count;   // or NULL
   uint32_t* rank;
   LutParams lut;          // lut.lut NULL: no LUT
+  uint32_t* seed_count;   // the seed scan's claims, or NULL
+  uint32_t* seed_list;
+  uint32_t* seed_mask;
+  int seed;
 };
+
+// The query's first `seed` leaves claim slots in those leaves' seed lists
+// (the seed scan, seed_scan_kernel): a returning atomic on the leaf's seed
+// counter gives the slot; a leaf lists at most kSeedSlots seeding queries,
+// and a query without a slot goes without that seed leaf (the k'-th of a
+// subset of its candidates still bounds the final k'-th).  The granted seed
+// indices form the query's seed mask.  Block-wide (every thread calls).
+__device__ void SeedClaims(int qi, uint32_t m, const uint64_t* keys, const TopLTail& tail) {
+  if (!tail.seed_count) return;   // (uniform)
+  __shared__ uint32_t s_mask;
+  if (threadIdx.x == 0) s_mask = 0;
+  __syncthreads();
+  const int i = int(threadIdx.x);
+  if (i < tail.seed && uint32_t(i) < m) {
+    const uint32_t leaf = uint32_t(keys[i] & 0xFFFFFFFFu);
+    const uint32_t slot = atomicAdd(&tail.seed_count[size_t(leaf) * kCounterStride], 1u);
+    if (slot < uint32_t(kSeedSlots)) {
+      tail.seed_list[size_t(leaf) * kSeedSlots + slot] = uint32_t(qi) | (uint32_t(i) << 24);
+      atomicOr(&s_mask, 1u << i);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) tail.seed_mask[qi] = s_mask;
+}
 
 __device__ void TopLFinish(int qi, int L, uint32_t m, const uint64_t* sel, int32_t* out_leaf,
                            float* out_dist, const TopLTail& tail) {
@@ -556,6 +585,7 @@ __device__ void TopLFinish(int qi, int L, uint32_t m, const uint64_t* sel, int32
       if (tail.leaf_count && uint32_t(i) < m) tail.rank[size_t(qi) * L + i] = rk[u];
     }
   }
+  SeedClaims(qi, m, sel, tail);
   if (tail.lut.lut) {
     __syncthreads();
     BuildLut(qi, tail.lut);
@@ -738,6 +768,7 @@ __device__ __forceinline__ void TopLBlock(const float* __restrict__ scores, int 
     if (tail.leaf_count && has) tail.rank[size_t(qi) * L + i] = atomicAdd(&tail.leaf_count[size_t(leaf) * kCounterStride], 1u);
   }
   SMX_PHASE(0, qi, 4);
+  SeedClaims(qi, m, srt, tail);
   if (tail.lut.lut) BuildLut(qi, tail.lut);
   SMX_PHASE(0, qi, 5);
 }
@@ -1048,17 +1079,29 @@ __device__ __forceinline__ uint2 ChunkTiles(uint32_t n, uint32_t chunk_tiles, ui
 // therefore not the query order; nothing depends on it (every result is an
 // exact top-k under a total order).
 //
-// Work items = (leaf, 32-query tile, chunk of <= chunk_tiles tiles), listed
+// Work items = (leaf, query tile, chunk of <= chunk_tiles tiles), listed
 // largest leaf first, cut into 8 XCD groups of consecutive leaves with equal
 // MFMA work (exclusive work prefix x 8 / total work), so that all items of a
-// leaf share a group.
+// leaf share a group.  A leaf's c queries fill c / 32 query tiles of 32
+// slots; a remainder of at most 16 queries takes one 16-slot tile (the
+// v_smfmac_i32_16x16x128_i8 path: half the MFMA work), a larger one a
+// 32-slot tile.  A work unit is a 16-slot tile: a 32-slot item's tiles weigh
+// 2 units, a 16-slot item's 1; the shares cut the units, and a tile belongs
+// to the share that holds its first unit.
 // ---------------------------------------------------------------------------
-// Per leaf: its query tiles, MFMA tiles (= the scan's work units) and items.
+// 32-slot and 16-slot query tiles of a leaf with c queries.
+__device__ __forceinline__ uint2 LeafQueryTiles(uint32_t c, uint32_t narrow) {
+  const uint32_t full = c / uint32_t(kQueriesPerTile), r = c % uint32_t(kQueriesPerTile);
+  if (r == 0) return make_uint2(full, 0u);
+  if (narrow && r <= uint32_t(kNarrowSlots)) return make_uint2(full, 1u);
+  return make_uint2(full + 1u, 0u);
+}
+// Per leaf: its items and units.
 __device__ __forceinline__ uint32_t LeafUnits(uint32_t c, uint32_t n, uint32_t chunk_tiles,
-                                              uint32_t& items) {
-  const uint32_t qt = (c + kQueriesPerTile - 1) / kQueriesPerTile;
-  items = qt * LeafChunks(n, chunk_tiles);
-  return qt * ((n + 31u) / 32u);
+                                              uint32_t narrow, uint32_t& items) {
+  const uint2 qt = LeafQueryTiles(c, narrow);
+  items = (qt.x + qt.y) * LeafChunks(n, chunk_tiles);
+  return (2u * qt.x + qt.y) * ((n + 31u) / 32u);
 }
 
 // Phase 1 in two multi-block passes over the leaf positions in work order
@@ -1069,20 +1112,23 @@ __device__ __forceinline__ uint32_t LeafUnits(uint32_t c, uint32_t n, uint32_t c
 // item (leaf_item0) and first unit (pos_unit0, by position), the 8 groups'
 // unit boundaries (gunits[0..8]; gunits[8] = all units) and the totals.
 struct WorklistPart {
-  unsigned long long items, units, pairs, bytes;
+  unsigned long long items, units, pairs, bytes, tiles16;
 };
+static_assert(sizeof(WorklistPart) == kWorklistPartWords * 8, "work-list part buffer layout");
 
 __device__ __forceinline__ void PositionWork(const uint32_t* __restrict__ cnt,
                                              const uint32_t* __restrict__ order,
                                              const uint32_t* __restrict__ leaf_size, int nl,
-                                             int nb, uint32_t chunk_tiles, int p, uint32_t& items,
-                                             uint32_t& units, uint32_t& pairs, uint64_t& bytes) {
-  items = units = pairs = 0;
+                                             int nb, uint32_t chunk_tiles, uint32_t narrow, int p,
+                                             uint32_t& items, uint32_t& units, uint32_t& pairs,
+                                             uint64_t& bytes, uint32_t& ntiles16) {
+  items = units = pairs = ntiles16 = 0;
   bytes = 0;
   if (p < nl) {
     const uint32_t leaf = order[p];
     const uint32_t c = cnt[size_t(leaf) * kCounterStride], n = leaf_size[leaf];
-    units = LeafUnits(c, n, chunk_tiles, items);
+    units = LeafUnits(c, n, chunk_tiles, narrow, items);
+    ntiles16 = LeafQueryTiles(c, narrow).y * ((n + 31u) / 32u);
     pairs = c;
     // algorithmic code bytes: 16 * B * ceil(n / 32) per (query, leaf) pair
     bytes = 16ull * nb * ((n + 31u) / 32u) * c;
@@ -1092,16 +1138,16 @@ __device__ __forceinline__ void PositionWork(const uint32_t* __restrict__ cnt,
 __global__ void __launch_bounds__(256) worklist_part_kernel(
     const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ order,
     const uint32_t* __restrict__ leaf_size, int nl, int nb, uint32_t chunk_tiles,
-    WorklistPart* __restrict__ part) {
-  __shared__ unsigned long long red[4][4];
-  uint32_t items, units, pairs;
+    uint32_t narrow, WorklistPart* __restrict__ part) {
+  __shared__ unsigned long long red[4][5];
+  uint32_t items, units, pairs, t16;
   uint64_t bytes;
-  PositionWork(cnt, order, leaf_size, nl, nb, chunk_tiles, int(blockIdx.x * 256 + threadIdx.x),
-               items, units, pairs, bytes);
-  unsigned long long v[4] = {items, units, pairs, bytes};
+  PositionWork(cnt, order, leaf_size, nl, nb, chunk_tiles, narrow,
+               int(blockIdx.x * 256 + threadIdx.x), items, units, pairs, bytes, t16);
+  unsigned long long v[5] = {items, units, pairs, bytes, t16};
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 5; ++k) {
     for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
     if (lane == 0) red[wid][k] = v[k];
   }
@@ -1112,6 +1158,7 @@ __global__ void __launch_bounds__(256) worklist_part_kernel(
     w.units = red[0][1] + red[1][1] + red[2][1] + red[3][1];
     w.pairs = red[0][2] + red[1][2] + red[2][2] + red[3][2];
     w.bytes = red[0][3] + red[1][3] + red[2][3] + red[3][3];
+    w.tiles16 = red[0][4] + red[1][4] + red[2][4] + red[3][4];
     part[blockIdx.x] = w;
   }
 }
@@ -1119,40 +1166,42 @@ __global__ void __launch_bounds__(256) worklist_part_kernel(
 __global__ void __launch_bounds__(256) worklist_kernel(
     const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ order,
     const uint32_t* __restrict__ leaf_size, int nl, int nb, uint32_t chunk_tiles,
-    const WorklistPart* __restrict__ part, uint32_t* __restrict__ leaf_item0,
+    uint32_t narrow, const WorklistPart* __restrict__ part, uint32_t* __restrict__ leaf_item0,
     uint32_t* __restrict__ pos_unit0, uint32_t* __restrict__ gunits, uint32_t* __restrict__ totals,
     unsigned long long* __restrict__ code_bytes) {
-  __shared__ unsigned long long red[4][6];
+  __shared__ unsigned long long red[4][7];
   __shared__ uint32_t wsum[4], s_units[256];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nblk = int(gridDim.x), blk = int(blockIdx.x);
   // the blocks before this one and all blocks (256 per round)
-  unsigned long long bi = 0, bu = 0, ti = 0, tu = 0, tp = 0, tb = 0;
+  unsigned long long bi = 0, bu = 0, ti = 0, tu = 0, tp = 0, tb = 0, tn = 0;
   for (int b = tid; b < nblk; b += 256) {
     const WorklistPart w = part[b];
     if (b < blk) { bi += w.items; bu += w.units; }
-    ti += w.items; tu += w.units; tp += w.pairs; tb += w.bytes;
+    ti += w.items; tu += w.units; tp += w.pairs; tb += w.bytes; tn += w.tiles16;
   }
-  unsigned long long v[6] = {bi, bu, ti, tu, tp, tb};
+  unsigned long long v[7] = {bi, bu, ti, tu, tp, tb, tn};
 #pragma unroll
-  for (int k = 0; k < 6; ++k) {
+  for (int k = 0; k < 7; ++k) {
     for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
     if (lane == 0) red[wid][k] = v[k];
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < 6; ++k) v[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+  for (int k = 0; k < 7; ++k) v[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
   const uint32_t total_w = uint32_t(v[3]);
   if (blk == 0 && tid == 0) {
     totals[0] = uint32_t(v[4]);
     totals[1] = uint32_t(v[2]);
     totals[2] = total_w;
+    totals[kTotalsTiles16] = uint32_t(v[6]);
     code_bytes[0] = v[5];
   }
   const int p = blk * 256 + tid;
-  uint32_t items, units, pairs;
+  uint32_t items, units, pairs, t16;
   uint64_t bytes;
-  PositionWork(cnt, order, leaf_size, nl, nb, chunk_tiles, p, items, units, pairs, bytes);
+  PositionWork(cnt, order, leaf_size, nl, nb, chunk_tiles, narrow, p, items, units, pairs, bytes,
+               t16);
   const uint32_t inc_i = BlockInclusiveScan256(items, wsum);
   __syncthreads();   // wsum is reused
   const uint32_t inc_u = BlockInclusiveScan256(units, wsum);
@@ -1173,9 +1222,9 @@ __global__ void __launch_bounds__(256) worklist_kernel(
   int prev = -1;
   if (p > 0) {
     const uint32_t prev_units = tid > 0 ? s_units[tid - 1] : [&] {
-      uint32_t it, un, pa;
+      uint32_t it, un, pa, t1;
       uint64_t by;
-      PositionWork(cnt, order, leaf_size, nl, nb, chunk_tiles, p - 1, it, un, pa, by);
+      PositionWork(cnt, order, leaf_size, nl, nb, chunk_tiles, narrow, p - 1, it, un, pa, by, t1);
       return un;
     }();
     prev = group_of(ex_u - prev_units);
@@ -1188,15 +1237,19 @@ __global__ void __launch_bounds__(256) worklist_kernel(
 }
 
 // The scan workgroups whose share starts in position p's units [ua, ub)
-// (leaf size n, first item item0): workgroup i of group g (i % 8 == g) takes
-// the units [U0 + span * k / nw, U0 + span * (k + 1) / nw) of its group, k =
-// i / 8 of the group's nw; its start {item, first tile, units, position}.
-// Threads first, first + step, ... of the caller take the k in turn.
+// (leaf size n, c queries, first item item0): workgroup i of group g (i % 8
+// == g) takes the units [U0 + span * k / nw, U0 + span * (k + 1) / nw) of
+// its group, k = i / 8 of the group's nw; its start {item, first tile,
+// units, position}: the first tile whose first unit is in the share (a
+// share that begins inside a 32-slot tile starts at the next tile, one unit
+// later).  Threads first, first + step, ... of the caller take the k in turn.
 __device__ void WaveStarts(const WorklistArgs& w, int p, const uint32_t* gunits, uint32_t item0,
-                           uint32_t ua, uint32_t ub, uint32_t n, uint32_t first, uint32_t step) {
+                           uint32_t ua, uint32_t ub, uint32_t n, uint32_t c, uint32_t first,
+                           uint32_t step) {
   if (ua >= ub) return;
   const uint32_t chunk_tiles = w.chunk_tiles;
   const uint32_t chunks = LeafChunks(n, chunk_tiles);
+  const uint2 qt = LeafQueryTiles(c, w.narrow);
   const uint32_t wdiv = max(1u, gunits[kGroups]);
   const int g = int(min<uint64_t>(kGroups - 1, (uint64_t(kGroups) * ua) / wdiv));
   const uint32_t nw = uint32_t(w.grid - g + kGroups - 1) / kGroups;
@@ -1209,20 +1262,35 @@ __device__ void WaveStarts(const WorklistArgs& w, int p, const uint32_t* gunits,
     const uint32_t us = U0 + uint32_t((uint64_t(span) * k) / nw);
     if (us >= ub) break;
     const uint32_t ue = U0 + uint32_t((uint64_t(span) * (k + 1)) / nw);
-    const uint32_t off = us - ua, tq = off / tiles, rem = off % tiles;
+    const uint32_t off = us - ua;
+    uint32_t q, j, skip = 0;
+    if (off < 2u * tiles * qt.x) {   // in the 32-slot tiles (2 units each)
+      q = off / (2u * tiles);
+      const uint32_t ru = off - q * 2u * tiles;
+      j = (ru + 1u) / 2u;
+      skip = 2u * j - ru;
+      if (j == tiles) {   // (the leaf's next query tile, or the next leaf's first item)
+        ++q;
+        j = 0;
+      }
+    } else {                         // in the 16-slot tile
+      q = qt.x;
+      j = off - 2u * tiles * qt.x;
+    }
     uint32_t ch = 0;
-    while (ChunkTiles(n, chunk_tiles, ch).y <= rem) ++ch;
-    SMX_CHECK(item0 + tq * chunks + ch, w.bd.items, "wave start item");
+    if (q < qt.x + qt.y)
+      while (ChunkTiles(n, chunk_tiles, ch).y <= j) ++ch;
+    const uint32_t units = ue - us > skip ? ue - us - skip : 0u;
+    SMX_CHECK(item0 + q * chunks + ch, w.bd.items + 1, "wave start item");
     SMX_GUARD(kGroups * k + g, w.bd.grid, "wave start")
-    w.wave_start[kGroups * k + g] = make_uint4(item0 + tq * chunks + ch, rem, ue - us, uint32_t(p));
+    w.wave_start[kGroups * k + g] = make_uint4(item0 + q * chunks + ch, j, units, uint32_t(p));
   }
 }
 
-// Phase 2 (64 lanes per leaf position): the leaf's work items, the empty
-// query slots of its last query tile, and the start of every scan wave whose
-// share begins inside this leaf.  Wave i of group g (i % 8 == g) takes the
-// units [U0 + span * k / n, U0 + span * (k + 1) / n) of its group, k = i / 8
-// of the group's n waves.
+// Phase 2 (64 lanes per leaf position): the leaf's work items (the last
+// query tile's item marked narrow when it has 16 slots), the empty query
+// slots of its last query tile, and the start of every scan wave whose share
+// begins inside this leaf.
 // (item0 = the leaf's first item, [ua, ub) = its units, gunits = the 8
 // groups' unit boundaries)
 __device__ void ItemsCore(const WorklistArgs& w, int p, int lane, const uint32_t* gunits,
@@ -1241,12 +1309,13 @@ __device__ void ItemsCore(const WorklistArgs& w, int p, int lane, const uint32_t
   const uint32_t leaf = w.order[p];
   const uint32_t c = w.cnt[size_t(leaf) * kCounterStride], n = w.leaf_size[leaf];
   const uint32_t chunks = LeafChunks(n, chunk_tiles);
-  const uint32_t qt = (c + kQueriesPerTile - 1) / kQueriesPerTile;
+  const uint2 qts = LeafQueryTiles(c, w.narrow);
+  const uint32_t qt = qts.x + qts.y;
   const uint64_t toff = w.tile_off[leaf], moff = w.member_off[leaf];
   for (uint32_t u = lane; u < qt * chunks; u += 64) {
     const uint2 cr = ChunkTiles(n, chunk_tiles, u % chunks);
     WorkItem it;
-    it.leaf = leaf;
+    it.leaf = leaf | (u / chunks >= qts.x ? kItemNarrow : 0u);
     it.n = n;
     it.j0 = cr.x;
     it.jend = cr.y;
@@ -1255,8 +1324,9 @@ __device__ void ItemsCore(const WorklistArgs& w, int p, int lane, const uint32_t
     SMX_GUARD(item0 + u, w.bd.items, "work item") w.work[item0 + u] = it;
   }
   if (qt) {
-    const uint32_t first = c - (qt - 1) * kQueriesPerTile;   // empty slots [first, 32)
-    const uint32_t ne = kQueriesPerTile - first;
+    const uint32_t slots = qts.y ? uint32_t(kNarrowSlots) : uint32_t(kQueriesPerTile);
+    const uint32_t first = c - (qt - 1) * kQueriesPerTile;   // empty slots [first, slots)
+    const uint32_t ne = slots - first;
     for (uint32_t e = lane; e < ne * chunks; e += 64) {
       ItemLane v;
       v.qid = kNoQuery;
@@ -1267,7 +1337,7 @@ __device__ void ItemsCore(const WorklistArgs& w, int p, int lane, const uint32_t
       w.lanes[size_t(item0 + (qt - 1) * chunks + e / ne) * kQueriesPerTile + first + e % ne] = v;
     }
   }
-  WaveStarts(w, p, gunits, item0, ua, ub, n, uint32_t(lane), 64u);
+  WaveStarts(w, p, gunits, item0, ua, ub, n, c, uint32_t(lane), 64u);
 }
 
 __global__ void __launch_bounds__(64) items_kernel(WorklistArgs w) {
@@ -1289,7 +1359,7 @@ constexpr int kWlPosPerBlock = 4;
 __device__ void WorklistFusedBlock(const WorklistArgs& w, int b) {
   __shared__ uint32_t wsum[4], s_gunits[kGroups + 1], s_last_un[256];
   __shared__ uint32_t s_ex_i[kWlPosPerBlock], s_ex_u[kWlPosPerBlock + 1];
-  __shared__ unsigned long long red[4][2];
+  __shared__ unsigned long long red[4][3];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nl = w.nl, p0 = tid * kWlPerThread;
   const int pb = b * kWlPosPerBlock, pe = min(nl, pb + kWlPosPerBlock);
@@ -1297,16 +1367,17 @@ __device__ void WorklistFusedBlock(const WorklistArgs& w, int b) {
 #pragma unroll
   for (int k = 0; k < kWlPerThread; ++k) leafv[k] = p0 + k < nl ? w.order[p0 + k] : 0u;
   uint32_t ti = 0, tu = 0;
-  unsigned long long tp = 0, tb = 0;
+  unsigned long long tp = 0, tb = 0, tn = 0;
 #pragma unroll
   for (int k = 0; k < kWlPerThread; ++k) {
     itv[k] = unv[k] = 0;
     if (p0 + k < nl) {
       const uint32_t leaf = leafv[k];
       const uint32_t c = w.cnt[size_t(leaf) * kCounterStride], n = w.leaf_size[leaf];
-      unv[k] = LeafUnits(c, n, w.chunk_tiles, itv[k]);
+      unv[k] = LeafUnits(c, n, w.chunk_tiles, w.narrow, itv[k]);
       tp += c;
       tb += 16ull * w.nb * ((n + 31u) / 32u) * c;   // algorithmic code bytes
+      tn += LeafQueryTiles(c, w.narrow).y * ((n + 31u) / 32u);
     }
     ti += itv[k];
     tu += unv[k];
@@ -1317,9 +1388,9 @@ __device__ void WorklistFusedBlock(const WorklistArgs& w, int b) {
   const uint32_t inc_u = BlockInclusiveScan256(tu, wsum);
   const uint32_t total_w = wsum[0] + wsum[1] + wsum[2] + wsum[3];
   if (b == 0) {
-    unsigned long long v[2] = {tp, tb};
+    unsigned long long v[3] = {tp, tb, tn};
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < 3; ++k) {
       for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
       if (lane == 0) red[wid][k] = v[k];
     }
@@ -1329,6 +1400,7 @@ __device__ void WorklistFusedBlock(const WorklistArgs& w, int b) {
     w.totals[0] = uint32_t(red[0][0] + red[1][0] + red[2][0] + red[3][0]);
     w.totals[1] = inc_i;   // thread 255's inclusive item prefix = all items
     w.totals[2] = total_w;
+    w.totals[kTotalsTiles16] = uint32_t(red[0][2] + red[1][2] + red[2][2] + red[3][2]);
     w.code_bytes[0] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
   }
   const uint64_t wdiv = max(1u, total_w);
@@ -1472,100 +1544,22 @@ constexpr uint32_t kSeedCap = 256u * kSeedPerThread;
 constexpr int kSeedMaxLeaves = 64;   // one wave of leaf slots
 constexpr int kSeedSel = 1024;       // values under the minima bound ranked exactly
 
-// The threshold key of query qi from its seed leaves, or kNoThreshold (no
-// bound); block-wide (256 threads, all call; the value is returned to all).
-template <int K>
-__device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
-  constexpr int NW = ((((K + 1) / 2) + 3) / 4);
-  constexpr int W = 4 * NW;
-  constexpr int U = SMX_SEED_U;   // datapoints whose code loads are in flight together
-  constexpr int NB = (K + 1) / 2;   // code bytes per half holding steps < K
-  __shared__ __align__(16) int8_t lut[2 * K * 16];
-  // pair tables: ptab[h][j][byte] = the LUT sum of the two nibbles of code
-  // byte j of half h (blocks 4j + h and 4j + 2 + h): one LDS lookup per code
-  // byte instead of one per nibble
-  __shared__ int16_t ptab[2 * NB * 256];
+// The threshold key of a query from its seed distances (ordered bits, 16
+// per thread of a 256-thread block, 0xFFFFFFFF = none): the exact kk-th
+// smallest value v as (v << 32 | 0xFFFFFFFF), which admits every candidate
+// at that distance.  Block-wide (every thread calls; the key is returned to
+// all).  kk <= 256: the kk-th of the 256 per-thread minima bounds the kk-th
+// value from above (a subset's kk-th is never smaller); the few values under
+// it (~1.3 kk) are ranked exactly.  Otherwise (or when those overflow),
+// rounds of a linear 256-bin histogram narrow the value range down.
+__device__ uint64_t ThresholdOfVals(const uint32_t (&vals)[kSeedPerThread], uint32_t kk) {
   __shared__ uint64_t skey[kSeedSel];
   __shared__ uint32_t hist[256];
-  __shared__ uint32_t s_start[kSeedMaxLeaves + 1];
-  __shared__ uint64_t s_tile0[kSeedMaxLeaves];
-  __shared__ float s_bias[kSeedMaxLeaves];
   __shared__ uint32_t wsum[4], s_lo[4], s_hi[4], s_bin, s_below, s_thi, s_cnt;
   __shared__ uint64_t s_T;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  SMX_PHASE(1, qi, 0);
-  if (a.seed <= 0) return kNoThreshold;
-  static_assert(2 * K * 16 / 4 <= 256, "one LUT word per thread");
-  if (tid < 2 * K * 16 / 4)
-    reinterpret_cast<uint32_t*>(lut)[tid] =
-        reinterpret_cast<const uint32_t*>(a.lut + size_t(qi) * 2 * K * 16)[tid];
-  const float inv = a.inv[qi];
-  const int nseed = min(a.seed, min(a.L, kSeedMaxLeaves));
-  if (wid == 0) {
-    // seed leaves and the exclusive prefix of their sizes (lanes >= nseed add 0)
-    const int leaf = lane < nseed ? a.topl_leaf[size_t(qi) * a.L + lane] : -1;
-    const uint32_t sz = leaf >= 0 ? a.leaf_size[leaf] : 0u;
-    uint32_t inc = sz;
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t t = uint32_t(__shfl_up(int(inc), off));
-      if (lane >= off) inc += t;
-    }
-    s_start[lane] = inc - sz;
-    s_tile0[lane] = leaf >= 0 ? a.tile_off[leaf] : 0ull;
-    s_bias[lane] = (leaf >= 0 && a.residual) ? a.topl_dist[size_t(qi) * a.L + lane] : 0.0f;
-    if (lane == 63) s_start[kSeedMaxLeaves] = inc;
-  }
-  __syncthreads();
-  SMX_PHASE(1, qi, 1);
-  const uint32_t total = min(s_start[kSeedMaxLeaves], kSeedCap);
-  const uint32_t kk = uint32_t(a.kk);
-  if (kk == 0 || total < kk) return kNoThreshold;   // no bound: the threshold stays open
-#pragma unroll
-  for (int i = 0; i < 2 * NB; ++i) {
-    const int h = i / NB, j = i % NB, s0 = 2 * j, s1 = 2 * j + 1;
-    int v = lut[(2 * s0 + h) * 16 + CodePairLo(uint32_t(tid))];
-    if (s1 < K) v += lut[(2 * s1 + h) * 16 + CodePairHi(uint32_t(tid))];
-    ptab[i * 256 + tid] = int16_t(v);
-  }
   if (tid == 0) s_cnt = 0;
   __syncthreads();
-
-  uint32_t vals[kSeedPerThread];
-  int r = 0;   // seed leaf of this thread's current number (numbers only grow)
-#pragma unroll
-  for (int i0 = 0; i0 < kSeedPerThread; i0 += U) {
-    if (uint32_t(i0) * 256u < total) {   // block-uniform
-      uint32_t c0[U][NW], c1[U][NW];
-      int ru[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t g = min(uint32_t(tid) + 256u * uint32_t(i0 + u), total - 1);
-        while (g >= s_start[r + 1]) ++r;
-        ru[u] = r;
-        const uint32_t dp = g - s_start[r];
-        SMX_CHECK(s_tile0[r] + (dp >> 5), a.bd.tiles, "seed tile");
-        const uint8_t* t0 = a.tiles + ((s_tile0[r] + (dp >> 5)) * 64 + (dp & 31)) * W;
-        LoadCodes<K>(t0, c0[u]);
-        LoadCodes<K>(t0 + 32 * W, c1[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        int acc = 0;
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          const uint32_t b0 = (c0[u][j >> 2] >> (8 * (j & 3))) & 0xFFu;
-          const uint32_t b1 = (c1[u][j >> 2] >> (8 * (j & 3))) & 0xFFu;
-          acc += int(ptab[j * 256 + b0]) + int(ptab[(NB + j) * 256 + b1]);
-        }
-        const uint32_t g = uint32_t(tid) + 256u * uint32_t(i0 + u);
-        vals[i0 + u] = g < total ? OrderedBits(DistOf(acc, inv, s_bias[ru[u]])) : 0xFFFFFFFFu;
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < U; ++u) vals[i0 + u] = 0xFFFFFFFFu;   // no datapoint
-    }
-  }
-  SMX_PHASE(1, qi, 2);
   if (kk <= 256u) {
     // The kk-th smallest of the 256 per-thread minima bounds the kk-th value
     // from above (a subset's kk-th is never smaller); the few values under it
@@ -1594,7 +1588,6 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
         if (CountLess(skey, c, key) == kk - 1u) s_T = (key & 0xFFFFFFFF00000000ull) | 0xFFFFFFFFull;
       }
       __syncthreads();
-      SMX_PHASE(1, qi, 3);
       return s_T;
     }
   }
@@ -1645,8 +1638,101 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
   }
   if (tid == 0) s_T = (uint64_t(hi) << 32) | 0xFFFFFFFFull;
   __syncthreads();
-  SMX_PHASE(1, qi, 3);
   return s_T;
+}
+
+// The threshold key of query qi from its seed leaves, or kNoThreshold (no
+// bound); block-wide (256 threads, all call; the value is returned to all).
+template <int K>
+__device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
+  constexpr int NW = ((((K + 1) / 2) + 3) / 4);
+  constexpr int W = 4 * NW;
+  constexpr int U = SMX_SEED_U;   // datapoints whose code loads are in flight together
+  constexpr int NB = (K + 1) / 2;   // code bytes per half holding steps < K
+  __shared__ __align__(16) int8_t lut[2 * K * 16];
+  // pair tables: ptab[h][j][byte] = the LUT sum of the two nibbles of code
+  // byte j of half h (blocks 4j + h and 4j + 2 + h): one LDS lookup per code
+  // byte instead of one per nibble
+  __shared__ int16_t ptab[2 * NB * 256];
+  __shared__ uint32_t s_start[kSeedMaxLeaves + 1];
+  __shared__ uint64_t s_tile0[kSeedMaxLeaves];
+  __shared__ float s_bias[kSeedMaxLeaves];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  SMX_PHASE(1, qi, 0);
+  if (a.seed <= 0) return kNoThreshold;
+  static_assert(2 * K * 16 / 4 <= 256, "one LUT word per thread");
+  if (tid < 2 * K * 16 / 4)
+    reinterpret_cast<uint32_t*>(lut)[tid] =
+        reinterpret_cast<const uint32_t*>(a.lut + size_t(qi) * LutRows(K) * 16)[tid];
+  const float inv = a.inv[qi];
+  const int nseed = min(a.seed, min(a.L, kSeedMaxLeaves));
+  if (wid == 0) {
+    // seed leaves and the exclusive prefix of their sizes (lanes >= nseed add 0)
+    const int leaf = lane < nseed ? a.topl_leaf[size_t(qi) * a.L + lane] : -1;
+    const uint32_t sz = leaf >= 0 ? a.leaf_size[leaf] : 0u;
+    uint32_t inc = sz;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t t = uint32_t(__shfl_up(int(inc), off));
+      if (lane >= off) inc += t;
+    }
+    s_start[lane] = inc - sz;
+    s_tile0[lane] = leaf >= 0 ? a.tile_off[leaf] : 0ull;
+    s_bias[lane] = (leaf >= 0 && a.residual) ? a.topl_dist[size_t(qi) * a.L + lane] : 0.0f;
+    if (lane == 63) s_start[kSeedMaxLeaves] = inc;
+  }
+  __syncthreads();
+  SMX_PHASE(1, qi, 1);
+  const uint32_t total = min(s_start[kSeedMaxLeaves], kSeedCap);
+  const uint32_t kk = uint32_t(a.kk);
+  if (kk == 0 || total < kk) return kNoThreshold;   // no bound: the threshold stays open
+#pragma unroll
+  for (int i = 0; i < 2 * NB; ++i) {
+    const int h = i / NB, j = i % NB, s0 = 2 * j, s1 = 2 * j + 1;
+    int v = lut[(2 * s0 + h) * 16 + CodePairLo(uint32_t(tid))];
+    if (s1 < K) v += lut[(2 * s1 + h) * 16 + CodePairHi(uint32_t(tid))];
+    ptab[i * 256 + tid] = int16_t(v);
+  }
+  __syncthreads();
+
+  uint32_t vals[kSeedPerThread];
+  int r = 0;   // seed leaf of this thread's current number (numbers only grow)
+#pragma unroll
+  for (int i0 = 0; i0 < kSeedPerThread; i0 += U) {
+    if (uint32_t(i0) * 256u < total) {   // block-uniform
+      uint32_t c0[U][NW], c1[U][NW];
+      int ru[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t g = min(uint32_t(tid) + 256u * uint32_t(i0 + u), total - 1);
+        while (g >= s_start[r + 1]) ++r;
+        ru[u] = r;
+        const uint32_t dp = g - s_start[r];
+        SMX_CHECK(s_tile0[r] + (dp >> 5), a.bd.tiles, "seed tile");
+        const uint8_t* t0 = a.tiles + ((s_tile0[r] + (dp >> 5)) * 64 + (dp & 31)) * W;
+        LoadCodes<K>(t0, c0[u]);
+        LoadCodes<K>(t0 + 32 * W, c1[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        int acc = 0;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const uint32_t b0 = (c0[u][j >> 2] >> (8 * (j & 3))) & 0xFFu;
+          const uint32_t b1 = (c1[u][j >> 2] >> (8 * (j & 3))) & 0xFFu;
+          acc += int(ptab[j * 256 + b0]) + int(ptab[(NB + j) * 256 + b1]);
+        }
+        const uint32_t g = uint32_t(tid) + 256u * uint32_t(i0 + u);
+        vals[i0 + u] = g < total ? OrderedBits(DistOf(acc, inv, s_bias[ru[u]])) : 0xFFFFFFFFu;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) vals[i0 + u] = 0xFFFFFFFFu;   // no datapoint
+    }
+  }
+  SMX_PHASE(1, qi, 2);
+  const uint64_t T = ThresholdOfVals(vals, kk);
+  SMX_PHASE(1, qi, 3);
+  return T;
 }
 
 // Per query: its threshold key (SeedTau).
@@ -1669,9 +1755,18 @@ __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a, WorklistArgs 
 // (tree_ah_hybrid_residual.cc:610-622), with the slot's sum limit from the
 // query's seed threshold.  One thread per pair; runs after the seed pass and
 // the work list.
+__device__ __forceinline__ void PairScatterTau(const SeedArgs& a, size_t p,
+                                               const uint32_t* __restrict__ leaf_item0,
+                                               uint64_t tau);
 __device__ __forceinline__ void PairScatter(const SeedArgs& a, size_t p, int nq,
                                             const uint32_t* __restrict__ leaf_item0) {
   if (p >= size_t(nq) * a.L) return;
+  PairScatterTau(a, p, leaf_item0, a.tau_key[p / a.L]);
+}
+// pair p's records with its query's threshold key tau
+__device__ __forceinline__ void PairScatterTau(const SeedArgs& a, size_t p,
+                                               const uint32_t* __restrict__ leaf_item0,
+                                               uint64_t tau) {
   const int32_t leaf = a.topl_leaf[p];
   if (leaf < 0) return;
   const uint32_t qi = uint32_t(p / a.L);
@@ -1685,7 +1780,6 @@ __device__ __forceinline__ void PairScatter(const SeedArgs& a, size_t p, int nq,
   // the slot's sum limit: the largest LUT16 sum whose distance can pass the
   // query's threshold (d is monotone in the sum), so the scan's setup needs
   // neither the threshold nor a search
-  const uint64_t tau = a.tau_key[qi];
   v.amax = tau == kNoThreshold ? 128 * a.nb
                                : SumLimit(FromOrdered(uint32_t(tau >> 32)), v.inv, v.bias,
                                           -128 * a.nb, 128 * a.nb);
@@ -1721,6 +1815,9 @@ __global__ void __launch_bounds__(256) pair_scatter_kernel(SeedArgs a, int nq) {
 // position nibble (x0 & 3 in fields 0..7, x1 & 3 in fields 8..15), each
 // address two VALU ops; a 256-entry table of both spent 60% of the LDS
 // cycles in bank conflicts.
+#ifndef SMX_POS_B64
+#define SMX_POS_B64 0
+#endif
 template <int K, int R, bool NOLDS = false>
 __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)[K / 2],
                                            const v4i* grp_tab, const int* pos_tab) {
@@ -1754,15 +1851,17 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
       }
 #undef SMX_SDWA_OFFS
       o[slot] = *reinterpret_cast<const v4i*>(reinterpret_cast<const char*>(grp_tab) + og);
+#if SMX_POS_B64
       // the index word read as the low half of a ds_read_b64: its bank is
       // (a/4) mod 64, so the 16 entries 16 bytes apart sit on 16 distinct
       // bank pairs (a ds_read_b32 banks (a/4) mod 32: entries p and p + 8
-      // collided, 2.97M conflict cycles per launch).  The empty asm takes
-      // the high half as an input so that the load is not narrowed to b32.
+      // collide).  The entry's high half is 0 and or-ed in, so that the load
+      // is not narrowed to b32.
       const uint2 pw = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(pos_tab) + op);
-      int xw;
-      asm("; pos word %1" : "=v"(xw) : "v"(pw.y), "0"(pw.x));
-      ix[slot] = xw;
+      ix[slot] = int(pw.x | pw.y);
+#else
+      ix[slot] = *reinterpret_cast<const int*>(reinterpret_cast<const char*>(pos_tab) + op);
+#endif
     }
   };
 #pragma unroll
@@ -1787,11 +1886,83 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
   __builtin_amdgcn_sched_group_barrier(0x100, 2 * R, 0);
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
+    // the index word's v_or right before its MFMA (placed early, it waits for
+    // the step's LDS reads R steps too soon)
+    if (!NOLDS && SMX_POS_B64) __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
     if (s == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
     if (s + R < KS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
   }
   return acc;
+}
+
+// One tile of a 16-slot item: S[dp][q] for 32 datapoints x 16 queries on
+// v_smfmac_i32_16x16x128_i8, two accumulator chains (A: datapoints 0..15, B:
+// 16..31) of K16 = ceil(K / 4) steps of 8 AH blocks each.  Operand layout
+// (tools/smfmac16_probe.hip): A lane (r, gA = lane / 16) holds row r; its
+// compressed values j < 8 pair with B lanes of group 2 (gA & 1), j >= 8 with
+// group 2 (gA & 1) + 1, in bytes 16 (gA >> 1) + 4 ((j % 8) / 2) + idx_j of
+// those lanes; B lane (n, gB) holds column n, 32 bytes; D lane (n, g) holds
+// column n, rows 4 g + e.  So A lane group gA takes the code byte 2 s' +
+// (gA & 1) of the 32-slot tile layout's half gA >> 1 -- blocks x0 = 8 s' +
+// 4 (gA & 1) + (gA >> 1) and x0 + 2 -- and B lane group gB then needs LUT
+// rows 8 s' + 2 gB and 8 s' + 2 gB + 1: the 32 contiguous bytes the 32-slot
+// path reads at its step 2 s' + (gB >> 1), half gB & 1.  The code bytes are
+// the 32-slot layout's (no second copy of the codes): lane (r, gA) loads the
+// 16-byte lane records of rows r and r + 16 of half gA >> 1 (`ca`, `cb`),
+// shifted right by 8 (gA & 1) bits, so that step s' reads byte 2 (s' % 2) of
+// dword s' / 2.  The same operand tables as the 32-slot path.
+template <int K, int R>
+__device__ __forceinline__ void TileSmfmac16(const uint32_t* ca, const uint32_t* cb,
+                                             const v8i (&b)[(K + 3) / 4], const v4i* grp_tab,
+                                             const int* pos_tab, v4i& acc_a, v4i& acc_b) {
+  constexpr int K16 = (K + 3) / 4;
+  constexpr int NS = 2 * K16;   // MFMAs: steps x chains, A and B in turn
+  v4i o[R];
+  int ix[R];
+  auto ld = [&](int slot, int t) {
+    const int st = t >> 1;
+    const uint32_t w = (t & 1) ? cb[st >> 1] : ca[st >> 1];
+    uint32_t og, op;
+#define SMX_SDWA_OFFS16(B)                                                                      \
+  asm("v_lshlrev_b32_sdwa %0, 4, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD "        \
+      "src1_sel:BYTE_" #B "\n\tv_and_b32_sdwa %1, %3, %2 dst_sel:DWORD dst_unused:UNUSED_PAD "   \
+      "src0_sel:DWORD src1_sel:BYTE_" #B                                                         \
+      : "=&v"(og), "=&v"(op) : "v"(w), "v"(0xF0u))
+    if (st & 1) {
+      SMX_SDWA_OFFS16(2);
+    } else {
+      SMX_SDWA_OFFS16(0);
+    }
+#undef SMX_SDWA_OFFS16
+    o[slot] = *reinterpret_cast<const v4i*>(reinterpret_cast<const char*>(grp_tab) + og);
+    ix[slot] = *reinterpret_cast<const int*>(reinterpret_cast<const char*>(pos_tab) + op);
+  };
+#pragma unroll
+  for (int p = 0; p < R; ++p)
+    if (p < NS) ld(p, p);
+  long long z0, z1, z2, z3;
+  asm volatile("v_mov_b64 %0, 0" : "=v"(z0));
+  asm volatile("v_mov_b64 %0, 0" : "=v"(z1));
+  asm volatile("v_mov_b64 %0, 0" : "=v"(z2));
+  asm volatile("v_mov_b64 %0, 0" : "=v"(z3));
+  typedef long long v2l __attribute__((ext_vector_type(2)));
+  acc_a = __builtin_bit_cast(v4i, v2l{z0, z1});
+  acc_b = __builtin_bit_cast(v4i, v2l{z2, z3});
+#pragma unroll
+  for (int t = 0; t < NS; ++t) {
+    if (t & 1)
+      acc_b = __builtin_amdgcn_smfmac_i32_16x16x128_i8(o[t % R], b[t >> 1], acc_b, ix[t % R], 0, 0);
+    else
+      acc_a = __builtin_amdgcn_smfmac_i32_16x16x128_i8(o[t % R], b[t >> 1], acc_a, ix[t % R], 0, 0);
+    if (t + R < NS) ld(t % R, t + R);
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, 2 * R, 0);
+#pragma unroll
+  for (int t = 0; t < NS; ++t) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if (t + R < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1918,8 +2089,10 @@ __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32
   while (su > 0 && nseg + 64 <= uint32_t(kMaxSegs)) {
     const uint32_t idx = sw + uint32_t(lane);
     const WorkItem it = a.work[min(idx, a.num_items - 1)];
+    const uint32_t wt = (it.leaf & kItemNarrow) ? 1u : 2u;   // units per tile
     const uint32_t j0 = (lane == 0 && sj) ? sj : it.j0;
-    const uint32_t t = it.jend > j0 ? min(it.jend - j0, su) : 0u;
+    const uint32_t tt = it.jend > j0 ? it.jend - j0 : 0u;      // the item's tiles
+    const uint32_t t = min(tt * wt, su);                       // ... in units
     uint32_t incl = t;
     for (int off = 1; off < 64; off <<= 1) {
       const uint32_t y = uint32_t(__shfl_up(int(incl), off));
@@ -1927,19 +2100,20 @@ __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32
     }
     const uint32_t excl = incl - t;
     const bool used = excl < su;   // a prefix of the lanes, lane 0 always
-    const bool take = used && t > 0;
+    const bool take = used && tt > 0;
     if (take) SMX_CHECK(idx, a.bd.items, "listed item");
     const uint64_t bt = __ballot(take);
     if (take) {
       const uint32_t pos = nseg + uint32_t(__popcll(bt & ((1ull << lane) - 1ull)));
       s_item[pos] = idx;
       s_next[pos] = j0;
-      s_end[pos] = j0 + min(t, su - excl);
+      // the tiles whose first unit is inside the share
+      s_end[pos] = j0 + min(tt, (su - excl + wt - 1) / wt);
       SegDesc dsc;
       dsc.tile_off = it.tile_off;
       dsc.member_off = it.member_off;
       dsc.n = it.n;
-      dsc.leaf = it.leaf;
+      dsc.leaf = it.leaf;   // (with its kItemNarrow flag)
       dsc.slot0 = idx * uint32_t(kQueriesPerTile);
       dsc.nslots = kQueriesPerTile;
       s_desc[pos] = dsc;
@@ -1959,7 +2133,9 @@ __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32
   }
 }
 
-template <int K, int ABL = 0>
+// NRW: the work list may hold 16-slot items (the 16-slot path is compiled
+// in); without it only the 32-slot path exists (fewer registers and code).
+template <int K, int ABL = 0, bool NRW = false>
 __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(ScanArgs a) {
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
   constexpr int W = 4 * NW;
@@ -1990,6 +2166,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
     grp_tab[threadIdx.x] = t;
     // position nibble p0 | p1 << 2: p0 in index fields 0..7, p1 in 8..15
     pos_tab[4 * threadIdx.x] = int((threadIdx.x & 3u) * 0x5555u | ((threadIdx.x >> 2) * 0x5555u) << 16);
+    pos_tab[4 * threadIdx.x + 1] = 0;   // the high half of the ds_read_b64
   }
   const uint32_t worker = blockIdx.x * NWAVES + wv;
   // this workgroup's share: `units` tiles from tile jfirst of item w on
@@ -2099,13 +2276,16 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       // prefetched during the segment before (the claimed-ahead one), so
       // the B-fragment loads issue at once
       // (slot c of the item: record slot0 + c when c < nslots, else empty)
+      // (a 16-slot item: slot lane % 16, the column of the lane's B fragment)
       auto slot_rec = [&](uint32_t sgi) {
         const uint32_t s0 = __builtin_amdgcn_readfirstlane(s_desc[sgi].slot0);
         const uint32_t ns = __builtin_amdgcn_readfirstlane(s_desc[sgi].nslots);
+        const bool nr = (__builtin_amdgcn_readfirstlane(s_desc[sgi].leaf) & kItemNarrow) != 0;
+        const uint32_t cs = nr ? uint32_t(lane & 15) : uint32_t(c);
         ItemLane r;
-        if (uint32_t(c) < ns) {
-          SMX_CHECK(s0 + uint32_t(c), a.bd.recs, "slot record");
-          r = a.lanes[size_t(s0) + c];
+        if (cs < ns) {
+          SMX_CHECK(s0 + cs, a.bd.recs, "slot record");
+          r = a.lanes[size_t(s0) + cs];
         } else {
           r.qid = kNoQuery;
           r.bias = 0.0f;
@@ -2133,32 +2313,48 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       const uint64_t moff = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(sd.member_off >> 32))) << 32) |
                             __builtin_amdgcn_readfirstlane(uint32_t(sd.member_off));
       const uint32_t n = __builtin_amdgcn_readfirstlane(sd.n);
-      const int leaf = int(__builtin_amdgcn_readfirstlane(sd.leaf));
+      const uint32_t leaf_w = __builtin_amdgcn_readfirstlane(sd.leaf);
+      const int leaf = int(leaf_w & ~kItemNarrow);
       SMX_CHECK(qid == kNoQuery ? 0u : qid, a.bd.nq, "slot record query");
       SMX_CHECK(leaf, a.bd.nl, "segment leaf");
       SMX_CHECK(toff + (n + 31u) / 32u, a.bd.tiles + 1, "segment tiles");
       SMX_CHECK(moff + n, a.bd.members + 1, "segment members");
-      // this segment's B fragments (LUT rows 2s+h of query c) and first tile
-      v8i b[K / 2];
-      uint32_t codes[NW] = {};
+      // the segment's tiles, on the 32-slot or the 16-slot path (the item's
+      // kItemNarrow flag; wave-uniform)
+      uint32_t tiles_done = 0;
+      auto run_seg = [&](auto nr_tag) {
+      constexpr bool NR = decltype(nr_tag)::value;
+      constexpr int KB_STEPS = NR ? (K + 3) / 4 : K / 2;   // B fragments (steps)
+      // this segment's B fragments and first tile: 32-slot, LUT rows
+      // 4s + 2h, 4s + 2h + 1 of query c per sparse step; 16-slot, rows
+      // 8s' + 2gB, 8s' + 2gB + 1 of query n = lane % 16 (gB = lane / 16)
+      v8i b[KB_STEPS];
+      uint32_t codes[NW] = {}, codes_b[NW] = {};
       // addresses as a wave-uniform base + a 32-bit lane offset (saddr
-      // loads: no 64-bit per-lane pointers live across the tile loop)
+      // loads: no 64-bit per-lane pointers live across the tile loop); the
+      // 16-slot path reads rows r and r + 16 of half (lane / 32) of the tile
       const uint8_t* tseg = a.tiles + toff * 64ull * W;
+      const uint32_t lane_off =
+          NR ? uint32_t((lane >> 5) * 32 + (lane & 15)) * uint32_t(W) : uint32_t(lane) * uint32_t(W);
       auto tile_ptr = [&](uint32_t t) {
         if (ABL & 32) t = j;   // timing ablation: every tile's codes = the first one's (cache-hot)
-        return tseg + size_t(t * uint32_t(64 * W) + uint32_t(lane) * uint32_t(W));
+        return tseg + size_t(t * uint32_t(64 * W) + lane_off);
       };
-      // LUT rows 4s + 2h, 4s + 2h + 1 of query c (32 bytes) per sparse step
-      const uint32_t boff = (lq * uint32_t(K) + uint32_t(h)) * 32u;
+      const uint32_t boff = NR ? lq * uint32_t(LutRows(K) * 16) + uint32_t(lane >> 4) * 32u
+                               : lq * uint32_t(LutRows(K) * 16) + uint32_t(h) * 32u;
       const uint8_t* lutb = reinterpret_cast<const uint8_t*>(a.lut);
       auto load_b = [&]() {
         // one per-lane address, the steps as immediate offsets
         const v8i* bp = reinterpret_cast<const v8i*>(lutb + size_t(boff));
 #pragma unroll
-        for (int s2 = 0; s2 < K / 2; ++s2) b[s2] = bp[2 * s2];
+        for (int s2 = 0; s2 < KB_STEPS; ++s2) b[s2] = bp[(NR ? 4 : 2) * s2];
+      };
+      auto load_codes = [&](uint32_t t, uint32_t (&ca)[NW], uint32_t (&cbb)[NW]) {
+        LoadCodes<K>(tile_ptr(t), ca);
+        if constexpr (NR) LoadCodes<K>(tile_ptr(t) + 16 * W, cbb);
       };
       load_b();
-      LoadCodes<K>(tile_ptr(j), codes);
+      load_codes(j, codes, codes_b);
       // the claimed-ahead segment's item and query ids, for its setup
       {
         const uint32_t sn = __builtin_amdgcn_readfirstlane(sg_next);
@@ -2176,7 +2372,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       // the largest LUT16 sum whose distance can pass the query's threshold)
       const int amax = cl.amax;
       if (flush) flush_prev();
-      if (lane < Q) {
+      if (lane < Q) {   // (16-slot: lanes 16..31 repeat slots 0..15; never counted)
         QParam v;
         v.qid = qid;
         v.amax = amax;
@@ -2189,15 +2385,16 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       WaveLdsSync();
       uint32_t whits = 0;   // wave-uniform
 
-      // the hit list's elements (16 sums per hit) spread over the lanes,
-      // element e = 16 * hit + i on lane e % 64: per-element test, key, and
-      // a ballot-ranked append to the LDS stage (no returning atomic; the 16
+      // the hit list's elements (EPH sums per hit) spread over the lanes,
+      // element e = EPH * hit + i on lane e % 64: per-element test, key, and
+      // a ballot-ranked append to the LDS stage (no returning atomic; the
       // lanes of one hit read its meta and parameters as broadcasts).
       // sum <= amax implies key <= the threshold key: the scan's thresholds
       // are the seed's (ordered(d_k') << 32 | 0xFFFFFFFF) or none, and d is
       // monotone in the sum
+      constexpr uint32_t EPH = NR ? 8u : 16u;
       auto drain = [&]() {
-        const uint32_t total = whits * 16u;
+        const uint32_t total = whits * EPH;
         uint32_t kn = __builtin_amdgcn_readfirstlane(wl.s_kn[par]);
         for (uint32_t e0 = 0; e0 < total; e0 += 64) {
           const uint32_t e = e0 + uint32_t(lane);
@@ -2205,16 +2402,24 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
           uint64_t key = 0;
           int cc = 0;
           if (e < total) {
-            const uint32_t hidx = e >> 4, i = e & 15u;
+            const uint32_t hidx = NR ? e >> 3 : e >> 4, i = e & (EPH - 1u);
             const uint32_t meta = wl.hmeta[hidx];
-            cc = int(meta & 31u);
-            const uint32_t hh = (meta >> 5) & 1u, jj = meta >> 6;
+            const uint32_t jj = meta >> 6;
+            uint32_t dp;
+            if constexpr (NR) {
+              // lane (n, g): column n, rows 4 g + (i & 3) of chain i >> 2
+              cc = int(meta & 15u);
+              dp = jj * kDpPerTile + 16u * (i >> 2) + 4u * ((meta >> 4) & 3u) + (i & 3u);
+            } else {
+              cc = int(meta & 31u);
+              const uint32_t hh = (meta >> 5) & 1u;
+              dp = jj * kDpPerTile + (i & 3u) + 8u * (i >> 2) + 4u * hh;
+            }
             const uint32_t word = reinterpret_cast<const uint32_t*>(&wl.hsum[hidx][0])[i >> 1];
             const int sum = int(int16_t(uint16_t(word >> (16u * (i & 1u)))));
             const QParam pq = wl.qp[cc];
             if (sum <= pq.amax) {
               pass = true;
-              const uint32_t dp = jj * kDpPerTile + (i & 3u) + 8u * (i >> 2) + 4u * hh;
               const float d = DistOf(sum, pq.inv, pq.bias);
               const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp)
                                                : a.members[moff + dp];
@@ -2243,56 +2448,105 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         WaveLdsSync();   // the hit list is rewritten next
       };
 
-      // one tile: K MFMAs, then the hit test
-      auto tile = [&](const uint32_t (&cd)[NW], uint32_t jt) {
-        v16i acc = TileSmfmac<K, R, (ABL & 64) != 0>(cd, b, grp_tab, pos_tab);
-        if (ABL & 4) {
-          int x = acc[0];
-#pragma unroll
-          for (int i = 1; i < 16; ++i) x ^= acc[i];
-          if (x == 0x7fffffff) a.cand_count[0] = x;
-          return;
+      // a hit's lanes append their sums (packed int16) and tag to the list
+      auto append_hit = [&](bool hit, uint64_t hb, const uint32_t* pk, uint32_t jt) {
+        // whits <= 64 here and a tile adds at most 64: the list (128)
+        // always has room, so the sums are dead before any drain
+        const uint32_t nh = uint32_t(__popcll(hb));
+        if (hit) {
+          const uint32_t hs =
+              whits + __builtin_amdgcn_mbcnt_hi(uint32_t(hb >> 32),
+                                                __builtin_amdgcn_mbcnt_lo(uint32_t(hb), 0u));
+          wl.hsum[hs][0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+          if constexpr (!NR) wl.hsum[hs][1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+          wl.hmeta[hs] = (jt << 6) | uint32_t(lane);
         }
+        whits += nh;
+        if (ABL & 8) st_hits += nh;
+        // no wait for the writes: a wave's LDS instructions execute in
+        // order, so the drain's later reads see them (compiler barrier only)
+        asm volatile("" ::: "memory");
+      };
+
+      // one tile: the MFMAs, then the hit test
+      auto tile = [&](const uint32_t (&cd)[NW], const uint32_t (&cd_b)[NW], uint32_t jt) {
         const uint32_t rows_left = n - jt * kDpPerTile;
-        if (rows_left < uint32_t(kDpPerTile)) {  // last tile of the leaf
-          // row (i&3) + 8(i>>2) + 4h >= rows_left, against one per-tile value
-          // (16 hoisted row numbers would cost 16 registers for the loop)
-          const int lim = int(rows_left) - 4 * h;
+        if constexpr (NR) {
+          // this lane's byte of each step at byte 2 (s' % 2) of dword s' / 2
+          const uint32_t sh = uint32_t((lane >> 4) & 1) * 8u;
+          uint32_t sa[NW], sb[NW];
 #pragma unroll
-          for (int i = 0; i < 16; ++i)
-            if ((i & 3) + 8 * (i >> 2) >= lim) acc[i] = 0x7FFF;
-        }
-        int m = min(min(acc[0], acc[1]), acc[2]);
+          for (int i = 0; i < NW; ++i) {
+            sa[i] = cd[i] >> sh;
+            sb[i] = cd_b[i] >> sh;
+          }
+          v4i acc_a, acc_b;
+          TileSmfmac16<K, R>(sa, sb, b, grp_tab, pos_tab, acc_a, acc_b);
+          if (ABL & 4) {
+            int x = acc_a[0] ^ acc_b[0];
 #pragma unroll
-        for (int i = 3; i < 15; i += 2) m = min(min(m, acc[i]), acc[i + 1]);
-        m = min(m, acc[15]);
-        const bool hit = m <= amax;
-        const uint64_t hb = __builtin_amdgcn_ballot_w64(hit);
-        if (ABL & 2) {   // timing ablation: the hit test without its list
-          if (hb == 0x1234567ull) a.cand_count[0] = 1u;
-          return;
-        }
-        if (hb) {
-          // whits <= 64 here and a tile adds at most 64: the list (128)
-          // always has room, so the sums are dead before any drain
-          const uint32_t nh = uint32_t(__popcll(hb));
-          if (hit) {
-            const uint32_t hs =
-                whits + __builtin_amdgcn_mbcnt_hi(uint32_t(hb >> 32),
-                                                  __builtin_amdgcn_mbcnt_lo(uint32_t(hb), 0u));
+            for (int i = 1; i < 4; ++i) x ^= acc_a[i] ^ acc_b[i];
+            if (x == 0x7fffffff) a.cand_count[0] = x;
+            return;
+          }
+          if (rows_left < uint32_t(kDpPerTile)) {  // last tile of the leaf
+            const int lim = int(rows_left) - 4 * (lane >> 4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              if (i >= lim) acc_a[i] = 0x7FFF;
+              if (16 + i >= lim) acc_b[i] = 0x7FFF;
+            }
+          }
+          const int m = min(min(min(acc_a[0], acc_a[1]), min(acc_a[2], acc_a[3])),
+                            min(min(acc_b[0], acc_b[1]), min(acc_b[2], acc_b[3])));
+          const bool hit = m <= amax;
+          const uint64_t hb = __builtin_amdgcn_ballot_w64(hit);
+          if (ABL & 2) {
+            if (hb == 0x1234567ull) a.cand_count[0] = 1u;
+            return;
+          }
+          if (hb) {
+            uint32_t pk[4];
+            pk[0] = (uint32_t(acc_a[0]) & 0xFFFFu) | (uint32_t(acc_a[1]) << 16);
+            pk[1] = (uint32_t(acc_a[2]) & 0xFFFFu) | (uint32_t(acc_a[3]) << 16);
+            pk[2] = (uint32_t(acc_b[0]) & 0xFFFFu) | (uint32_t(acc_b[1]) << 16);
+            pk[3] = (uint32_t(acc_b[2]) & 0xFFFFu) | (uint32_t(acc_b[3]) << 16);
+            append_hit(hit, hb, pk, jt);
+          }
+        } else {
+          v16i acc = TileSmfmac<K, R, (ABL & 64) != 0>(cd, b, grp_tab, pos_tab);
+          if (ABL & 4) {
+            int x = acc[0];
+#pragma unroll
+            for (int i = 1; i < 16; ++i) x ^= acc[i];
+            if (x == 0x7fffffff) a.cand_count[0] = x;
+            return;
+          }
+          if (rows_left < uint32_t(kDpPerTile)) {  // last tile of the leaf
+            // row (i&3) + 8(i>>2) + 4h >= rows_left, against one per-tile value
+            // (16 hoisted row numbers would cost 16 registers for the loop)
+            const int lim = int(rows_left) - 4 * h;
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if ((i & 3) + 8 * (i >> 2) >= lim) acc[i] = 0x7FFF;
+          }
+          int m = min(min(acc[0], acc[1]), acc[2]);
+#pragma unroll
+          for (int i = 3; i < 15; i += 2) m = min(min(m, acc[i]), acc[i + 1]);
+          m = min(m, acc[15]);
+          const bool hit = m <= amax;
+          const uint64_t hb = __builtin_amdgcn_ballot_w64(hit);
+          if (ABL & 2) {   // timing ablation: the hit test without its list
+            if (hb == 0x1234567ull) a.cand_count[0] = 1u;
+            return;
+          }
+          if (hb) {
             uint32_t pk[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k)
               pk[k] = (uint32_t(acc[2 * k]) & 0xFFFFu) | (uint32_t(acc[2 * k + 1]) << 16);
-            wl.hsum[hs][0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-            wl.hsum[hs][1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
-            wl.hmeta[hs] = (jt << 6) | uint32_t(lane);
+            append_hit(hit, hb, pk, jt);
           }
-          whits += nh;
-          if (ABL & 8) st_hits += nh;
-          // no wait for the writes: a wave's LDS instructions execute in
-          // order, so the drain's later reads see them (compiler barrier only)
-          asm volatile("" ::: "memory");
         }
       };
       // a hit list over half full is drained between tiles with the B
@@ -2335,17 +2589,16 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
           na_known = false;
         }
       };
-      uint32_t tiles_done = 0;
       {
-        uint32_t cb[NW];
+        uint32_t cb[NW], cb_b[NW];
         uint32_t t = j, tn = 0;
         for (;;) {
           bool more = next_tile(t, tn);
           // unconditional (the current tile again when none follows): one
           // load per tile on every path, so the wait for this tile's codes
           // leaves the next tile's load in flight (vmcnt(1), not vmcnt(0))
-          LoadCodes<K>(tile_ptr(more ? tn : t), cb);
-          tile(codes, t);
+          load_codes(more ? tn : t, cb, cb_b);
+          tile(codes, codes_b, t);
           ++tiles_done;
           if (pending) copy_prev();   // after the segment's first tile: the atomic has returned
           if (!more) break;
@@ -2353,8 +2606,8 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
           advance(t, tn);
           t = tn;
           more = next_tile(t, tn);
-          LoadCodes<K>(tile_ptr(more ? tn : t), codes);
-          tile(cb, t);
+          load_codes(more ? tn : t, codes, codes_b);
+          tile(cb, cb_b, t);
           ++tiles_done;
           if (!more) break;
           drain_mid();
@@ -2365,6 +2618,15 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       if (whits) {
         drain();
         whits = 0;
+      }
+      };
+      if constexpr (NRW) {
+        if (leaf_w & kItemNarrow)
+          run_seg(std::true_type{});
+        else
+          run_seg(std::false_type{});
+      } else {
+        run_seg(std::false_type{});
       }
       if (ABL & 8) st_t2 = __builtin_amdgcn_s_memtime();
       if (ABL & 8) {
@@ -2382,6 +2644,144 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
     if (flush) flush_prev();
     if (pending) copy_prev();
   }
+}
+
+// ---------------------------------------------------------------------------
+// The seed scan: every query's threshold from its first `seed` leaves on the
+// 16-slot MFMA path instead of per-query LDS lookups.  The top-L kernel has
+// listed, per leaf, the queries it seeds (SeedClaims: at most kSeedSlots);
+// one wave per leaf runs its first SeedLeafCap(seed) datapoints for those
+// queries, 16 at a time, and stores every (query, datapoint) distance as
+// ordered bits at seed_keys[q][i * cap + dp] (i = the leaf's seed index in
+// q's top-L).  The same distances as the scan (d = fl(fl(S inv) + bias)),
+// so the kk-th of them bounds the final kk-th from above.  Blocks from
+// `seed_blocks` on build the work list (WorklistFusedBlock), as the per-query
+// seed launch does.
+// ---------------------------------------------------------------------------
+template <int K>
+__global__ void __launch_bounds__(256) seed_scan_kernel(SeedArgs a, WorklistArgs w,
+                                                        int seed_blocks) {
+  if (int(blockIdx.x) >= seed_blocks) {   // the fused work-list blocks
+    WorklistFusedBlock(w, int(blockIdx.x) - seed_blocks);
+    return;
+  }
+  constexpr int NW = ((((K + 1) / 2) + 3) / 4);
+  constexpr int W = 4 * NW;
+  constexpr int K16 = (K + 3) / 4;
+  __shared__ __align__(256) v4i opnd_tab[32];
+  v4i* const grp_tab = opnd_tab;
+  int* const pos_tab = reinterpret_cast<int*>(opnd_tab + 16);
+  if (threadIdx.x < 16) {   // the scan's operand tables (lut16_scan_kernel)
+    const uint32_t g0 = threadIdx.x & 3u, g1 = threadIdx.x >> 2;
+    v4i t = {0, 0, 0, 0};
+    t[g0 >> 1] = int(1u << (16 * (g0 & 1u)));
+    t[2 + (g1 >> 1)] = int(1u << (16 * (g1 & 1u)));
+    grp_tab[threadIdx.x] = t;
+    pos_tab[4 * threadIdx.x] = int((threadIdx.x & 3u) * 0x5555u | ((threadIdx.x >> 2) * 0x5555u) << 16);
+    pos_tab[4 * threadIdx.x + 1] = 0;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int leaf = int(blockIdx.x) * 4 + int(threadIdx.x >> 6);
+  if (leaf >= a.nl) return;
+  const uint32_t cnt = min(a.seed_count[size_t(leaf) * kCounterStride], uint32_t(kSeedSlots));
+  if (cnt == 0) return;
+  const uint32_t cap = uint32_t(SeedLeafCap(a.seed));
+  const uint32_t n = min(a.leaf_size[leaf], cap);
+  const uint32_t tiles = (n + 31u) / 32u;
+  const uint8_t* tseg = a.tiles + a.tile_off[leaf] * 64ull * W;
+  const uint32_t lane_off = uint32_t((lane >> 5) * 32 + (lane & 15)) * uint32_t(W);
+  const uint32_t sh = uint32_t((lane >> 4) & 1) * 8u;
+  const uint32_t rg = uint32_t(lane >> 4);   // D rows 4 rg + e of column lane % 16
+  for (uint32_t g = 0; g < cnt; g += 16) {
+    const uint32_t sl = g + uint32_t(lane & 15);
+    const bool valid = sl < cnt;
+    const uint32_t rec = valid ? a.seed_list[size_t(leaf) * kSeedSlots + sl] : 0u;
+    const uint32_t qi = rec & 0xFFFFFFu, si = rec >> 24;
+    const float bias = (valid && a.residual) ? a.topl_dist[size_t(qi) * a.L + si] : 0.0f;
+    const float inv = a.inv[qi];
+    uint32_t* out = a.seed_keys + size_t(qi) * kSeedKeys + si * cap;
+    v8i b[K16];
+    const v8i* bp = reinterpret_cast<const v8i*>(reinterpret_cast<const uint8_t*>(a.lut) +
+                                                  size_t(qi) * (LutRows(K) * 16) +
+                                                  uint32_t(lane >> 4) * 32u);
+#pragma unroll
+    for (int s2 = 0; s2 < K16; ++s2) b[s2] = bp[4 * s2];
+    for (uint32_t t = 0; t < tiles; ++t) {
+      uint32_t ca[NW], cb[NW];
+      const uint8_t* tp = tseg + size_t(t) * (64 * W) + lane_off;
+      LoadCodes<K>(tp, ca);
+      LoadCodes<K>(tp + 16 * W, cb);
+#pragma unroll
+      for (int i = 0; i < NW; ++i) {
+        ca[i] >>= sh;
+        cb[i] >>= sh;
+      }
+      v4i acc_a, acc_b;
+      TileSmfmac16<K, 3>(ca, cb, b, grp_tab, pos_tab, acc_a, acc_b);
+      if (valid) {
+        // datapoints 32 t + 16 c + 4 rg + e of chain c: 4 contiguous keys each
+        const uint32_t d0 = t * 32u + 4u * rg;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const v4i& acc = c ? acc_b : acc_a;
+          const uint32_t dp = d0 + 16u * uint32_t(c);
+          uint32_t k4[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) k4[e] = OrderedBits(DistOf(acc[e], inv, bias));
+          if (dp + 3u < n) {
+            *reinterpret_cast<uint4*>(out + dp) = make_uint4(k4[0], k4[1], k4[2], k4[3]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (dp + uint32_t(e) < n) out[dp + e] = k4[e];
+          }
+        }
+      }
+    }
+  }
+}
+
+// Per query (one 256-thread block): its threshold key from the seed scan's
+// distances (the granted seed leaves' first min(size, cap) keys), then every
+// one of its (query, leaf) pairs into the scan's work items with its sum
+// limit -- the pair scatter of the per-query path, one launch for both.
+__global__ void __launch_bounds__(256) seed_select_kernel(SeedArgs a) {
+  const int qi = int(blockIdx.x);
+  const int tid = threadIdx.x;
+  const uint32_t cap = uint32_t(SeedLeafCap(a.seed));
+  const int nseed = min(a.seed, min(a.L, kSeedMaxMfma));
+  const uint32_t mask = a.seed_mask[qi];
+  __shared__ uint32_t s_cnt[kSeedMaxMfma];
+  if (tid < nseed) {
+    uint32_t c = 0;
+    if ((mask >> tid) & 1u) {
+      const int32_t leaf = a.topl_leaf[size_t(qi) * a.L + tid];
+      c = leaf >= 0 ? min(a.leaf_size[leaf], cap) : 0u;
+    }
+    s_cnt[tid] = c;
+  }
+  __syncthreads();
+  uint32_t total = 0;
+  for (int i = 0; i < nseed; ++i) total += s_cnt[i];
+  uint64_t T = kNoThreshold;
+  const uint32_t kk = uint32_t(a.kk);
+  if (kk > 0 && total >= kk) {   // (block-uniform)
+    const uint32_t* keys = a.seed_keys + size_t(qi) * kSeedKeys;
+    const uint32_t span = uint32_t(nseed) * cap;   // <= kSeedKeys
+    uint32_t vals[kSeedPerThread];
+#pragma unroll
+    for (int k = 0; k < kSeedPerThread; ++k) {
+      const uint32_t idx = uint32_t(tid) + 256u * uint32_t(k);
+      const uint32_t i = idx / cap, dp = idx - i * cap;
+      const bool ok = idx < span && dp < s_cnt[min(i, uint32_t(kSeedMaxMfma - 1))];
+      vals[k] = ok ? keys[idx] : 0xFFFFFFFFu;
+    }
+    T = ThresholdOfVals(vals, kk);
+  }
+  if (tid == 0) a.tau_key[qi] = T;
+  for (int i = tid; i < a.L; i += 256)
+    PairScatterTau(a, size_t(qi) * a.L + size_t(i), a.leaf_item0, T);
 }
 
 // One-query variant for the stage entry point: raw sums of one leaf.
@@ -2468,7 +2868,8 @@ __device__ __forceinline__ uint32_t RescanQuery(const RescanArgs& a, int qi, uin
   const int K = a.ksteps, NB = (K + 1) / 2, NW = (NB + 3) / 4, W = 4 * NW;
   if (tid == 0) atomicAdd(&a.stats[10], 1u);
   for (int e = tid; e < 2 * K * 16 / 4; e += 256)
-    reinterpret_cast<uint32_t*>(lut)[e] = reinterpret_cast<const uint32_t*>(a.lut + size_t(qi) * 2 * K * 16)[e];
+    reinterpret_cast<uint32_t*>(lut)[e] =
+        reinterpret_cast<const uint32_t*>(a.lut + size_t(qi) * LutRows(K) * 16)[e];
   __syncthreads();
   for (int i = 0; i < 2 * NB; ++i) {
     const int h = i / NB, j = i % NB, s0 = 2 * j, s1 = 2 * j + 1;
@@ -3259,7 +3660,11 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   static const int dbg = [] { const char* e = std::getenv("SMX_DBG_FRONT"); return e ? std::atoi(e) : 0; }();
   tail.leaf_count = (dbg & 1) ? nullptr : f.leaf_count;
   tail.rank = f.rank;
-  tail.lut = LutParams{queries, ix.dim, ix.codebook, ix.nb, ix.dpb, 2 * ix.ksteps, ix.metric,
+  tail.seed_count = f.seed_count;
+  tail.seed_list = f.seed_list;
+  tail.seed_mask = f.seed_mask;
+  tail.seed = f.seed;
+  tail.lut = LutParams{queries, ix.dim, ix.codebook, ix.nb, ix.dpb, LutRows(ix.ksteps), ix.metric,
                        ix.residual, (dbg & 2) ? nullptr : f.lut, f.mult, f.inv, nullptr};
   if (f.one_to_many) {
     const size_t n = size_t(nq) * ix.nl;
@@ -3313,7 +3718,7 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
 hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq, int8_t* lut,
                           float* mult, float* inv, uint8_t* lut_u8, hipStream_t s) {
   if (nq == 0) return hipSuccess;
-  const LutParams p{queries, ix.dim, ix.codebook, ix.nb, ix.dpb, 2 * ix.ksteps, ix.metric,
+  const LutParams p{queries, ix.dim, ix.codebook, ix.nb, ix.dpb, LutRows(ix.ksteps), ix.metric,
                     ix.residual, lut, mult, inv, lut_u8};
   hipLaunchKernelGGL(lut_build_kernel, dim3(nq), dim3(256), 0, s, p);
   return hipGetLastError();
@@ -3323,7 +3728,7 @@ WorklistArgs MakeWorklistArgs(const DeviceIndex& ix, const uint32_t* leaf_count,
                               uint32_t* leaf_item0, uint32_t* pos_unit0, uint32_t* gunits,
                               ItemLane* lanes, uint4* wave_start, int grid, uint32_t* totals,
                               unsigned long long* code_bytes, uint32_t chunk_tiles,
-                              const Bounds& bd) {
+                              uint32_t narrow, const Bounds& bd) {
   WorklistArgs w;
   w.bd = bd;
   w.cnt = leaf_count;
@@ -3335,6 +3740,7 @@ WorklistArgs MakeWorklistArgs(const DeviceIndex& ix, const uint32_t* leaf_count,
   w.nb = ix.nb;
   w.chunk_tiles = chunk_tiles;
   w.grid = grid;
+  w.narrow = narrow;
   w.leaf_item0 = leaf_item0;
   w.pos_unit0 = pos_unit0;
   w.gunits = gunits;
@@ -3349,18 +3755,18 @@ WorklistArgs MakeWorklistArgs(const DeviceIndex& ix, const uint32_t* leaf_count,
 hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, WorkItem* work,
                           uint32_t* leaf_item0, uint32_t* pos_unit0, uint32_t* gunits,
                           ItemLane* lanes, uint4* wave_start, int grid, uint32_t* totals,
-                          unsigned long long* code_bytes, uint32_t chunk_tiles,
+                          unsigned long long* code_bytes, uint32_t chunk_tiles, uint32_t narrow,
                           unsigned long long* part, const Bounds& bd, hipStream_t s) {
   const int nblk = (ix.nl + 255) / 256;   // (worklist_kernel loops over any count)
   WorklistPart* wp = reinterpret_cast<WorklistPart*>(part);
   hipLaunchKernelGGL(worklist_part_kernel, dim3(nblk), dim3(256), 0, s, leaf_count, ix.leaf_order,
-                     ix.leaf_size, ix.nl, ix.nb, chunk_tiles, wp);
+                     ix.leaf_size, ix.nl, ix.nb, chunk_tiles, narrow, wp);
   hipLaunchKernelGGL(worklist_kernel, dim3(nblk), dim3(256), 0, s, leaf_count, ix.leaf_order,
-                     ix.leaf_size, ix.nl, ix.nb, chunk_tiles, wp, leaf_item0, pos_unit0, gunits,
-                     totals, code_bytes);
+                     ix.leaf_size, ix.nl, ix.nb, chunk_tiles, narrow, wp, leaf_item0, pos_unit0,
+                     gunits, totals, code_bytes);
   const WorklistArgs w = MakeWorklistArgs(ix, leaf_count, work, leaf_item0, pos_unit0, gunits,
                                           lanes, wave_start, grid, totals, code_bytes, chunk_tiles,
-                                          bd);
+                                          narrow, bd);
   hipLaunchKernelGGL(items_kernel, dim3(ix.nl), dim3(64), 0, s, w);
   return hipGetLastError();
 }
@@ -3392,6 +3798,9 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
     else if (variant == 68)                                                                \
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 68>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
                          0, s, a);                                                         \
+    else if (narrow)                                                                       \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, true>), dim3(grid),                     \
+                         dim3(64 * ScanWaves<KV>()), 0, s, a);                             \
     else                                                                                   \
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
                          0, s, a);                                                         \
@@ -3400,13 +3809,17 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
 #define SMX_SCAN_CASE(KV)                                                                  \
   case KV:                                                                                 \
     if (variant != 0) return hipErrorInvalidValue;                                         \
-    hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()),  \
-                       0, s, a);                                                           \
+    if (narrow)                                                                            \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, true>), dim3(grid),                     \
+                         dim3(64 * ScanWaves<KV>()), 0, s, a);                             \
+    else                                                                                   \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
+                         0, s, a);                                                         \
     break;
 #endif
 
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,
-                      hipStream_t s) {
+                      hipStream_t s, bool narrow) {
   switch (ix.ksteps) {
     SMX_SCAN_CASE(4)
     SMX_SCAN_CASE(8)
@@ -3502,6 +3915,42 @@ hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStrea
     default:
       return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+#define SMX_SEED_SCAN_CASE(KV)                                                              \
+  case KV:                                                                                 \
+    hipLaunchKernelGGL(seed_scan_kernel<KV>, dim3(sb + nwl), dim3(256), 0, s, a,            \
+                       wl ? *wl : WorklistArgs{}, sb);                                      \
+    break;
+
+hipError_t LaunchSeedScan(const DeviceIndex& ix, const SeedArgs& a, hipStream_t s,
+                          const WorklistArgs* wl) {
+  static_assert(256 * kSeedPerThread == kSeedKeys, "the seed select holds kSeedKeys values");
+  if (wl && wl->nl > kFusedWorklistLeaves) return hipErrorInvalidValue;
+  if (a.seed < 1 || a.seed > kSeedMaxMfma) return hipErrorInvalidValue;
+  const int sb = (ix.nl + 3) / 4;   // one wave per leaf
+  const int nwl = wl ? (wl->nl + kWlPosPerBlock - 1) / kWlPosPerBlock : 0;
+  switch (ix.ksteps) {
+    SMX_SEED_SCAN_CASE(4)
+    SMX_SEED_SCAN_CASE(8)
+    SMX_SEED_SCAN_CASE(12)
+    SMX_SEED_SCAN_CASE(16)
+    SMX_SEED_SCAN_CASE(20)
+    SMX_SEED_SCAN_CASE(24)
+    SMX_SEED_SCAN_CASE(26)
+    SMX_SEED_SCAN_CASE(28)
+    SMX_SEED_SCAN_CASE(32)
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+#undef SMX_SEED_SCAN_CASE
+
+hipError_t LaunchSeedSelect(const SeedArgs& a, int nq, hipStream_t s) {
+  if (nq == 0) return hipSuccess;
+  hipLaunchKernelGGL(seed_select_kernel, dim3(nq), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -76,11 +76,13 @@ int EffectiveKSteps(int nb) {
 
 // Per-call counters (one buffer, zeroed by the partition kernel):
 //   [0, nl)            pairs per leaf
+//   [nl, 2 nl)         seeding queries per leaf (the seed scan's claims)
 //   [stats, +32)       stats words (SelectArgs::overflow and the work-list totals)
 struct CounterLayout {
-  uint32_t stats, words;
+  uint32_t seeds, stats, words;
   explicit CounterLayout(int nl) {
-    stats = uint32_t(nl) * smx::kCounterStride;   // nl strided leaf counters first
+    seeds = uint32_t(nl) * smx::kCounterStride;       // nl strided leaf counters first
+    stats = 2u * uint32_t(nl) * smx::kCounterStride;  // then the seed counters
     words = stats + 32u;
   }
 };
@@ -102,6 +104,9 @@ struct Workspace {
   float* mult = nullptr;
   float* inv = nullptr;
   uint32_t* counters = nullptr;     // see CounterLayout
+  uint32_t* seed_list = nullptr;    // [nl][kSeedSlots] the leaves' seeding queries
+  uint32_t* seed_mask = nullptr;    // [nq] granted seed leaves per query
+  uint32_t* seed_keys = nullptr;    // [nq][kSeedKeys] seed distances
   uint32_t* rank = nullptr;         // [nq*L] each pair's position in its leaf's list
   uint32_t* leaf_item0 = nullptr;   // [nl] each leaf's first work item
   smx::WorkItem* work = nullptr;    // [max_items]
@@ -109,7 +114,7 @@ struct Workspace {
   uint4* wave_start = nullptr;      // [grid] each scan wave's static share
   uint32_t* pos_unit0 = nullptr;    // [nl+1] work units before each leaf (work order)
   uint32_t* gunits = nullptr;       // [16] the XCD groups' unit boundaries
-  unsigned long long* wl_part = nullptr;   // [4 * ceil(nl / 256)] work-list block sums
+  unsigned long long* wl_part = nullptr;   // [kWorklistPartWords * ceil(nl / 256)] block sums
   uint64_t* tau = nullptr;          // [nq]
   uint64_t* cand = nullptr;         // [nq][cap]
   uint32_t* cand_count = nullptr;   // [nq] strided (kCounterStride)
@@ -120,7 +125,7 @@ struct Workspace {
   void Release() {
     DFree(queries); DFree(topl_leaf); DFree(topl_dist); DFree(scores); DFree(lut); DFree(mult);
     DFree(inv);
-    DFree(counters); DFree(rank); DFree(leaf_item0); DFree(lanes); DFree(wave_start);
+    DFree(counters); DFree(seed_list); DFree(seed_mask); DFree(seed_keys); DFree(rank); DFree(leaf_item0); DFree(lanes); DFree(wave_start);
     DFree(pos_unit0); DFree(gunits); DFree(wl_part);
     DFree(work); DFree(tau); DFree(cand); DFree(cand_count); DFree(out_idx);
     DFree(out_dist);
@@ -144,6 +149,13 @@ struct smx_index {
   int scan_variant = 0;            // see smx::LaunchScan
   int fused_worklist_leaves = smx::kFusedWorklistLeaves;   // 0: always the side stream
   uint32_t chunk_tiles = 20;       // tiles per work item (tools/tune.py: 16-20 best at glove)
+  // a leaf's remainder of <= 16 queries on the 16-slot scan path
+  // (v_smfmac_i32_16x16x128_i8); SMX_NARROW=0 keeps every query tile 32 wide
+  bool narrow_tiles = true;
+  // SMX_SEED_MFMA=1: the per-query thresholds by the seed scan (MFMA,
+  // seed_scan_kernel + seed_select_kernel) instead of the per-query
+  // LDS-lookup kernel (measured slower at glove shape: 0.180 vs 0.164 ms)
+  bool seed_mfma = false;
   int grid = 0;                    // scan grid: resident one-wave workgroups (occupancy API)
   bool profiling = false;
   bool use_graph = false;          // SMX_GRAPH=1: replay the pipeline as a hipGraph
@@ -406,13 +418,16 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
   int rc;
   if ((rc = DAlloc(&w.queries, size_t(anq) * ix.dim)) || (rc = DAlloc(&w.topl_leaf, apairs)) ||
       (rc = DAlloc(&w.topl_dist, apairs)) || (rc = DAlloc(&w.scores, size_t(anq) * nl)) ||
-      (rc = DAlloc(&w.lut, size_t(anq) * 2 * ix.ksteps * 16)) || (rc = DAlloc(&w.mult, anq)) ||
+      (rc = DAlloc(&w.lut, size_t(anq) * smx::LutRows(ix.ksteps) * 16)) || (rc = DAlloc(&w.mult, anq)) ||
       (rc = DAlloc(&w.inv, anq)) || (rc = DAlloc(&w.counters, CounterLayout(nl).words)) ||
+      (rc = DAlloc(&w.seed_list, size_t(nl) * smx::kSeedSlots)) ||
+      (rc = DAlloc(&w.seed_mask, size_t(anq))) ||
+      (rc = DAlloc(&w.seed_keys, size_t(anq) * smx::kSeedKeys)) ||
       (rc = DAlloc(&w.rank, apairs)) || (rc = DAlloc(&w.leaf_item0, size_t(nl))) ||
       (rc = DAlloc(&w.lanes, size_t(max_items) * smx::kQueriesPerTile)) ||
       (rc = DAlloc(&w.wave_start, size_t(std::max(h->grid, 1)))) ||
       (rc = DAlloc(&w.pos_unit0, size_t(nl + 1))) || (rc = DAlloc(&w.gunits, 16)) ||
-      (rc = DAlloc(&w.wl_part, size_t(4) * ((nl + 255) / 256))) ||
+      (rc = DAlloc(&w.wl_part, size_t(smx::kWorklistPartWords) * ((nl + 255) / 256))) ||
       (rc = DAlloc(&w.work, max_items)) || (rc = DAlloc(&w.tau, anq)) ||
       (rc = DAlloc(&w.cand, acand)) ||
       (rc = DAlloc(&w.cand_count, size_t(anq) * smx::kCounterStride)) ||
@@ -469,11 +484,18 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   // stats: [0] overflow flag [1] max overflowing count [2] max count
   //        [3] pairs [4] work items [5] item-tiles (MFMA tiles of the scan)
   //        [6..7] code bytes (u64) [8] survivors summed over queries [9] fallbacks
+  //        [10] rescanned queries [11] rescan rounds [12] 16-slot tiles
   uint32_t* stats = w.counters + lay.stats;
   unsigned long long* code_bytes = reinterpret_cast<unsigned long long*>(stats + 6);
   const int seed = std::min(h->seed_leaves, L);
 
   const int variant = h->scan_variant;
+  // 16-slot tiles where leaves see few queries on average (configs 3/4: ~8
+  // per leaf); with ~100 (glove) the 32-slot-only kernel is faster (the
+  // 16-slot path costs registers and code in the kernel that carries it)
+  const uint32_t narrow = (h->narrow_tiles && variant == 0 &&
+                           uint64_t(nq) * uint64_t(L) < uint64_t(smx::kNarrowQueriesPerLeaf) *
+                                                            uint64_t(ix.nl)) ? 1u : 0u;
   smx::Bounds bd;
   bd.nq = uint32_t(nq);
   bd.items = w.max_items;
@@ -501,6 +523,17 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sa.L = L;
   sa.seed = seed;
   sa.kk = kk;
+  // the seed scan (MFMA) for 1..kSeedMaxMfma seed leaves; SMX_SEED_MFMA=0:
+  // the per-query seed kernel and a separate pair scatter
+  // (the seed lists hold query | seed index << 24: nq < 2^24)
+  const bool seed_mfma = h->seed_mfma && seed >= 1 && seed <= smx::kSeedMaxMfma &&
+                         nq < (1 << 24);
+  sa.mfma = seed_mfma ? 1 : 0;
+  sa.seed_count = w.counters + lay.seeds;
+  sa.seed_list = w.seed_list;
+  sa.seed_mask = w.seed_mask;
+  sa.seed_keys = w.seed_keys;
+  sa.nl = nl;
   sa.residual = ix.residual;
 
   smx::ScanArgs a{};
@@ -594,7 +627,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     // front end: state reset, partition scores, top-L + ranks + LUTs
     smx::FrontArgs f;
     f.init.counters = w.counters;
-    f.init.n_counters = uint32_t(nl);
+    f.init.n_counters = 2u * uint32_t(nl);   // pair and seed counters
     f.init.stats = stats;
     f.init.n_stats = 32u;
     f.init.cand_count = w.cand_count;
@@ -607,6 +640,12 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     f.mult = w.mult;
     f.inv = w.inv;
     f.one_to_many = single ? 1 : 0;
+    if (seed_mfma) {
+      f.seed_count = w.counters + lay.seeds;
+      f.seed_list = w.seed_list;
+      f.seed_mask = w.seed_mask;
+      f.seed = seed;
+    }
     SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s, &f));
     Mark(h, 1, s);
     if (ix.nl <= h->fused_worklist_leaves) {
@@ -614,9 +653,12 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
       // stream: a fork/join costs 5-10 us per cross-queue edge)
       const smx::WorklistArgs wla = smx::MakeWorklistArgs(
           ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes, w.wave_start, h->grid,
-          stats + 3, code_bytes, h->chunk_tiles, bd);
+          stats + 3, code_bytes, h->chunk_tiles, narrow, bd);
       Mark(h, 3, s);
-      SMX_HIP(smx::LaunchSeed(ix, sa, nq, s, &wla));
+      if (seed_mfma)
+        SMX_HIP(smx::LaunchSeedScan(ix, sa, s, &wla));
+      else
+        SMX_HIP(smx::LaunchSeed(ix, sa, nq, s, &wla));
       Mark(h, 4, s);
     } else {
       // Fork.  Side stream: the work list (and the empty slots' records);
@@ -629,21 +671,27 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
       // graph keeps it on the launch queue with the kernels before and after
       // it; the shorter work-list branch pays the cross-queue edges.
       SMX_HIP(hipEventRecord(h->fork_ev, s));
-      SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
+      if (seed_mfma)
+        SMX_HIP(smx::LaunchSeedScan(ix, sa, s));
+      else
+        SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
       Mark(h, 4, s);
       SMX_HIP(hipStreamWaitEvent(h->side, h->fork_ev, 0));
       SMX_HIP(smx::LaunchWorklist(ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes,
                                   w.wave_start, h->grid, stats + 3, code_bytes, h->chunk_tiles,
-                                  w.wl_part, bd, h->side));
+                                  narrow, w.wl_part, bd, h->side));
       Mark(h, 3, h->side);
       SMX_HIP(hipEventRecord(h->join_ev, h->side));
       SMX_HIP(hipStreamWaitEvent(s, h->join_ev, 0));   // join
     }
     // every pair's lane record with its sum limit (needs the work list and
-    // the seed thresholds)
-    SMX_HIP(smx::LaunchPairScatter(ix, sa, nq, s));
+    // the seed thresholds; the seed scan's select computes those first)
+    if (seed_mfma)
+      SMX_HIP(smx::LaunchSeedSelect(sa, nq, s));
+    else
+      SMX_HIP(smx::LaunchPairScatter(ix, sa, nq, s));
     Mark(h, 5, s);
-    SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s));
+    SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s, narrow != 0));
     Mark(h, 6, s);
     SMX_HIP(smx::LaunchFinalSelect(sel, nq, s));
     Mark(h, 7, s);
@@ -714,7 +762,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   // handled on the device, so the call returns with the work enqueued
   // (search_batched_device is stream-ordered; the host-buffer entry points
   // synchronise on their result copies).  Profiled calls read the stats.
-  uint32_t st[12] = {};
+  uint32_t st[16] = {};
   if (h->profiling || variant == 8) {
     SMX_HIP(hipMemcpyAsync(h->host_stats, stats, sizeof(st), hipMemcpyDeviceToHost, s));
     SMX_HIP(hipStreamSynchronize(s));
@@ -784,7 +832,9 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   t.scan_pairs = int32_t(st[3]);
   t.overflow_retries = int32_t(st[11]);   // rescan passes (queries: st[10])
   t.max_candidates = int32_t(st[2]);
-  t.scan_item_tiles = double(st[5]);
+  // units = 2 x 32-slot tiles + 16-slot tiles
+  t.scan_item_tiles16 = double(st[12]);
+  t.scan_item_tiles = (double(st[5]) - double(st[12])) * 0.5;
   t.mean_candidates = float(st[8]) / float(nq);
   t.scan_workgroups = h->grid;
   return SMX_OK;
@@ -875,6 +925,8 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
   }
   if (const char* fw = std::getenv("SMX_FUSED_WORKLIST"))
     h->fused_worklist_leaves = std::min(std::atoi(fw), smx::kFusedWorklistLeaves);
+  if (const char* nw = std::getenv("SMX_NARROW")) h->narrow_tiles = nw[0] != '0';
+  if (const char* sm = std::getenv("SMX_SEED_MFMA")) h->seed_mfma = sm[0] != '0';
   const char* ng = std::getenv("SMX_NO_GRAPH");
   // Eager launches by default: six kernels a call queue back to back on the
   // stream, while consecutive replays of a captured graph left ~13 us
@@ -1230,7 +1282,7 @@ int smx_create_lookup_tables(smx_index* h, const float* queries, int32_t nq, uin
   uint8_t* du = nullptr;
   int rc;
   if ((rc = DAlloc(&dq, size_t(nq) * ix.dim)) || (rc = DAlloc(&dm, nq)) || (rc = DAlloc(&di, nq)) ||
-      (rc = DAlloc(&dl, size_t(nq) * 2 * ix.ksteps * 16)) || (rc = DAlloc(&du, size_t(nq) * ix.nb * 16))) {
+      (rc = DAlloc(&dl, size_t(nq) * smx::LutRows(ix.ksteps) * 16)) || (rc = DAlloc(&du, size_t(nq) * ix.nb * 16))) {
     DFree(dq); DFree(dm); DFree(di); DFree(dl); DFree(du);
     return rc;
   }
@@ -1282,7 +1334,7 @@ int smx_lut16_leaf_scores(smx_index* h, int32_t leaf, const uint8_t* lut, int32_
   SMX_HIP(hipSetDevice(h->device));
   hipStream_t s = h->stream;
   const smx::DeviceIndex& ix = h->ix;
-  const int rows = 2 * ix.ksteps;
+  const int rows = smx::LutRows(ix.ksteps);
   std::vector<int8_t> l8(size_t(rows) * 16, 0);
   for (int i = 0; i < ix.nb * 16; ++i) l8[i] = int8_t(int(lut[i]) - 128);
   uint64_t n64 = 0;

@@ -125,6 +125,7 @@ def _oversized_leaf_index(spilled):
     rng = np.random.default_rng(77)
     nl, n, dim = (1 << 17) + 1, 40000, 16
     centers = rng.standard_normal((nl, dim)).astype(np.float32)
+    centers[7] *= 3.0   # so that queries along it rank leaf 7 first
     labels = rng.integers(0, nl, n)
     labels[:20000] = 7
     members = [np.arange(n)]
@@ -146,9 +147,10 @@ def _oversized_leaf_index(spilled):
     ix = TreeAHIndex(metric=0, dim=dim, num_blocks=nb, dims_per_block=2, residual=True,
                      centers=centers, codebook=codebook, leaf_offsets=offsets, leaf_members=mem,
                      member_codes=codes, num_datapoints=n, dataset=db)
-    q = np.concatenate([centers[7] + 0.05 * rng.standard_normal((16, dim)),
+    u = centers[7] / np.linalg.norm(centers[7])
+    q = np.concatenate([10.0 * u + 0.05 * rng.standard_normal((16, dim)),
                         rng.standard_normal((16, dim))]).astype(np.float32)
-    return ix, q
+    return ix, q, db
 
 
 @pytest.mark.parametrize("spilled", [False, True])
@@ -159,7 +161,7 @@ def test_shards_without_global_topn_merge_to_the_oracle(oracle, spilled, world):
     global id on the device); merge == unsharded GPU == ideal oracle."""
     from scann_amd import _native
     from scann_amd.distributed import NativeShardEngine
-    ix, q = _oversized_leaf_index(spilled)
+    ix, q, db = _oversized_leaf_index(spilled)
     assert ix.global_topn_shift_value() == 0 and int(ix.leaf_sizes().max()) > (1 << 14)
     whole = _native.NativeIndex(ix)
     shards = [ix.shard(r, world) for r in range(world)]
@@ -184,11 +186,26 @@ def test_shards_without_global_topn_merge_to_the_oracle(oracle, spilled, world):
             np.testing.assert_array_equal(sc.cpu().numpy(), oc)
             np.testing.assert_array_equal(si.cpu().numpy().astype(np.uint32), oi)
             np.testing.assert_array_equal(sd.cpu().numpy().view(np.uint32), od.view(np.uint32))
-        # a shard handle's own search_batched (k' > 256: the block select's
-        # global-id rows) runs from its member rows too
+        # a shard handle's own search_batched (k' > 256: the block select
+        # finds rows by global id) == the oracle on the shard's rows under
+        # their global ids
         s0 = _native.NativeIndex(shards[0])
-        gi, gd, gc = s0.search_batched(q, 20, 300, 10, True)
-        assert (gc > 0).all()
+        sh = shards[0]
+        # (the oracle takes a shard's whole-index shift and spill setting)
+        own = TreeAHIndex(metric=ix.metric, dim=ix.dim, num_blocks=ix.num_blocks,
+                          dims_per_block=ix.dims_per_block, residual=ix.residual,
+                          centers=ix.centers, codebook=ix.codebook, leaf_offsets=sh.leaf_offsets,
+                          leaf_members=sh.leaf_members, member_codes=sh.member_codes,
+                          num_datapoints=ix.num_datapoints, dataset=db,
+                          leaf_row_base=sh.leaf_row_base, global_topn_shift=0,
+                          global_spilled=spilled)
+        for leaves, pre in ((20, 300), (4, 150)):
+            gi, gd, gc = s0.search_batched(q, leaves, pre, 10, True)
+            oi, od, oc = oracle.search(own, q, leaves, pre, 10, True, oracle.MODE_IDEAL)
+            assert (gc[:16] > 0).all()
+            np.testing.assert_array_equal(gc, oc)
+            np.testing.assert_array_equal(gi, oi)
+            np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
         s0.close()
     finally:
         whole.close()

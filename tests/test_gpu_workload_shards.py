@@ -12,8 +12,9 @@ GPU as bench.py builds it (scann_amd/generate.py), then:
   * the shard as a standalone index (TreeAHIndex.standalone) on the GPU ==
     the oracle (ideal mode) on the same index, ids and distance bits, at the
     bench's operating points (tree_ah_hybrid_residual.cc:631-846);
-  * the same with a 512-entry candidate list, so that lists overflow and are
-    rescanned on the device (the timings report the rescan passes);
+  * the same with 512-entry candidate lists and no seed threshold, so that
+    lists overflow and are rescanned on the device (the timings report the
+    rescan passes);
   * (disjoint index) the shard engine's own list -- search_shard + merge of
     that one list, the bench's N = 1 path -- gives the same neighbors by
     global id.
@@ -51,8 +52,11 @@ def _check_points(oracle, ix, q, points, min_rows_per_leaf, multi_chunk_leaves):
     try:
         for lv, pre in points:
             oi, od, oc = oracle.search(view, q, lv, pre, 10, True, oracle.MODE_IDEAL, 16)
-            for cap in (0, 512):   # sized per call (autocap); small: overflow rescans
-                nv.set_tuning(candidates_per_query=cap)
+            # sized per call (autocap); then 512-entry lists without a seed
+            # threshold: every scanned row is a candidate, lists overflow and
+            # are rescanned on the device
+            for cap, seed in ((0, 4), (512, 0)):
+                nv.set_tuning(candidates_per_query=cap, seed_leaves=seed)
                 nv.set_profiling(True)
                 gi, gd, gc = nv.search_batched(q, lv, pre, 10, True)
                 t = nv.timings()

@@ -9,17 +9,17 @@ import pytest
 import worklist_model as wm
 
 
-@pytest.mark.parametrize("qtile", [32, 64])
-@pytest.mark.parametrize("seed", range(6))
-def test_shares_cover_items_exactly_once(seed, qtile):
+@pytest.mark.parametrize("small", [True, False])
+@pytest.mark.parametrize("seed", range(10))
+def test_shares_cover_items_exactly_once(seed, small):
     rng = np.random.default_rng(seed)
     nl = int(rng.integers(1, 300))
     sizes = rng.integers(0, 3000, nl)
     sizes[rng.random(nl) < 0.1] = 0                      # empty leaves
     counts = rng.poisson(rng.uniform(0.5, 150), nl)
     counts[rng.random(nl) < 0.2] = 0                     # leaves no query visits
-    wm.check([int(x) for x in sizes], [int(x) for x in counts], grid=256, qtile=qtile,
-             chunk_tiles=int(rng.choice([8, 16, 20, 40])))
+    wm.check([int(x) for x in sizes], [int(x) for x in counts], grid=int(rng.choice([64, 256, 3072])),
+             chunk_tiles=int(rng.choice([8, 16, 20, 40])), small=small)
 
 
 @pytest.mark.parametrize("sizes,counts", [
@@ -30,5 +30,24 @@ def test_shares_cover_items_exactly_once(seed, qtile):
     ([4000] * 3, [200, 1, 64]),      # leaves of many chunks, full query tiles
 ])
 def test_edge_shapes(sizes, counts):
-    for qtile in (32, 64):
-        wm.check(sizes, counts, grid=256, qtile=qtile)
+    for small in (True, False):
+        for grid in (8, 256, 3072):
+            wm.check(sizes, counts, grid=grid, small=small)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_few_queries_per_leaf_take_16_slot_tiles(seed):
+    """configs[4]'s density (a few queries per leaf): the items are 16-slot
+    tiles (weight 1), shares of 1-3 units (more workgroups than units) stay
+    exact, and a remainder of 17-31 queries keeps a 32-slot tile."""
+    rng = np.random.default_rng(300 + seed)
+    nl = int(rng.integers(50, 2000))
+    sizes = rng.integers(0, 4000, nl)
+    counts = rng.poisson(rng.uniform(1, 12), nl)
+    wl = wm.check([int(x) for x in sizes], [int(x) for x in counts],
+                  grid=int(rng.choice([256, 3072, 8192])), chunk_tiles=20)
+    for leaf, n, j0, j1, q, w in wl["work"]:
+        c = int(counts[leaf])
+        assert w == (1 if (c - 32 * q) <= 16 else 2)
+    assert wm.query_tiles(17) == (1, 0) and wm.query_tiles(16) == (0, 1)
+    assert wm.query_tiles(48) == (1, 1) and wm.query_tiles(64) == (2, 0)

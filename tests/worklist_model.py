@@ -41,16 +41,31 @@ def leaf_order(sizes):
     return order
 
 
-def build(sizes, counts, grid, qtile, chunk_tiles):
+def query_tiles(c, small=True):
+    """(32-slot, 16-slot) query tiles of a leaf with c queries (LeafQueryTiles):
+    a remainder of at most 16 queries takes a 16-slot tile."""
+    full, r = divmod(c, 32)
+    if r == 0:
+        return full, 0
+    if small and r <= 16:
+        return full, 1
+    return full + 1, 0
+
+
+def build(sizes, counts, grid, chunk_tiles, small=True):
+    """Items (leaf, n, j0, jend, query tile, weight) and the workgroups'
+    shares (first item, first tile, units).  A unit is a 16-slot tile: a
+    32-slot item's tiles weigh 2, a 16-slot item's 1; a tile belongs to the
+    share holding its first unit."""
     nl = len(sizes)
     order = leaf_order(sizes)
     items_p, units_p = [], []
     for p in range(nl):
         leaf = order[p]
         c, n = counts[leaf], sizes[leaf]
-        qt = (c + qtile - 1) // qtile
-        items_p.append(qt * chunks_of(n, chunk_tiles))
-        units_p.append(qt * ((n + 31) // 32))
+        q32, q16 = query_tiles(c, small)
+        items_p.append((q32 + q16) * chunks_of(n, chunk_tiles))
+        units_p.append((2 * q32 + q16) * ((n + 31) // 32))
     ex_i = np.concatenate([[0], np.cumsum(items_p)[:-1]]).astype(int)
     ex_u = np.concatenate([[0], np.cumsum(units_p)[:-1]]).astype(int)
     total_w = int(sum(units_p))
@@ -79,11 +94,12 @@ def build(sizes, counts, grid, qtile, chunk_tiles):
         leaf = order[p]
         c, n = counts[leaf], sizes[leaf]
         chunks = chunks_of(n, chunk_tiles)
-        qt = (c + qtile - 1) // qtile
+        q32, q16 = query_tiles(c, small)
         item0 = int(ex_i[p])
-        for u in range(qt * chunks):
+        for u in range((q32 + q16) * chunks):
             j0, j1 = chunk_tiles_range(n, chunk_tiles, u % chunks)
-            work[item0 + u] = (leaf, n, j0, j1, u // chunks)
+            q = u // chunks
+            work[item0 + u] = (leaf, n, j0, j1, q, 2 if q < q32 else 1)
         ua, ub = int(ex_u[p]), int(ex_u[p]) + units_p[p]
         if ua >= ub:
             continue
@@ -98,50 +114,58 @@ def build(sizes, counts, grid, qtile, chunk_tiles):
                 break
             ue = U0 + (span * (k + 1)) // nw
             off = us - ua
-            tq, rem = divmod(off, tiles)
+            if off < 2 * tiles * q32:
+                q, ru = divmod(off, 2 * tiles)
+                j = (ru + 1) // 2          # the first tile whose first unit is >= off
+                skip = 2 * j - ru
+                if j == tiles:
+                    q, j = q + 1, 0
+            else:
+                q, j, skip = q32, off - 2 * tiles * q32, 0
             ch = 0
-            while chunk_tiles_range(n, chunk_tiles, ch)[1] <= rem:
-                ch += 1
-            wave_start[GROUPS * k + g] = (item0 + tq * chunks + ch, rem, ue - us)
+            if q < q32 + q16:
+                while chunk_tiles_range(n, chunk_tiles, ch)[1] <= j:
+                    ch += 1
+            wave_start[GROUPS * k + g] = (item0 + q * chunks + ch, j, max(0, ue - us - skip))
             k += 1
     return dict(order=order, work=work, wave_start=wave_start, gunits=gunits, total_w=total_w,
-                chunk_tiles=chunk_tiles, qtile=qtile)
+                chunk_tiles=chunk_tiles)
 
 
 def list_segments(wl, b, max_segs=512):
     """The segments (item, j0, jend) of workgroup b's share, as ListSegments
-    walks it (64 lanes per step); raises if a taken item is not a real one."""
+    walks it (64 lanes per step): an item's tiles cost its weight in units;
+    a partly taken item takes the tiles whose first unit is inside the share.
+    Raises if a taken item is not a real one."""
     work = wl["work"]
     sw, sj, su = wl["wave_start"][b]
     segs = []
     while su > 0:
-        ts, used_lanes = [], 0
+        used_lanes = 0
         excl = 0
         for lane in range(64):
             idx = sw + lane
-            it = work[min(idx, len(work) - 1)] if work else None
-            if idx >= len(work):
-                # the device reads a clamped item here; it must never be used
-                t = None
-            else:
-                j0 = sj if (lane == 0 and sj) else it[2]
-                t = min(it[3] - j0, su) if it[3] > j0 else 0
             if excl >= su:
                 break
-            if t is None:
+            if idx >= len(work):
                 raise AssertionError(f"share of workgroup {b} runs past the items (item {idx})")
+            it = work[idx]
+            w = it[5]
+            j0 = sj if (lane == 0 and sj) else it[2]
+            t = max(0, it[3] - j0)
             used_lanes += 1
-            if t > 0:
-                segs.append((idx, j0, j0 + min(t, su - excl)))
-            excl += t
+            take = min(t, -(-(su - excl) // w))
+            if take > 0:
+                segs.append((idx, j0, j0 + take))
+            excl += min(t * w, su)
         sw += used_lanes
         su -= min(su, excl)
         sj = 0
     return segs
 
 
-def check(sizes, counts, grid=256, qtile=64, chunk_tiles=20):
-    wl = build(sizes, counts, grid, qtile, chunk_tiles)
+def check(sizes, counts, grid=256, chunk_tiles=20, small=True):
+    wl = build(sizes, counts, grid, chunk_tiles, small)
     assert all(w is not None for w in wl["wave_start"]), "a workgroup's share is not written"
     seen = {}
     for b in range(grid):
@@ -151,8 +175,11 @@ def check(sizes, counts, grid=256, qtile=64, chunk_tiles=20):
                 assert key not in seen, f"tile {t} of item {idx} scanned twice"
                 seen[key] = b
     # every tile of every item exactly once
-    for idx, (leaf, n, j0, j1, qt) in enumerate(wl["work"]):
+    tiles = 0
+    for idx, (leaf, n, j0, j1, qt, w) in enumerate(wl["work"]):
         for t in range(j0, j1):
             assert (idx, t) in seen, f"tile {t} of item {idx} (leaf {leaf}) never scanned"
-    assert len(seen) == wl["total_w"]
+        tiles += j1 - j0
+    assert len(seen) == tiles
+    assert sum((j1 - j0) * w for (_, _, j0, j1, _, w) in wl["work"]) == wl["total_w"]
     return wl
