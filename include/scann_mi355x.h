@@ -238,6 +238,16 @@ int smx_exact_distances(smx_index* index, const float* queries, int32_t nq,
 int smx_lut16_leaf_scores(smx_index* index, int32_t leaf, const uint8_t* lut,
                           int32_t* out_scores);
 
+/* The seed threshold select on its own (device buffers, enqueued on `stream`):
+ * for each of `sets` sets of 4096 order-preserving distance bits (uint32,
+ * 0xFFFFFFFF = no value), out[i] = (v << 32) | 0xFFFFFFFF for v the kk-th
+ * smallest value of set i, or ~0 when it holds fewer than kk values -- the
+ * pruning bound a query's first leaves give its scan, the role of the
+ * running top-k threshold of the reference's TopNeighbors
+ * (scann/utils/fast_top_neighbors.h) before the scan starts. */
+int smx_kth_threshold_keys(const uint32_t* d_vals, int32_t sets, int32_t kk, uint64_t* d_out,
+                           void* stream);
+
 /* ---- index build (device buffers, enqueued on `stream`) ----------------- */
 
 /* Nearest center of every row: out[i] = argmin_j ||x_i - c_j||^2 (ties to the

@@ -57,6 +57,7 @@ SIGNATURES = {
     "smx_search_pre_reorder": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp]),
     "smx_exact_distances": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp]),
     "smx_lut16_leaf_scores": (ctypes.c_int, [_vp, _i32, _vp, _vp]),
+    "smx_kth_threshold_keys": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp]),
     "smx_set_profiling": (ctypes.c_int, [_vp, _i32]),
     "smx_get_timings": (ctypes.c_int, [_vp, ctypes.POINTER(Timings)]),
     "smx_set_tuning": (ctypes.c_int, [_vp, _i32, _i32, _i32, _i32]),
@@ -160,6 +161,12 @@ def _current_stream(stream):
     if torch is not None and torch.cuda.is_available() and torch.cuda.is_initialized():
         return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     return None
+
+
+def kth_threshold_keys_device(vals_ptr, sets, kk, out_ptr, stream=None):
+    """smx_kth_threshold_keys on device buffers (the seed threshold select)."""
+    check(load().smx_kth_threshold_keys(vals_ptr, int(sets), int(kk), out_ptr, stream),
+          "smx_kth_threshold_keys")
 
 
 def nearest_centers_device(x_ptr, n, d, c_ptr, k, out_ptr, primary_ptr=None, lam=0.0,

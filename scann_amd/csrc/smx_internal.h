@@ -19,13 +19,15 @@ constexpr int kNarrowSlots = 16;
 constexpr int kTotalsTiles16 = 9;
 // The seed scan (the per-query thresholds on MFMA): each leaf lists at most
 // kSeedSlots of the queries it seeds (the top-L kernel claims the slots), each
-// query keeps at most kSeedKeys seed distances -- SeedLeafCap per seed leaf.
-constexpr int kSeedSlots = 32;
-constexpr int kSeedKeys = 4096;
-constexpr int kSeedMaxMfma = 32;   // seed leaves per query (the seed mask's bits)
-__host__ __device__ constexpr int SeedLeafCap(int seed) {
-  return seed <= 0 ? 0 : (kSeedKeys / seed < 1024 ? (kSeedKeys / seed) & ~31 : 1024);
-}
+// query keeps at most kSeedKeys seed distances (SeedTau's kSeedCap).
+constexpr int kSeedSlots = 64;
+#ifndef SMX_SEED_PER_THREAD
+#define SMX_SEED_PER_THREAD 16   // seed rows per query / 256 (a build-time knob)
+#endif
+constexpr int kSeedKeys = 256 * SMX_SEED_PER_THREAD;
+constexpr int kSeedMaxMfma = 32;   // seed leaves per query on the seed scan
+// a seed-scan unit: one wave, 16 queries of a leaf x 256 rows (8 tiles)
+constexpr int kSeedSpans = kSeedKeys / 256;
 constexpr uint32_t kItemNarrow = 1u << 31;
 // 16-slot tiles are used when a call averages fewer queries per leaf
 // (nq * L / num_leaves) than this
@@ -174,9 +176,11 @@ struct SeedArgs {
   // granted seed leaves and their distances
   int mfma;
   const uint32_t* seed_count; // [nl] strided (kCounterStride)
-  const uint32_t* seed_list;  // [nl][kSeedSlots] query | seed index << 24
-  const uint32_t* seed_mask;  // [nq] bit i: seed leaf i was scanned
-  uint32_t* seed_keys;        // [nq][kSeedKeys] ordered distances, [i][SeedLeafCap]
+  const uint64_t* seed_list;  // [nl][kSeedSlots] query | seed index << 24 | (o | c << 16) << 32
+  const uint32_t* seed_total;  // [nq][2] rows spanned, rows granted
+  uint32_t* seed_keys;         // [nq][kSeedKeys] ordered distances (SeedClaims' layout)
+  const uint32_t* seed_units;  // leaf << 6 | group << 4 | span, one per wave unit
+  const uint32_t* seed_nunits; // their number (a counter)
   int nl;
   // the inversion (pair scatter): every (query, leaf) pair's slot in its
   // leaf's work items
@@ -324,8 +328,11 @@ struct FrontArgs {
   int one_to_many = 0;              // the single-query partition scores (A.8 order)
   // the seed scan's claims (NULL: the per-query seed kernel)
   uint32_t* seed_count = nullptr;   // [nl] strided, zeroed by init
-  uint32_t* seed_list = nullptr;    // [nl][kSeedSlots]
-  uint32_t* seed_mask = nullptr;    // [nq]
+  uint64_t* seed_list = nullptr;    // [nl][kSeedSlots]
+  uint32_t* seed_total = nullptr;   // [nq][2]
+  uint32_t* seed_keys = nullptr;    // [nq][kSeedKeys] (dropped seed leaves' ranges)
+  uint32_t* seed_units = nullptr;   // [nq * kSeedMaxMfma * kSeedSpans] the seed scan's units
+  uint32_t* seed_nunits = nullptr;  // their count (zeroed by init)
   int seed = 0;                     // seed leaves per query (<= kSeedMaxMfma)
 };
 hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int nq,
@@ -366,12 +373,14 @@ hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStrea
                       const WorklistArgs* wl = nullptr);
 // The seed scan (MFMA): every listed (leaf, seeding query) pair's distances
 // into seed_keys; with `wl`, extra blocks build the whole work list
-// (ix.nl <= kFusedWorklistLeaves).  Needs 1 <= a.seed <= kSeedMaxMfma.
-hipError_t LaunchSeedScan(const DeviceIndex& ix, const SeedArgs& a, hipStream_t s,
+// (ix.nl <= kFusedWorklistLeaves).  Needs 1 <= a.seed <= kSeedMaxMfma;
+// `blocks` 4-wave blocks walk the call's seed units.
+hipError_t LaunchSeedScan(const DeviceIndex& ix, const SeedArgs& a, int blocks, hipStream_t s,
                           const WorklistArgs* wl = nullptr);
 // Per query its threshold from the seed scan's distances, then its pairs'
 // lane records (after the work list: they need leaf_item0).
 hipError_t LaunchSeedSelect(const SeedArgs& a, int nq, hipStream_t s);
+hipError_t LaunchKthKeys(const uint32_t* vals, int sets, int kk, uint64_t* out, hipStream_t s);
 // Every (query, leaf) pair's lane record into its leaf's work items (after
 // LaunchWorklist and the seed thresholds: each record carries its sum limit).
 hipError_t LaunchPairScatter(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s);

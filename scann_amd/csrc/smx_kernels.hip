@@ -531,33 +531,78 @@ struct TopLTail {
   uint32_t* rank;
   LutParams lut;          // lut.lut NULL: no LUT
   uint32_t* seed_count;   // the seed scan's claims, or NULL
-  uint32_t* seed_list;
-  uint32_t* seed_mask;
+  uint64_t* seed_list;
+  uint32_t* seed_total;
+  uint32_t* seed_keys;
+  uint32_t* seed_units;
+  uint32_t* seed_nunits;
+  const uint32_t* leaf_size;
   int seed;
 };
 
 // The query's first `seed` leaves claim slots in those leaves' seed lists
-// (the seed scan, seed_scan_kernel): a returning atomic on the leaf's seed
-// counter gives the slot; a leaf lists at most kSeedSlots seeding queries,
-// and a query without a slot goes without that seed leaf (the k'-th of a
-// subset of its candidates still bounds the final k'-th).  The granted seed
-// indices form the query's seed mask.  Block-wide (every thread calls).
+// (the seed scan, seed_scan_kernel).  The seed values are SeedTau's: the
+// leaves in the query's order, leaf i's first c_i rows, c_i = min(size_i,
+// kSeedKeys - o_i), o_i = the rows of the leaves before it, so that the
+// query's keys seed_keys[q][o_i + dp] are exactly the values SeedTau would
+// rank.  A returning atomic on the leaf's seed counter gives the slot; a leaf
+// lists at most kSeedSlots seeding queries, and a query without a slot goes
+// without that leaf: its range is filled with "no value" here (the k'-th of a
+// subset of the candidates still bounds the final k'-th from above).
+// seed_total[q] = {rows spanned, rows granted}.  Block-wide (every thread
+// calls; seed <= kSeedMaxMfma <= 64).
 __device__ void SeedClaims(int qi, uint32_t m, const uint64_t* keys, const TopLTail& tail) {
   if (!tail.seed_count) return;   // (uniform)
-  __shared__ uint32_t s_mask;
-  if (threadIdx.x == 0) s_mask = 0;
-  __syncthreads();
-  const int i = int(threadIdx.x);
-  if (i < tail.seed && uint32_t(i) < m) {
-    const uint32_t leaf = uint32_t(keys[i] & 0xFFFFFFFFu);
-    const uint32_t slot = atomicAdd(&tail.seed_count[size_t(leaf) * kCounterStride], 1u);
-    if (slot < uint32_t(kSeedSlots)) {
-      tail.seed_list[size_t(leaf) * kSeedSlots + slot] = uint32_t(qi) | (uint32_t(i) << 24);
-      atomicOr(&s_mask, 1u << i);
+  __shared__ uint32_t s_drop, s_off[kSeedMaxMfma], s_cnt[kSeedMaxMfma];
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x < 64) {
+    const int nseed = min(tail.seed, int(min(m, uint32_t(kSeedMaxMfma))));
+    const bool has = lane < nseed;
+    const uint32_t leaf = has ? uint32_t(keys[lane] & 0xFFFFFFFFu) : 0u;
+    const uint32_t sz = has ? tail.leaf_size[leaf] : 0u;
+    uint32_t inc = sz;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t t = uint32_t(__shfl_up(int(inc), off));
+      if (lane >= off) inc += t;
+    }
+    const uint32_t o = inc - sz;
+    const uint32_t c = o < uint32_t(kSeedKeys) ? min(sz, uint32_t(kSeedKeys) - o) : 0u;
+    bool dropped = false;
+    if (c > 0) {
+      const uint32_t slot = atomicAdd(&tail.seed_count[size_t(leaf) * kCounterStride], 1u);
+      if (slot < uint32_t(kSeedSlots)) {
+        tail.seed_list[size_t(leaf) * kSeedSlots + slot] =
+            (uint64_t(o | (c << 16)) << 32) | (uint32_t(qi) | (uint32_t(lane) << 24));
+        if (slot % 16u == 0) {   // a new group of 16: its wave units, 256 rows each
+          const uint32_t spans = (min(sz, uint32_t(kSeedKeys)) + 255u) / 256u;
+          const uint32_t u0 = atomicAdd(tail.seed_nunits, spans);
+          for (uint32_t sp = 0; sp < spans; ++sp)
+            tail.seed_units[u0 + sp] = (leaf << 6) | ((slot / 16u) << 4) | sp;
+        }
+      } else {
+        dropped = true;
+      }
+    }
+    uint32_t granted = dropped ? 0u : c;
+    for (int off = 32; off > 0; off >>= 1) granted += uint32_t(__shfl_xor(int(granted), off));
+    const uint64_t drop = __ballot(dropped);
+    if (lane < kSeedMaxMfma) {
+      s_off[lane] = o;
+      s_cnt[lane] = c;
+    }
+    const uint32_t span = min(uint32_t(__shfl(int(inc), 63)), uint32_t(kSeedKeys));
+    if (lane == 0) {
+      s_drop = uint32_t(drop);
+      tail.seed_total[2 * size_t(qi)] = span;
+      tail.seed_total[2 * size_t(qi) + 1] = granted;
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) tail.seed_mask[qi] = s_mask;
+  for (uint32_t d = s_drop; d; d &= d - 1) {   // (block-uniform; rare)
+    const int i = __builtin_ctz(d);
+    for (uint32_t j = threadIdx.x; j < s_cnt[i]; j += blockDim.x)
+      tail.seed_keys[size_t(qi) * kSeedKeys + s_off[i] + j] = 0xFFFFFFFFu;
+  }
 }
 
 __device__ void TopLFinish(int qi, int L, uint32_t m, const uint64_t* sel, int32_t* out_leaf,
@@ -894,6 +939,16 @@ __global__ void __launch_bounds__(256) topl_select_global_kernel(const float* __
   TopLGlobalSelect(scores, nl, L, lcap, lds64, out_leaf, out_dist, tail);
 }
 
+// The values of histogram bin b (bin = floor((v - lo) scale / 2^32)) as the
+// new [lo, hi]: v - lo in [ceil(b 2^32 / scale), ceil((b + 1) 2^32 / scale) - 1]
+// (64-bit: the upper end passes 2^32 when hi - lo is near 2^32).
+__device__ __forceinline__ void BinRange(uint32_t b, uint64_t scale, uint32_t& lo, uint32_t& hi) {
+  const uint64_t blo = uint64_t(lo) + ((uint64_t(b) << 32) + scale - 1) / scale;
+  const uint64_t bhi = uint64_t(lo) + ((uint64_t(b + 1) << 32) + scale - 1) / scale - 1u;
+  lo = uint32_t(blo);
+  hi = uint32_t(min(bhi, uint64_t(hi)));
+}
+
 // Exact top-L for many leaves (configs[4]: 50000) by a sampled threshold:
 // the k-th smallest of 2048 sampled scores (k = 1.5 L * 2048 / nl + 16,
 // found exactly by histogram rounds over 8 values per thread) is a value T at
@@ -943,10 +998,7 @@ __device__ uint32_t BlockKthOfSamples(const uint32_t (&v)[kSampleVals], uint32_t
     __syncthreads();
     const uint32_t b = s_bin;
     below = s_below;
-    const uint32_t blo = lo + uint32_t(((uint64_t(b) << 32) + scale - 1) / scale);
-    const uint32_t bhi = lo + uint32_t(((uint64_t(b + 1) << 32) + scale - 1) / scale) - 1u;
-    lo = blo;
-    hi = min(bhi, hi);
+    BinRange(b, scale, lo, hi);
     __syncthreads();   // hist, wsum and s_bin are rewritten by the next round
   }
   return hi;
@@ -1536,13 +1588,54 @@ __device__ __forceinline__ void LoadCodes(const uint8_t* p, uint32_t* codes) {
 #ifndef SMX_SEED_U
 #define SMX_SEED_U 4
 #endif
-#ifndef SMX_SEED_PER_THREAD
-#define SMX_SEED_PER_THREAD 16
-#endif
-constexpr int kSeedPerThread = SMX_SEED_PER_THREAD;
+constexpr int kSeedPerThread = kSeedKeys / 256;
 constexpr uint32_t kSeedCap = 256u * kSeedPerThread;
 constexpr int kSeedMaxLeaves = 64;   // one wave of leaf slots
 constexpr int kSeedSel = 1024;       // values under the minima bound ranked exactly
+
+// The rank of `key` among the 256 keys the threads of a 256-thread block
+// hold (distinct keys).  Each wave sorts its 64 keys in registers (bitonic,
+// lane exchanges, no barrier) into sbuf[64 w ..]; a key's rank is its place
+// in its wave's order plus, per other wave, the number of that wave's keys
+// below it (binary search of the sorted run).  Block-wide (every thread
+// calls); sbuf holds 256 keys.
+__device__ uint32_t BlockRank256(uint64_t key, uint64_t* sbuf) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint64_t v = key;
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const uint32_t lo = uint32_t(__shfl_xor(int(uint32_t(v)), j));
+      const uint32_t hi = uint32_t(__shfl_xor(int(uint32_t(v >> 32)), j));
+      const uint64_t o = (uint64_t(hi) << 32) | lo;
+      const bool up = (lane & k) == 0, low = (lane & j) == 0;
+      v = (low == up) ? (o < v ? o : v) : (o > v ? o : v);
+    }
+  }
+  sbuf[threadIdx.x] = v;
+  __syncthreads();
+  uint32_t r = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint64_t* run = sbuf + 64 * w;
+    if (w == wid) continue;
+    uint32_t b = 0;   // keys of run w below key: the first b with run[b] >= key
+#pragma unroll
+    for (uint32_t step = 32; step > 0; step >>= 1)
+      if (run[b + step - 1] < key) b += step;
+    r += b + (run[b] < key ? 1u : 0u);   // b = 63: all 64 below?
+  }
+  // the key's place in its own wave's sorted run
+  const uint64_t* own = sbuf + 64 * wid;
+  uint32_t b = 0;
+#pragma unroll
+  for (uint32_t step = 32; step > 0; step >>= 1)
+    if (own[b + step - 1] < key) b += step;
+  b += own[b] < key ? 1u : 0u;
+  __syncthreads();   // sbuf is rewritten by the next call
+  return r + b;
+}
 
 // The threshold key of a query from its seed distances (ordered bits, 16
 // per thread of a 256-thread block, 0xFFFFFFFF = none): the exact kk-th
@@ -1569,9 +1662,7 @@ __device__ uint64_t ThresholdOfVals(const uint32_t (&vals)[kSeedPerThread], uint
 #pragma unroll
     for (int i = 0; i < kSeedPerThread; ++i) vmin = min(vmin, vals[i]);
     const uint64_t mk = (uint64_t(vmin) << 32) | uint32_t(tid);
-    skey[tid] = mk;
-    __syncthreads();
-    if (CountLess(skey, 256u, mk) == kk - 1u) s_thi = vmin;
+    if (BlockRank256(mk, skey) == kk - 1u) s_thi = vmin;
     __syncthreads();
     const uint32_t thi = s_thi;
 #pragma unroll
@@ -1582,6 +1673,13 @@ __device__ uint64_t ThresholdOfVals(const uint32_t (&vals)[kSeedPerThread], uint
       }
     __syncthreads();
     const uint32_t c = s_cnt;
+    if (c <= 256u) {   // block rank of the compacted keys (the rest padded above them)
+      const uint64_t key = uint32_t(tid) < c ? skey[tid] : (~0ull << 16) | uint32_t(tid);
+      __syncthreads();   // skey is the rank's buffer
+      if (BlockRank256(key, skey) == kk - 1u) s_T = (key & 0xFFFFFFFF00000000ull) | 0xFFFFFFFFull;
+      __syncthreads();
+      return s_T;
+    }
     if (c <= uint32_t(kSeedSel)) {
       for (uint32_t i = tid; i < c; i += 256) {
         const uint64_t key = skey[i];
@@ -1629,11 +1727,7 @@ __device__ uint64_t ThresholdOfVals(const uint32_t (&vals)[kSeedPerThread], uint
     __syncthreads();
     const uint32_t b = s_bin;
     below = s_below;
-    // values of bin b: v - lo in [ceil(b 2^32 / scale), ceil((b+1) 2^32 / scale) - 1]
-    const uint32_t blo = lo + uint32_t(((uint64_t(b) << 32) + scale - 1) / scale);
-    const uint32_t bhi = lo + uint32_t(((uint64_t(b + 1) << 32) + scale - 1) / scale) - 1u;
-    lo = blo;
-    hi = min(bhi, hi);
+    BinRange(b, scale, lo, hi);
     __syncthreads();   // hist, wsum and s_bin are rewritten by the next round
   }
   if (tid == 0) s_T = (uint64_t(hi) << 32) | 0xFFFFFFFFull;
@@ -2649,15 +2743,20 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
 // ---------------------------------------------------------------------------
 // The seed scan: every query's threshold from its first `seed` leaves on the
 // 16-slot MFMA path instead of per-query LDS lookups.  The top-L kernel has
-// listed, per leaf, the queries it seeds (SeedClaims: at most kSeedSlots);
-// one wave per leaf runs its first SeedLeafCap(seed) datapoints for those
-// queries, 16 at a time, and stores every (query, datapoint) distance as
-// ordered bits at seed_keys[q][i * cap + dp] (i = the leaf's seed index in
-// q's top-L).  The same distances as the scan (d = fl(fl(S inv) + bias)),
-// so the kk-th of them bounds the final kk-th from above.  Blocks from
+// listed, per leaf, the queries it seeds with each one's row budget
+// (SeedClaims: at most kSeedSlots records {query, seed index, offset o, rows
+// c}) and, per group of 16 of them, one wave unit per 256 rows of the leaf
+// (up to kSeedKeys).  The launch's waves walk the units: a unit's wave issues
+// the code loads of its 8 tiles at once, then runs them for its 16 queries up
+// to the group's largest budget, storing each query's distances of rows dp <
+// c as ordered bits at seed_keys[q][o + dp] -- the same values, in the same
+// places, as SeedTau ranks: d = fl(fl(S inv) + bias), the scan's distance, so
+// the kk-th of them bounds the final kk-th from above.  Blocks from
 // `seed_blocks` on build the work list (WorklistFusedBlock), as the per-query
 // seed launch does.
 // ---------------------------------------------------------------------------
+static_assert(kSeedSpans <= 16 && kSeedSlots / 16 <= 4, "seed unit fields");
+
 template <int K>
 __global__ void __launch_bounds__(256) seed_scan_kernel(SeedArgs a, WorklistArgs w,
                                                         int seed_blocks) {
@@ -2668,6 +2767,7 @@ __global__ void __launch_bounds__(256) seed_scan_kernel(SeedArgs a, WorklistArgs
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
   constexpr int W = 4 * NW;
   constexpr int K16 = (K + 3) / 4;
+  constexpr int T = 8;   // tiles per unit
   __shared__ __align__(256) v4i opnd_tab[32];
   v4i* const grp_tab = opnd_tab;
   int* const pos_tab = reinterpret_cast<int*>(opnd_tab + 16);
@@ -2680,62 +2780,70 @@ __global__ void __launch_bounds__(256) seed_scan_kernel(SeedArgs a, WorklistArgs
     pos_tab[4 * threadIdx.x] = int((threadIdx.x & 3u) * 0x5555u | ((threadIdx.x >> 2) * 0x5555u) << 16);
     pos_tab[4 * threadIdx.x + 1] = 0;
   }
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int leaf = int(blockIdx.x) * 4 + int(threadIdx.x >> 6);
-  if (leaf >= a.nl) return;
-  const uint32_t cnt = min(a.seed_count[size_t(leaf) * kCounterStride], uint32_t(kSeedSlots));
-  if (cnt == 0) return;
-  const uint32_t cap = uint32_t(SeedLeafCap(a.seed));
-  const uint32_t n = min(a.leaf_size[leaf], cap);
-  const uint32_t tiles = (n + 31u) / 32u;
-  const uint8_t* tseg = a.tiles + a.tile_off[leaf] * 64ull * W;
+  __syncthreads();   // (the last barrier)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t nunits = *a.seed_nunits;
   const uint32_t lane_off = uint32_t((lane >> 5) * 32 + (lane & 15)) * uint32_t(W);
   const uint32_t sh = uint32_t((lane >> 4) & 1) * 8u;
   const uint32_t rg = uint32_t(lane >> 4);   // D rows 4 rg + e of column lane % 16
-  for (uint32_t g = 0; g < cnt; g += 16) {
+  for (uint32_t u = uint32_t(blockIdx.x) * 4u + uint32_t(wid); u < nunits;
+       u += uint32_t(seed_blocks) * 4u) {   // (wave-uniform)
+    const uint32_t ur = a.seed_units[u];
+    const uint32_t leaf = ur >> 6, g = ((ur >> 4) & 3u) * 16u, row0 = (ur & 15u) * 256u;
+    const uint32_t cnt = min(a.seed_count[size_t(leaf) * kCounterStride], uint32_t(kSeedSlots));
     const uint32_t sl = g + uint32_t(lane & 15);
     const bool valid = sl < cnt;
-    const uint32_t rec = valid ? a.seed_list[size_t(leaf) * kSeedSlots + sl] : 0u;
-    const uint32_t qi = rec & 0xFFFFFFu, si = rec >> 24;
+    const uint64_t rec = valid ? a.seed_list[size_t(leaf) * kSeedSlots + sl] : 0ull;
+    const uint32_t qi = uint32_t(rec) & 0xFFFFFFu, si = uint32_t(rec) >> 24;
+    const uint32_t o = uint32_t(rec >> 32) & 0xFFFFu, c = uint32_t(rec >> 48);
+    uint32_t need = c;   // the group's largest budget
+    for (int off = 8; off > 0; off >>= 1) need = max(need, uint32_t(__shfl_xor(int(need), off)));
+    if (need <= row0) continue;
+    const uint32_t tiles = min(uint32_t(T), (need - row0 + 31u) / 32u);
+    const uint8_t* tseg = a.tiles + (a.tile_off[leaf] + row0 / 32u) * 64ull * W;
+    uint32_t ca[T][NW], cb[T][NW];
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
+      const uint32_t t = min(uint32_t(i), tiles - 1u);   // (clamped: no branch)
+      const uint8_t* tp = tseg + size_t(t) * (64 * W) + lane_off;
+      LoadCodes<K>(tp, ca[i]);
+      LoadCodes<K>(tp + 16 * W, cb[i]);
+    }
     const float bias = (valid && a.residual) ? a.topl_dist[size_t(qi) * a.L + si] : 0.0f;
     const float inv = a.inv[qi];
-    uint32_t* out = a.seed_keys + size_t(qi) * kSeedKeys + si * cap;
+    uint32_t* out = a.seed_keys + size_t(qi) * kSeedKeys + o;
     v8i b[K16];
     const v8i* bp = reinterpret_cast<const v8i*>(reinterpret_cast<const uint8_t*>(a.lut) +
                                                   size_t(qi) * (LutRows(K) * 16) +
                                                   uint32_t(lane >> 4) * 32u);
 #pragma unroll
     for (int s2 = 0; s2 < K16; ++s2) b[s2] = bp[4 * s2];
-    for (uint32_t t = 0; t < tiles; ++t) {
-      uint32_t ca[NW], cb[NW];
-      const uint8_t* tp = tseg + size_t(t) * (64 * W) + lane_off;
-      LoadCodes<K>(tp, ca);
-      LoadCodes<K>(tp + 16 * W, cb);
 #pragma unroll
-      for (int i = 0; i < NW; ++i) {
-        ca[i] >>= sh;
-        cb[i] >>= sh;
+    for (int i = 0; i < T; ++i) {
+      if (uint32_t(i) >= tiles) break;   // (wave-uniform)
+      uint32_t xa[NW], xb[NW];
+#pragma unroll
+      for (int j = 0; j < NW; ++j) {
+        xa[j] = ca[i][j] >> sh;
+        xb[j] = cb[i][j] >> sh;
       }
       v4i acc_a, acc_b;
-      TileSmfmac16<K, 3>(ca, cb, b, grp_tab, pos_tab, acc_a, acc_b);
-      if (valid) {
-        // datapoints 32 t + 16 c + 4 rg + e of chain c: 4 contiguous keys each
-        const uint32_t d0 = t * 32u + 4u * rg;
+      TileSmfmac16<K, 3>(xa, xb, b, grp_tab, pos_tab, acc_a, acc_b);
+      // rows row0 + 32 i + 16 ch + 4 rg + e of chain ch: 4 contiguous keys each
+      const uint32_t d0 = row0 + uint32_t(i) * 32u + 4u * rg;
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const v4i& acc = c ? acc_b : acc_a;
-          const uint32_t dp = d0 + 16u * uint32_t(c);
-          uint32_t k4[4];
+      for (int ch = 0; ch < 2; ++ch) {
+        const v4i& acc = ch ? acc_b : acc_a;
+        const uint32_t dp = d0 + 16u * uint32_t(ch);
+        uint32_t k4[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) k4[e] = OrderedBits(DistOf(acc[e], inv, bias));
-          if (dp + 3u < n) {
-            *reinterpret_cast<uint4*>(out + dp) = make_uint4(k4[0], k4[1], k4[2], k4[3]);
-          } else {
+        for (int e = 0; e < 4; ++e) k4[e] = OrderedBits(DistOf(acc[e], inv, bias));
+        if (dp + 3u < c && ((o + dp) & 3u) == 0) {
+          *reinterpret_cast<uint4*>(out + dp) = make_uint4(k4[0], k4[1], k4[2], k4[3]);
+        } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (dp + uint32_t(e) < n) out[dp + e] = k4[e];
-          }
+          for (int e = 0; e < 4; ++e)
+            if (dp + uint32_t(e) < c) out[dp + e] = k4[e];
         }
       }
     }
@@ -2743,45 +2851,50 @@ __global__ void __launch_bounds__(256) seed_scan_kernel(SeedArgs a, WorklistArgs
 }
 
 // Per query (one 256-thread block): its threshold key from the seed scan's
-// distances (the granted seed leaves' first min(size, cap) keys), then every
-// one of its (query, leaf) pairs into the scan's work items with its sum
-// limit -- the pair scatter of the per-query path, one launch for both.
+// distances (seed_keys[q][0, span), "no value" where a seed leaf was not
+// granted; SeedTau's rule when at least kk were), then every one of its
+// (query, leaf) pairs into the scan's work items with its sum limit -- the
+// pair scatter of the per-query path, one launch for both.
 __global__ void __launch_bounds__(256) seed_select_kernel(SeedArgs a) {
   const int qi = int(blockIdx.x);
   const int tid = threadIdx.x;
-  const uint32_t cap = uint32_t(SeedLeafCap(a.seed));
-  const int nseed = min(a.seed, min(a.L, kSeedMaxMfma));
-  const uint32_t mask = a.seed_mask[qi];
-  __shared__ uint32_t s_cnt[kSeedMaxMfma];
-  if (tid < nseed) {
-    uint32_t c = 0;
-    if ((mask >> tid) & 1u) {
-      const int32_t leaf = a.topl_leaf[size_t(qi) * a.L + tid];
-      c = leaf >= 0 ? min(a.leaf_size[leaf], cap) : 0u;
-    }
-    s_cnt[tid] = c;
-  }
-  __syncthreads();
-  uint32_t total = 0;
-  for (int i = 0; i < nseed; ++i) total += s_cnt[i];
+  const uint32_t span = a.seed_total[2 * size_t(qi)], granted = a.seed_total[2 * size_t(qi) + 1];
   uint64_t T = kNoThreshold;
   const uint32_t kk = uint32_t(a.kk);
-  if (kk > 0 && total >= kk) {   // (block-uniform)
+  if (kk > 0 && granted >= kk) {   // (block-uniform)
     const uint32_t* keys = a.seed_keys + size_t(qi) * kSeedKeys;
-    const uint32_t span = uint32_t(nseed) * cap;   // <= kSeedKeys
     uint32_t vals[kSeedPerThread];
 #pragma unroll
     for (int k = 0; k < kSeedPerThread; ++k) {
       const uint32_t idx = uint32_t(tid) + 256u * uint32_t(k);
-      const uint32_t i = idx / cap, dp = idx - i * cap;
-      const bool ok = idx < span && dp < s_cnt[min(i, uint32_t(kSeedMaxMfma - 1))];
-      vals[k] = ok ? keys[idx] : 0xFFFFFFFFu;
+      vals[k] = idx < span ? keys[idx] : 0xFFFFFFFFu;
     }
     T = ThresholdOfVals(vals, kk);
   }
   if (tid == 0) a.tau_key[qi] = T;
   for (int i = tid; i < a.L; i += 256)
     PairScatterTau(a, size_t(qi) * a.L + size_t(i), a.leaf_item0, T);
+}
+
+// Stage entry point of the threshold select: per set of kSeedKeys ordered
+// distance bits (0xFFFFFFFF = none), ThresholdOfVals' key, or kNoThreshold
+// when the set holds fewer than kk values (SeedTau's rule).
+__global__ void __launch_bounds__(256) kth_keys_kernel(const uint32_t* __restrict__ vals,
+                                                       uint32_t kk, uint64_t* __restrict__ out) {
+  __shared__ uint32_t s_n;
+  const int tid = threadIdx.x;
+  if (tid == 0) s_n = 0;
+  __syncthreads();
+  uint32_t v[kSeedPerThread], n = 0;
+#pragma unroll
+  for (int k = 0; k < kSeedPerThread; ++k) {
+    v[k] = vals[size_t(blockIdx.x) * kSeedKeys + uint32_t(tid) + 256u * uint32_t(k)];
+    n += v[k] != 0xFFFFFFFFu ? 1u : 0u;
+  }
+  atomicAdd(&s_n, n);
+  __syncthreads();
+  const uint64_t T = (kk > 0 && s_n >= kk) ? ThresholdOfVals(v, kk) : kNoThreshold;
+  if (tid == 0) out[blockIdx.x] = T;
 }
 
 // One-query variant for the stage entry point: raw sums of one leaf.
@@ -3662,7 +3775,11 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   tail.rank = f.rank;
   tail.seed_count = f.seed_count;
   tail.seed_list = f.seed_list;
-  tail.seed_mask = f.seed_mask;
+  tail.seed_total = f.seed_total;
+  tail.seed_keys = f.seed_keys;
+  tail.seed_units = f.seed_units;
+  tail.seed_nunits = f.seed_nunits;
+  tail.leaf_size = ix.leaf_size;
   tail.seed = f.seed;
   tail.lut = LutParams{queries, ix.dim, ix.codebook, ix.nb, ix.dpb, LutRows(ix.ksteps), ix.metric,
                        ix.residual, (dbg & 2) ? nullptr : f.lut, f.mult, f.inv, nullptr};
@@ -3924,12 +4041,12 @@ hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStrea
                        wl ? *wl : WorklistArgs{}, sb);                                      \
     break;
 
-hipError_t LaunchSeedScan(const DeviceIndex& ix, const SeedArgs& a, hipStream_t s,
+hipError_t LaunchSeedScan(const DeviceIndex& ix, const SeedArgs& a, int blocks, hipStream_t s,
                           const WorklistArgs* wl) {
   static_assert(256 * kSeedPerThread == kSeedKeys, "the seed select holds kSeedKeys values");
   if (wl && wl->nl > kFusedWorklistLeaves) return hipErrorInvalidValue;
   if (a.seed < 1 || a.seed > kSeedMaxMfma) return hipErrorInvalidValue;
-  const int sb = (ix.nl + 3) / 4;   // one wave per leaf
+  const int sb = std::max(blocks, 1);   // 4-wave blocks walking the seed units
   const int nwl = wl ? (wl->nl + kWlPosPerBlock - 1) / kWlPosPerBlock : 0;
   switch (ix.ksteps) {
     SMX_SEED_SCAN_CASE(4)
@@ -3951,6 +4068,12 @@ hipError_t LaunchSeedScan(const DeviceIndex& ix, const SeedArgs& a, hipStream_t 
 hipError_t LaunchSeedSelect(const SeedArgs& a, int nq, hipStream_t s) {
   if (nq == 0) return hipSuccess;
   hipLaunchKernelGGL(seed_select_kernel, dim3(nq), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t LaunchKthKeys(const uint32_t* vals, int sets, int kk, uint64_t* out, hipStream_t s) {
+  if (sets <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kth_keys_kernel, dim3(sets), dim3(256), 0, s, vals, uint32_t(kk), out);
   return hipGetLastError();
 }
 

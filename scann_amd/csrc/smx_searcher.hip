@@ -79,10 +79,11 @@ int EffectiveKSteps(int nb) {
 //   [nl, 2 nl)         seeding queries per leaf (the seed scan's claims)
 //   [stats, +32)       stats words (SelectArgs::overflow and the work-list totals)
 struct CounterLayout {
-  uint32_t seeds, stats, words;
+  uint32_t seeds, units, stats, words;
   explicit CounterLayout(int nl) {
     seeds = uint32_t(nl) * smx::kCounterStride;       // nl strided leaf counters first
-    stats = 2u * uint32_t(nl) * smx::kCounterStride;  // then the seed counters
+    units = 2u * uint32_t(nl) * smx::kCounterStride;  // then the seed counters, the seed units'
+    stats = units + smx::kCounterStride;
     words = stats + 32u;
   }
 };
@@ -104,8 +105,9 @@ struct Workspace {
   float* mult = nullptr;
   float* inv = nullptr;
   uint32_t* counters = nullptr;     // see CounterLayout
-  uint32_t* seed_list = nullptr;    // [nl][kSeedSlots] the leaves' seeding queries
-  uint32_t* seed_mask = nullptr;    // [nq] granted seed leaves per query
+  uint64_t* seed_list = nullptr;    // [nl][kSeedSlots] the leaves' seeding queries
+  uint32_t* seed_total = nullptr;   // [nq][2] seed rows spanned, granted
+  uint32_t* seed_units = nullptr;   // [nq * kSeedMaxMfma * kSeedSpans] seed-scan wave units
   uint32_t* seed_keys = nullptr;    // [nq][kSeedKeys] seed distances
   uint32_t* rank = nullptr;         // [nq*L] each pair's position in its leaf's list
   uint32_t* leaf_item0 = nullptr;   // [nl] each leaf's first work item
@@ -125,7 +127,7 @@ struct Workspace {
   void Release() {
     DFree(queries); DFree(topl_leaf); DFree(topl_dist); DFree(scores); DFree(lut); DFree(mult);
     DFree(inv);
-    DFree(counters); DFree(seed_list); DFree(seed_mask); DFree(seed_keys); DFree(rank); DFree(leaf_item0); DFree(lanes); DFree(wave_start);
+    DFree(counters); DFree(seed_list); DFree(seed_total); DFree(seed_units); DFree(seed_keys); DFree(rank); DFree(leaf_item0); DFree(lanes); DFree(wave_start);
     DFree(pos_unit0); DFree(gunits); DFree(wl_part);
     DFree(work); DFree(tau); DFree(cand); DFree(cand_count); DFree(out_idx);
     DFree(out_dist);
@@ -157,6 +159,7 @@ struct smx_index {
   // LDS-lookup kernel (measured slower at glove shape: 0.180 vs 0.164 ms)
   bool seed_mfma = false;
   int grid = 0;                    // scan grid: resident one-wave workgroups (occupancy API)
+  int cus = 0;                     // compute units of the device
   bool profiling = false;
   bool use_graph = false;          // SMX_GRAPH=1: replay the pipeline as a hipGraph
   hipGraphExec_t graph_exec = nullptr;
@@ -421,7 +424,8 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
       (rc = DAlloc(&w.lut, size_t(anq) * smx::LutRows(ix.ksteps) * 16)) || (rc = DAlloc(&w.mult, anq)) ||
       (rc = DAlloc(&w.inv, anq)) || (rc = DAlloc(&w.counters, CounterLayout(nl).words)) ||
       (rc = DAlloc(&w.seed_list, size_t(nl) * smx::kSeedSlots)) ||
-      (rc = DAlloc(&w.seed_mask, size_t(anq))) ||
+      (rc = DAlloc(&w.seed_total, 2 * size_t(anq))) ||
+      (rc = DAlloc(&w.seed_units, size_t(anq) * smx::kSeedMaxMfma * smx::kSeedSpans)) ||
       (rc = DAlloc(&w.seed_keys, size_t(anq) * smx::kSeedKeys)) ||
       (rc = DAlloc(&w.rank, apairs)) || (rc = DAlloc(&w.leaf_item0, size_t(nl))) ||
       (rc = DAlloc(&w.lanes, size_t(max_items) * smx::kQueriesPerTile)) ||
@@ -531,8 +535,10 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sa.mfma = seed_mfma ? 1 : 0;
   sa.seed_count = w.counters + lay.seeds;
   sa.seed_list = w.seed_list;
-  sa.seed_mask = w.seed_mask;
+  sa.seed_total = w.seed_total;
   sa.seed_keys = w.seed_keys;
+  sa.seed_units = w.seed_units;
+  sa.seed_nunits = w.counters + lay.units;
   sa.nl = nl;
   sa.residual = ix.residual;
 
@@ -627,7 +633,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     // front end: state reset, partition scores, top-L + ranks + LUTs
     smx::FrontArgs f;
     f.init.counters = w.counters;
-    f.init.n_counters = 2u * uint32_t(nl);   // pair and seed counters
+    f.init.n_counters = 2u * uint32_t(nl) + 1u;   // pair, seed and seed-unit counters
     f.init.stats = stats;
     f.init.n_stats = 32u;
     f.init.cand_count = w.cand_count;
@@ -643,7 +649,10 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     if (seed_mfma) {
       f.seed_count = w.counters + lay.seeds;
       f.seed_list = w.seed_list;
-      f.seed_mask = w.seed_mask;
+      f.seed_total = w.seed_total;
+      f.seed_keys = w.seed_keys;
+      f.seed_units = w.seed_units;
+      f.seed_nunits = w.counters + lay.units;
       f.seed = seed;
     }
     SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s, &f));
@@ -656,7 +665,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
           stats + 3, code_bytes, h->chunk_tiles, narrow, bd);
       Mark(h, 3, s);
       if (seed_mfma)
-        SMX_HIP(smx::LaunchSeedScan(ix, sa, s, &wla));
+        SMX_HIP(smx::LaunchSeedScan(ix, sa, 2 * h->cus, s, &wla));
       else
         SMX_HIP(smx::LaunchSeed(ix, sa, nq, s, &wla));
       Mark(h, 4, s);
@@ -672,7 +681,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
       // it; the shorter work-list branch pays the cross-queue edges.
       SMX_HIP(hipEventRecord(h->fork_ev, s));
       if (seed_mfma)
-        SMX_HIP(smx::LaunchSeedScan(ix, sa, s));
+        SMX_HIP(smx::LaunchSeedScan(ix, sa, 2 * h->cus, s));
       else
         SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
       Mark(h, 4, s);
@@ -918,6 +927,7 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
     int per_cu = 0;
     SMX_HIP(smx::ScanBlocksPerCU(h->ix, &per_cu));
     h->grid = prop.multiProcessorCount * std::max(1, per_cu);
+    h->cus = prop.multiProcessorCount;
   }
   if (hipHostMalloc(reinterpret_cast<void**>(&h->host_stats), 32 * sizeof(uint32_t)) != hipSuccess) {
     smx_index_destroy(h);
@@ -1036,6 +1046,15 @@ int smx_nearest_centers(const float* x, int64_t n, int32_t d, const float* cente
   if (!(lambda >= 0.0f)) return Fail(SMX_INVALID_ARGUMENT, "lambda must be >= 0");
   SMX_HIP(smx::LaunchNearestCenters(x, n, d, centers, k, primary, lambda, out, out_loss,
                                     static_cast<hipStream_t>(stream)));
+  return SMX_OK;
+}
+
+int smx_kth_threshold_keys(const uint32_t* vals, int32_t sets, int32_t kk, uint64_t* out,
+                           void* stream) {
+  if (sets < 0 || kk < 0) return Fail(SMX_INVALID_ARGUMENT, "need sets >= 0, kk >= 0");
+  if (sets == 0) return SMX_OK;
+  if (!vals || !out) return Fail(SMX_INVALID_ARGUMENT, "null input or output buffer");
+  SMX_HIP(smx::LaunchKthKeys(vals, sets, kk, out, static_cast<hipStream_t>(stream)));
   return SMX_OK;
 }
 

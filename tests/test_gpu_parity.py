@@ -331,16 +331,3 @@ def test_single_query_search_matches_oracle(native, oracle, fix, reorder, reques
         np.testing.assert_array_equal(gd[:gc].view(np.uint32), od[0, :gc].view(np.uint32))
 
 
-def _nat_env(native, ix, env):
-    """A handle created with the given switches (read at handle creation)."""
-    import os
-    old = {k: os.environ.get(k) for k in env}
-    try:
-        os.environ.update(env)
-        return native.NativeIndex(ix)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
