@@ -71,8 +71,8 @@ CONFIGS = {
     # configs[3] / configs[4]: generated on the device (scann_amd/generate.py),
     # range split; at N=1 this GPU holds rank 0's shard of the `split`-way split
     "soar100m": dict(n=100_000_000, leaves=10000, leaves_to_search=100, metric=0, seed=4,
-                     generated=True, split=8, soar=1.5, dim=96, components=4096,
-                     train_sample=250_000, sweep=[20, 40, 60, 100],
+                     generated=True, split=8, soar=1.5, dim=96, components=512, spread=1.6,
+                     train_sample=250_000, sweep=[20, 40, 60, 100, 150, 200],
                      parity_points=[(100, 100), (1000, 256)],
                      workload="configs[3]: synthetic 100M x 96 dot product + SOAR (lambda 1.5, "
                               "overretrieve 2), tree-AH 10000 leaves, LUT16 AH 48 blocks x 2 "
@@ -80,7 +80,9 @@ CONFIGS = {
                               "range split 8 ways: one rank's shard (12.5M rows, 25M members) "
                               "+ the merge of 8 shard lists",
                      data="synthetic, generated on the device (Philox per 65536-row chunk, "
-                          "4096-component unit-norm mixture; SURVEY §8d)",
+                          "512 broad components (noise norm 1.6 against unit means: each "
+                          "spans ~20 leaves, so recall rises with leaves_to_search), unit "
+                          "norm; SURVEY §8d)",
                      metric_name="QPS per GPU of a range-split rank, configs[3] (100M x 96 "
                                  "dot + SOAR, 10000 leaves, 8-way split), batch=1000"),
     "deep1b": dict(n=1_000_000_000, leaves=50000, leaves_to_search=400, metric=0, seed=5,
@@ -574,7 +576,7 @@ def main_generated(args, rank, world, local, dist, dev):
     n = args.n if args.n != 1_183_514 else CFG["n"]
     t = time.time()
     ds = generate.GeneratedDataset(n, CFG["dim"], CFG["seed"], components=CFG["components"],
-                                   device=dev)
+                                   spread=CFG.get("spread", 0.9), device=dev)
     torch.cuda.synchronize()
     t_build = time.perf_counter()
     ix = generate.build_generated_shard(

@@ -17,7 +17,8 @@ from .index import IndexDesc
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SMX_LIB: an alternative build of the same library (tuning experiments)
-LIB_PATH = os.environ.get("SMX_LIB") or os.path.join(_HERE, "lib", "libscann_mi355x.so")
+PRODUCT_LIB = os.path.join(_HERE, "lib", "libscann_mi355x.so")
+LIB_PATH = os.environ.get("SMX_LIB") or PRODUCT_LIB
 
 SMX_OK = 0
 
@@ -106,9 +107,15 @@ def load(path: str = LIB_PATH):
         pass
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
-        fn.restype = res
-        fn.argtypes = args
+        # a library built from an older source (an A/B of $SMX_LIB builds)
+        # may predate an entry point: it then fails when called, not here;
+        # the product library exports every one (tests/test_capi.py)
+        fn = getattr(lib, name, None)
+        if fn is None and os.path.abspath(path) == PRODUCT_LIB:
+            raise ImportError(f"{path} does not export {name}: rebuild it")
+        if fn is not None:
+            fn.restype = res
+            fn.argtypes = args
     _lib = lib
     return lib
 

@@ -640,7 +640,8 @@ __device__ void TopLFinish(int qi, int L, uint32_t m, const uint64_t* sel, int32
 // Exact top-L by (score, center index) with one NT-thread block per query,
 // the row in registers (VPT scores per thread, nl <= NT * VPT; a block per
 // query, not a wave: 1000 queries must fill 1024 SIMDs several waves deep;
-// NT = 1024 for 10^4 - 1.6 * 10^4 leaves; above, topl_sample_kernel).  Linear 256-bin histograms of the
+// NT = 1024 up to 1.6 * 10^4 leaves when L > 256 rules the sampled kernel out;
+// above kSampleTopLMinLeaves leaves, topl_sample_kernel).  Linear 256-bin histograms of the
 // ordered score bits between the boundary set's [LO, HI] (radix digits of
 // nearby floats would all hit one bin) narrow down to the bin holding the
 // L-th score until at most 256 keys are left.  The boundary set is always a
@@ -962,6 +963,7 @@ __device__ __forceinline__ void BinRange(uint32_t b, uint64_t scale, uint32_t& l
 // register kernel spilled 56 VGPRs at 52 scores per thread).
 constexpr int kSampleVals = 8;          // samples per thread (2048 per query)
 constexpr uint32_t kSampleCap = 16384;   // most LDS keys (128 KB)
+constexpr int kSampleTopLMinLeaves = 4096;   // the sampled top-L above this many leaves
 
 __device__ uint32_t BlockKthOfSamples(const uint32_t (&v)[kSampleVals], uint32_t kk) {
   __shared__ uint32_t hist[256], wsum[4], s_lo[4], s_hi[4], s_bin, s_below;
@@ -1413,6 +1415,8 @@ __device__ void WorklistFusedBlock(const WorklistArgs& w, int b) {
   __shared__ uint32_t s_ex_i[kWlPosPerBlock], s_ex_u[kWlPosPerBlock + 1];
   __shared__ unsigned long long red[4][3];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // (phase stamps of block 0: start, leaf_item0 written, end)
+  if (b == 0) SMX_PHASE(1, kPhaseQueries - 1, 0);
   const int nl = w.nl, p0 = tid * kWlPerThread;
   const int pb = b * kWlPosPerBlock, pe = min(nl, pb + kWlPosPerBlock);
   uint32_t leafv[kWlPerThread], itv[kWlPerThread], unv[kWlPerThread];
@@ -1493,9 +1497,11 @@ __device__ void WorklistFusedBlock(const WorklistArgs& w, int b) {
     eu += unv[k];
     prev_un = unv[k];
   }
+  if (b == 0) SMX_PHASE(1, kPhaseQueries - 1, 1);   // (leaf_item0 written)
   __syncthreads();
   for (int p = pb + wid; p < pe; p += 4)
     ItemsCore(w, p, lane, s_gunits, s_ex_i[p - pb], s_ex_u[p - pb], s_ex_u[p - pb + 1]);
+  if (b == 0) SMX_PHASE(1, kPhaseQueries - 1, 2);
 }
 
 // ---------------------------------------------------------------------------
@@ -1599,20 +1605,40 @@ constexpr int kSeedSel = 1024;       // values under the minima bound ranked exa
 // in its wave's order plus, per other wave, the number of that wave's keys
 // below it (binary search of the sorted run).  Block-wide (every thread
 // calls); sbuf holds 256 keys.
+// The value of lane (lane ^ J): DPP quad permutes for J = 1, 2, ds_swizzle
+// (bit-mask mode, no LDS access) for J = 4, 8, 16, one ds_bpermute for 32.
+template <int J>
+__device__ __forceinline__ uint32_t LaneXor(uint32_t v) {
+  if constexpr (J == 1)
+    return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0xB1, 0xF, 0xF, false));
+  else if constexpr (J == 2)
+    return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x4E, 0xF, 0xF, false));
+  else if constexpr (J <= 16)
+    return uint32_t(__builtin_amdgcn_ds_swizzle(int(v), 0x1F | (J << 10)));
+  else
+    return uint32_t(__shfl_xor(int(v), J));
+}
+
+template <int K, int J>
+__device__ __forceinline__ void BitonicStep(uint64_t& v, int lane) {
+  const uint32_t lo = LaneXor<J>(uint32_t(v));
+  const uint32_t hi = LaneXor<J>(uint32_t(v >> 32));
+  const uint64_t o = (uint64_t(hi) << 32) | lo;
+  const bool up = (lane & K) == 0, low = (lane & J) == 0;
+  v = (low == up) ? (o < v ? o : v) : (o > v ? o : v);
+  if constexpr (J > 1) BitonicStep<K, J / 2>(v, lane);
+}
+
+template <int K>
+__device__ __forceinline__ void BitonicStages(uint64_t& v, int lane) {
+  BitonicStep<K, K / 2>(v, lane);
+  if constexpr (K < 64) BitonicStages<K * 2>(v, lane);
+}
+
 __device__ uint32_t BlockRank256(uint64_t key, uint64_t* sbuf) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint64_t v = key;
-#pragma unroll
-  for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const uint32_t lo = uint32_t(__shfl_xor(int(uint32_t(v)), j));
-      const uint32_t hi = uint32_t(__shfl_xor(int(uint32_t(v >> 32)), j));
-      const uint64_t o = (uint64_t(hi) << 32) | lo;
-      const bool up = (lane & k) == 0, low = (lane & j) == 0;
-      v = (low == up) ? (o < v ? o : v) : (o > v ? o : v);
-    }
-  }
+  BitonicStages<2>(v, lane);
   sbuf[threadIdx.x] = v;
   __syncthreads();
   uint32_t r = 0;
@@ -1829,9 +1855,11 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
   return T;
 }
 
-// Per query: its threshold key (SeedTau).
 // Per query: its threshold key (SeedTau); blocks from nq on build the work
-// list (WorklistFusedBlock).
+// list (WorklistFusedBlock).  (Work-list blocks first, with the pair scatter
+// in the seed blocks behind a release flag from block 0, measured slower:
+// block 0 published leaf_item0 only 48.7 us after its start beside the seed
+// blocks -- tools/phase_stamps.py)
 template <int K>
 __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a, WorklistArgs w, int nq) {
   const int qi = blockIdx.x;
@@ -2751,17 +2779,18 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
 // to the group's largest budget, storing each query's distances of rows dp <
 // c as ordered bits at seed_keys[q][o + dp] -- the same values, in the same
 // places, as SeedTau ranks: d = fl(fl(S inv) + bias), the scan's distance, so
-// the kk-th of them bounds the final kk-th from above.  Blocks from
-// `seed_blocks` on build the work list (WorklistFusedBlock), as the per-query
-// seed launch does.
+// the kk-th of them bounds the final kk-th from above.  Wave w of the seed
+// blocks takes units w, w + stride, ..., their records loaded ahead.  Blocks below
+// `wl_blocks` build the work list (WorklistFusedBlock), as the per-query seed
+// launch does -- first, so that they are resident beside the seed waves.
 // ---------------------------------------------------------------------------
 static_assert(kSeedSpans <= 16 && kSeedSlots / 16 <= 4, "seed unit fields");
 
 template <int K>
 __global__ void __launch_bounds__(256) seed_scan_kernel(SeedArgs a, WorklistArgs w,
-                                                        int seed_blocks) {
-  if (int(blockIdx.x) >= seed_blocks) {   // the fused work-list blocks
-    WorklistFusedBlock(w, int(blockIdx.x) - seed_blocks);
+                                                        int wl_blocks) {
+  if (int(blockIdx.x) < wl_blocks) {   // the fused work-list blocks
+    WorklistFusedBlock(w, int(blockIdx.x));
     return;
   }
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
@@ -2786,21 +2815,39 @@ __global__ void __launch_bounds__(256) seed_scan_kernel(SeedArgs a, WorklistArgs
   const uint32_t lane_off = uint32_t((lane >> 5) * 32 + (lane & 15)) * uint32_t(W);
   const uint32_t sh = uint32_t((lane >> 4) & 1) * 8u;
   const uint32_t rg = uint32_t(lane >> 4);   // D rows 4 rg + e of column lane % 16
-  for (uint32_t u = uint32_t(blockIdx.x) * 4u + uint32_t(wid); u < nunits;
-       u += uint32_t(seed_blocks) * 4u) {   // (wave-uniform)
-    const uint32_t ur = a.seed_units[u];
-    const uint32_t leaf = ur >> 6, g = ((ur >> 4) & 3u) * 16u, row0 = (ur & 15u) * 256u;
-    const uint32_t cnt = min(a.seed_count[size_t(leaf) * kCounterStride], uint32_t(kSeedSlots));
-    const uint32_t sl = g + uint32_t(lane & 15);
-    const bool valid = sl < cnt;
-    const uint64_t rec = valid ? a.seed_list[size_t(leaf) * kSeedSlots + sl] : 0ull;
+  // units u0, u0 + stride, ... of this wave, two stages ahead: the unit
+  // record of the one after next and the leaf records of the next are in
+  // flight while this one runs
+  const uint32_t stride = (gridDim.x - uint32_t(wl_blocks)) * 4u;
+  uint32_t u = (blockIdx.x - uint32_t(wl_blocks)) * 4u + uint32_t(wid);
+  const uint32_t sl16 = uint32_t(lane & 15);
+  auto unit_rec = [&](uint32_t v) { return v < nunits ? a.seed_units[v] : 0u; };
+  struct LeafRecs {
+    uint32_t ur, cnt;
+    uint64_t rec, toff;
+  };
+  auto leaf_recs = [&](uint32_t ur) {   // (slots past the count hold stale records)
+    const uint32_t leaf = ur >> 6, g = ((ur >> 4) & 3u) * 16u;
+    return LeafRecs{ur, a.seed_count[size_t(leaf) * kCounterStride],
+                    a.seed_list[size_t(leaf) * kSeedSlots + g + sl16], a.tile_off[leaf]};
+  };
+  LeafRecs nxt = leaf_recs(unit_rec(u));
+  uint32_t ur2 = unit_rec(u + stride);
+  for (; u < nunits; u += stride) {   // (wave-uniform)
+    const LeafRecs cur = nxt;
+    nxt = leaf_recs(ur2);
+    ur2 = unit_rec(u + 2u * stride);
+    const uint32_t g = ((cur.ur >> 4) & 3u) * 16u, row0 = (cur.ur & 15u) * 256u;
+    const uint32_t cnt = min(cur.cnt, uint32_t(kSeedSlots));
+    const bool valid = g + sl16 < cnt;
+    const uint64_t rec = valid ? cur.rec : 0ull;
     const uint32_t qi = uint32_t(rec) & 0xFFFFFFu, si = uint32_t(rec) >> 24;
     const uint32_t o = uint32_t(rec >> 32) & 0xFFFFu, c = uint32_t(rec >> 48);
     uint32_t need = c;   // the group's largest budget
     for (int off = 8; off > 0; off >>= 1) need = max(need, uint32_t(__shfl_xor(int(need), off)));
     if (need <= row0) continue;
     const uint32_t tiles = min(uint32_t(T), (need - row0 + 31u) / 32u);
-    const uint8_t* tseg = a.tiles + (a.tile_off[leaf] + row0 / 32u) * 64ull * W;
+    const uint8_t* tseg = a.tiles + (cur.toff + row0 / 32u) * 64ull * W;
     uint32_t ca[T][NW], cb[T][NW];
 #pragma unroll
     for (int i = 0; i < T; ++i) {
@@ -3802,11 +3849,10 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   } else if (L <= kWaveTopL && ix.nl <= 256 * 8) {
     hipLaunchKernelGGL((topl_block_kernel<8, 256>), dim3(nq), dim3(256), 0, s, scores, ix.nl, L,
                        out_leaf, out_dist, tail);
-  } else if (L <= kWaveTopL && ix.nl <= 1024 * 16) {
-    hipLaunchKernelGGL((topl_block_kernel<16, 1024>), dim3(nq), dim3(1024), 0, s, scores, ix.nl,
-                       L, out_leaf, out_dist, tail);
-  } else if (ix.nl > 1024 * 16 && L <= 4096) {
-    // many leaves (configs[4]): the sampled threshold, exact
+  } else if (ix.nl > kSampleTopLMinLeaves && L <= 4096) {
+    // many leaves (configs[3]'s 10^4, configs[4]'s 5 x 10^4): the sampled
+    // threshold, exact (same box A/B at 10^4 leaves, L = 100: partition
+    // stage 116 -> 106 us against topl_block_kernel<16, 1024>)
     uint32_t lcap = 1;
     while (lcap < uint32_t(std::min(L, ix.nl))) lcap <<= 1;
     // LDS keys: the compacted keys (expected 1.5 L + 16 nl / 2048, room for
@@ -3819,6 +3865,9 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
     const size_t lds_s = size_t(std::max(cap, lcap)) * 8;
     hipLaunchKernelGGL(topl_sample_kernel, dim3(nq), dim3(256), lds_s, s, scores, ix.nl, L, lcap,
                        cap, out_leaf, out_dist, tail);
+  } else if (L <= kWaveTopL && ix.nl <= 1024 * 16) {
+    hipLaunchKernelGGL((topl_block_kernel<16, 1024>), dim3(nq), dim3(1024), 0, s, scores, ix.nl,
+                       L, out_leaf, out_dist, tail);
   } else if (ix.nl <= kLdsSelectLeaves && lds + kStaticLds <= 160 * 1024) {
     hipLaunchKernelGGL(topl_select_kernel, dim3(nq), dim3(256), lds, s, scores, ix.nl, L, kcap,
                        out_leaf, out_dist, tail);
@@ -4038,7 +4087,7 @@ hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStrea
 #define SMX_SEED_SCAN_CASE(KV)                                                              \
   case KV:                                                                                 \
     hipLaunchKernelGGL(seed_scan_kernel<KV>, dim3(sb + nwl), dim3(256), 0, s, a,            \
-                       wl ? *wl : WorklistArgs{}, sb);                                      \
+                       wl ? *wl : WorklistArgs{}, nwl);                                     \
     break;
 
 hipError_t LaunchSeedScan(const DeviceIndex& ix, const SeedArgs& a, int blocks, hipStream_t s,

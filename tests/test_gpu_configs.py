@@ -8,7 +8,7 @@ as well).  The oracle's result for a query does not depend on the other
 queries of the batch, so a subset is a complete check of those queries.
 
   configs[1] glove-100-angular: 1,183,514 x 100 dot, 1000 leaves, L=100,
-             nq=1000, reorder 100, k=10 (lut16_scan_kernel<25>)
+             nq=1000, reorder 100, k=10 (lut16_scan_kernel<26>)
   configs[2] SIFT1M: squared L2, non-residual, 2000 leaves, D=128
              (lut16_scan_kernel<32>), 300k rows
   configs[3] 100M x 96 dot + SOAR, 10000 leaves, range split over 8 ranks:

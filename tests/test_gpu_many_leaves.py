@@ -47,8 +47,8 @@ def native():
     return _native
 
 
-@pytest.mark.parametrize("nl,metric", [(1000, 0), (2048, 1), (5000, 0), (20000, 0), (20000, 1),
-                                       (50000, 0)])
+@pytest.mark.parametrize("nl,metric", [(1000, 0), (2048, 1), (5000, 0), (10000, 1), (20000, 0),
+                                       (20000, 1), (50000, 0)])
 def test_partition_topl_many_leaves(native, oracle, nl, metric):
     ix, q = _random_index(nl, 2 * nl, 16, metric, seed=nl + metric)
     n = native.NativeIndex(ix)
@@ -75,7 +75,7 @@ def test_partition_topl_all_ties(native, oracle, nl):
         np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
 
 
-@pytest.mark.parametrize("nl,metric", [(20000, 0), (50000, 0), (20000, 1), (70000, 0)])
+@pytest.mark.parametrize("nl,metric", [(10000, 0), (20000, 0), (50000, 0), (20000, 1), (70000, 0)])
 def test_search_many_leaves_matches_oracle(native, oracle, nl, metric):
     """(70000 leaves: past 65536, the work list's block sums take two
     rounds and the global top-N shift drops to 15.)"""

@@ -42,7 +42,13 @@ def main():
         nat.search_batched_device(qd.data_ptr(), NQ, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True,
                                   oi.data_ptr(), od.data_ptr(), None)
     torch.cuda.synchronize()
-    r = np.fromfile(path, dtype=np.uint64).reshape(3, 4096, 8)[:, :NQ].astype(np.int64)
+    full = np.fromfile(path, dtype=np.uint64).reshape(3, 4096, 8).astype(np.int64)
+    r = full[:, :NQ]
+    wl0 = full[1, 4095, :3]   # the fused work list's block 0: start, leaf_item0 written, end
+    if (wl0 > 0).all():
+        t0 = r[1][(r[1][:, 0] > 0), 0].min()
+        print("work-list block 0 (us from the first seed block's start): start %.1f, "
+              "leaf_item0 written %.1f, end %.1f" % tuple((wl0 - t0) / 100.0))
     for kid, (name, phases) in NAMES.items():
         t = r[kid]
         n = len(phases) + 1
