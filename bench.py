@@ -72,7 +72,8 @@ CONFIGS = {
     # range split; at N=1 this GPU holds rank 0's shard of the `split`-way split
     "soar100m": dict(n=100_000_000, leaves=10000, leaves_to_search=100, metric=0, seed=4,
                      generated=True, split=8, soar=1.5, dim=96, components=512, spread=1.6,
-                     train_sample=250_000, sweep=[20, 40, 60, 100, 150, 200],
+                     train_sample=250_000,
+                     sweep=[20, 40, 60, 100, 150, 200, [100, 256], [200, 256], [400, 256]],
                      parity_points=[(100, 100), (1000, 256)],
                      workload="configs[3]: synthetic 100M x 96 dot product + SOAR (lambda 1.5, "
                               "overretrieve 2), tree-AH 10000 leaves, LUT16 AH 48 blocks x 2 "
