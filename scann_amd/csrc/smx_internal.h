@@ -29,6 +29,9 @@ constexpr int kSeedMaxMfma = 32;   // seed leaves per query on the seed scan
 // a seed-scan unit: one wave, 16 queries of a leaf x 256 rows (8 tiles)
 constexpr int kSeedSpans = kSeedKeys / 256;
 constexpr uint32_t kItemNarrow = 1u << 31;
+// WorklistArgs::narrow / SeedArgs::narrow: 0 = 32-slot tiles only, 1 = a
+// leaf's last <= 16 queries in a 16-slot tile, kNarrowOnly = 16-slot tiles only
+constexpr uint32_t kNarrowOnly = 2;
 // 16-slot tiles are used when a call averages fewer queries per leaf
 // (nq * L / num_leaves) than this
 constexpr int kNarrowQueriesPerLeaf = 32;
@@ -181,6 +184,7 @@ struct SeedArgs {
   uint32_t* seed_keys;         // [nq][kSeedKeys] ordered distances (SeedClaims' layout)
   const uint32_t* seed_units;  // leaf << 6 | group << 4 | span, one per wave unit
   const uint32_t* seed_nunits; // their number (a counter)
+  uint32_t narrow;             // the work list's tile mode (kNarrowOnly: 16-slot query tiles)
   int nl;
   // the inversion (pair scatter): every (query, leaf) pair's slot in its
   // leaf's work items
@@ -358,7 +362,7 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count,
 // holds 16-slot items); 4: the same without its threshold epilogue (timing
 // ablation, results invalid; the diagnostic variants take 32-slot items only).
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,
-                      hipStream_t s, bool narrow);
+                      hipStream_t s, uint32_t narrow);
 // Resident scan workgroups per CU (occupancy of the index's instantiation).
 hipError_t ScanBlocksPerCU(const DeviceIndex& ix, int* blocks);
 // The per-query thresholds (tau_key) from the seed leaves.

@@ -1143,8 +1143,10 @@ __device__ __forceinline__ uint2 ChunkTiles(uint32_t n, uint32_t chunk_tiles, ui
 // 2 units, a 16-slot item's 1; the shares cut the units, and a tile belongs
 // to the share that holds its first unit.
 // ---------------------------------------------------------------------------
-// 32-slot and 16-slot query tiles of a leaf with c queries.
+// 32-slot and 16-slot query tiles of a leaf with c queries (narrow 1: a
+// remainder of at most 16 queries in a 16-slot tile; 2: 16-slot tiles only).
 __device__ __forceinline__ uint2 LeafQueryTiles(uint32_t c, uint32_t narrow) {
+  if (narrow == kNarrowOnly) return make_uint2(0u, (c + kNarrowSlots - 1u) / kNarrowSlots);
   const uint32_t full = c / uint32_t(kQueriesPerTile), r = c % uint32_t(kQueriesPerTile);
   if (r == 0) return make_uint2(full, 0u);
   if (narrow && r <= uint32_t(kNarrowSlots)) return make_uint2(full, 1u);
@@ -1327,9 +1329,10 @@ __device__ void WaveStarts(const WorklistArgs& w, int p, const uint32_t* gunits,
         ++q;
         j = 0;
       }
-    } else {                         // in the 16-slot tile
-      q = qt.x;
-      j = off - 2u * tiles * qt.x;
+    } else {                         // in the 16-slot tiles (one unit per tile)
+      const uint32_t o16 = off - 2u * tiles * qt.x;
+      q = qt.x + o16 / tiles;
+      j = o16 % tiles;
     }
     uint32_t ch = 0;
     if (q < qt.x + qt.y)
@@ -1379,7 +1382,9 @@ __device__ void ItemsCore(const WorklistArgs& w, int p, int lane, const uint32_t
   }
   if (qt) {
     const uint32_t slots = qts.y ? uint32_t(kNarrowSlots) : uint32_t(kQueriesPerTile);
-    const uint32_t first = c - (qt - 1) * kQueriesPerTile;   // empty slots [first, slots)
+    // empty slots [first, slots) of the last query tile
+    const uint32_t first = qts.y ? c - qts.x * kQueriesPerTile - (qts.y - 1u) * kNarrowSlots
+                                 : c - (qt - 1) * kQueriesPerTile;
     const uint32_t ne = slots - first;
     for (uint32_t e = lane; e < ne * chunks; e += 64) {
       ItemLane v;
@@ -1562,6 +1567,12 @@ __device__ __forceinline__ v16i TileSums(const uint32_t* codes, const v4i* frag)
   }
   return acc;
 }
+
+// NW code words as one vector value (dword-aligned): a ring slot kept as a
+// register tuple, so that the allocator does not split it across a loop
+// back edge (a split copies the words -- and waits for their load).
+template <int N>
+using CodeVec = uint32_t __attribute__((ext_vector_type(N), aligned(4)));
 
 template <int K>
 __device__ __forceinline__ void LoadCodes(const uint8_t* p, uint32_t* codes) {
@@ -1906,10 +1917,12 @@ __device__ __forceinline__ void PairScatterTau(const SeedArgs& a, size_t p,
                                : SumLimit(FromOrdered(uint32_t(tau >> 32)), v.inv, v.bias,
                                           -128 * a.nb, 128 * a.nb);
   SMX_CHECK(leaf, a.bd.nl, "pair leaf");
-  const uint32_t w0 = leaf_item0[leaf] + (r / kQueriesPerTile) * chunks;
+  // query tile r / ts, slot r % ts (16-slot tiles only: ts = 16)
+  const uint32_t ts = a.narrow == kNarrowOnly ? uint32_t(kNarrowSlots) : uint32_t(kQueriesPerTile);
+  const uint32_t w0 = leaf_item0[leaf] + (r / ts) * chunks;
   for (uint32_t ch = 0; ch < chunks; ++ch) {
     SMX_GUARD(w0 + ch, a.bd.items, "pair lane")
-    a.lanes[size_t(w0 + ch) * kQueriesPerTile + (r % kQueriesPerTile)] = v;
+    a.lanes[size_t(w0 + ch) * kQueriesPerTile + (r % ts)] = v;
   }
 }
 
@@ -2255,9 +2268,9 @@ __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32
   }
 }
 
-// NRW: the work list may hold 16-slot items (the 16-slot path is compiled
-// in); without it only the 32-slot path exists (fewer registers and code).
-template <int K, int ABL = 0, bool NRW = false>
+// NRW: 0 = 32-slot items only (only that path is compiled in: fewer
+// registers and code), 1 = both kinds, kNarrowOnly = 16-slot items only.
+template <int K, int ABL = 0, int NRW = 0>
 __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(ScanArgs a) {
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
   constexpr int W = 4 * NW;
@@ -2475,8 +2488,10 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         LoadCodes<K>(tile_ptr(t), ca);
         if constexpr (NR) LoadCodes<K>(tile_ptr(t) + 16 * W, cbb);
       };
+      // (the 16-slot-only kernel loads its tiles in its own ring below)
+      constexpr bool DEEP = NR && NRW == int(kNarrowOnly);
       load_b();
-      load_codes(j, codes, codes_b);
+      if constexpr (!DEEP) load_codes(j, codes, codes_b);
       // the claimed-ahead segment's item and query ids, for its setup
       {
         const uint32_t sn = __builtin_amdgcn_readfirstlane(sg_next);
@@ -2674,67 +2689,159 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       // a hit list over half full is drained between tiles with the B
       // fragments dead (reloaded after, from L2): the drain's registers
       // then never compete with them (rare: ~1 hit lane per tile)
+      // (the 16-slot-only kernel keeps its B fragments through the drain: a
+      // reload there would add loads to one side of the join, and the ring's
+      // in-flight code loads would be waited for at the join)
       auto drain_mid = [&]() {
         if (whits > 64u) {
           drain();
           whits = 0;
-          load_b();
+          if constexpr (!DEEP) load_b();
+          // (DEEP: nothing left in flight on this rare path, so that the
+          // join keeps the ring's exact load counts -- the drain's stores
+          // would otherwise make every later wait on the ring vmcnt(0))
+          if constexpr (DEEP) __builtin_amdgcn_s_waitcnt(0);
         }
       };
 
       if (ABL & 8) st_t1 = __builtin_amdgcn_s_memtime();
-      // the tiles this wave takes, a claimed pair at a time with the next
-      // pair claimed ahead; two code buffers in turn (the load of the next
-      // tile is in flight while this one computes; a rotating copy would
-      // force a wait for it at the copy)
-      uint32_t pe = min(j + 2, end);        // the current pair [.., pe)
-      uint32_t na_raw = claim2(sg);          // the next pair (lane 0)
-      bool na_known = false;
-      uint32_t na = end;
-      auto next_tile = [&](uint32_t t, uint32_t& tn) -> bool {
-        if (t + 1 < pe) {
-          tn = t + 1;
-          return true;
-        }
-        if (!na_known) {
-          na = __builtin_amdgcn_readfirstlane(na_raw);
-          na_known = true;
-        }
-        if (na >= end) return false;
-        tn = na;
-        return true;
-      };
-      auto advance = [&](uint32_t t, uint32_t tn) {
-        if (!(t + 1 < pe)) {   // moved into the pair claimed ahead: claim another
-          pe = min(tn + 2, end);
+      if constexpr (DEEP) {
+        // 16-slot tiles only (few queries per leaf: a tile's MFMA work is
+        // small against its code load): a ring of D tiles in flight per wave
+        // instead of one, the registers freed by the 32-slot path's B
+        // fragments.  The tiles come from the same pair claims (the current
+        // pair, then the pair claimed ahead); every refill issues its load
+        // unconditionally (the last tile again at the end), so the wait for a
+        // slot's codes leaves the later slots' loads in flight.
+        constexpr int D = NW <= 3 ? 4 : 3;
+        uint32_t cur = j, pe = min(j + 2, end), na = end;
+        uint32_t na_raw = claim2(sg);
+        bool na_known = false;
+        auto produce = [&](uint32_t& tn) -> bool {   // the tile after the last produced one
+          if (cur + 1 < pe) {
+            tn = ++cur;
+            return true;
+          }
+          if (!na_known) {
+            na = __builtin_amdgcn_readfirstlane(na_raw);
+            na_known = true;
+          }
+          if (na >= end) return false;
+          cur = na;
+          pe = min(na + 2, end);
           na_raw = claim2(sg);
           na_known = false;
+          tn = cur;
+          return true;
+        };
+        using CV = CodeVec<NW>;
+        CV ra[D], rb[D];
+        uint32_t tq[D];
+        bool ok[D];
+        auto load_slot = [&](uint32_t t, CV& x, CV& y) {
+          const uint8_t* p = tile_ptr(t);
+          x = *reinterpret_cast<const CV*>(p);
+          y = *reinterpret_cast<const CV*>(p + 16 * W);
+        };
+        tq[0] = j;
+        ok[0] = true;
+        load_slot(j, ra[0], rb[0]);
+#pragma unroll
+        for (int d = 1; d < D; ++d) {
+          ok[d] = ok[d - 1] && produce(tq[d]);
+          if (!ok[d]) tq[d] = tq[d - 1];
+          load_slot(tq[d], ra[d], rb[d]);
         }
-      };
-      {
-        uint32_t cb[NW], cb_b[NW];
-        uint32_t t = j, tn = 0;
+        // one ring slot: its tile (when it holds one), then its refill -- the
+        // tile after the last produced one.  The loop leaves only at the
+        // bottom, when slot 0 is empty (the slots empty in order): early
+        // exits between the slots put the ring's registers through merges
+        // that cost exact load counts (every wait became vmcnt(0/1)).
+        bool live = true;
+        auto step = [&](auto dc) {
+          constexpr int d = decltype(dc)::value;
+          if (ok[d]) {
+            uint32_t xa[NW], xb[NW];
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+              xa[i] = ra[d][i];
+              xb[i] = rb[d][i];
+            }
+            tile(xa, xb, tq[d]);
+            ++tiles_done;
+            if (pending) {   // after the segment's first tile (its stores: as the drain's)
+              copy_prev();
+              __builtin_amdgcn_s_waitcnt(0);
+            }
+          }
+          const uint32_t prev = tq[(d + D - 1) % D];
+          ok[d] = live && produce(tq[d]);
+          live = ok[d];
+          if (!ok[d]) tq[d] = prev;
+          load_slot(tq[d], ra[d], rb[d]);
+          drain_mid();
+        };
         for (;;) {
-          bool more = next_tile(t, tn);
-          // unconditional (the current tile again when none follows): one
-          // load per tile on every path, so the wait for this tile's codes
-          // leaves the next tile's load in flight (vmcnt(1), not vmcnt(0))
-          load_codes(more ? tn : t, cb, cb_b);
-          tile(codes, codes_b, t);
-          ++tiles_done;
-          if (pending) copy_prev();   // after the segment's first tile: the atomic has returned
-          if (!more) break;
-          drain_mid();
-          advance(t, tn);
-          t = tn;
-          more = next_tile(t, tn);
-          load_codes(more ? tn : t, codes, codes_b);
-          tile(cb, cb_b, t);
-          ++tiles_done;
-          if (!more) break;
-          drain_mid();
-          advance(t, tn);
-          t = tn;
+          step(std::integral_constant<int, 0>{});
+          step(std::integral_constant<int, 1>{});
+          step(std::integral_constant<int, 2>{});
+          if constexpr (D > 3) step(std::integral_constant<int, 3>{});
+          if (!ok[0]) break;
+        }
+      } else {
+        // the tiles this wave takes, a claimed pair at a time with the next
+        // pair claimed ahead; two code buffers in turn (the load of the next
+        // tile is in flight while this one computes; a rotating copy would
+        // force a wait for it at the copy)
+        uint32_t pe = min(j + 2, end);        // the current pair [.., pe)
+        uint32_t na_raw = claim2(sg);          // the next pair (lane 0)
+        bool na_known = false;
+        uint32_t na = end;
+        auto next_tile = [&](uint32_t t, uint32_t& tn) -> bool {
+          if (t + 1 < pe) {
+            tn = t + 1;
+            return true;
+          }
+          if (!na_known) {
+            na = __builtin_amdgcn_readfirstlane(na_raw);
+            na_known = true;
+          }
+          if (na >= end) return false;
+          tn = na;
+          return true;
+        };
+        auto advance = [&](uint32_t t, uint32_t tn) {
+          if (!(t + 1 < pe)) {   // moved into the pair claimed ahead: claim another
+            pe = min(tn + 2, end);
+            na_raw = claim2(sg);
+            na_known = false;
+          }
+        };
+        {
+          uint32_t cb[NW], cb_b[NW];
+          uint32_t t = j, tn = 0;
+          for (;;) {
+            bool more = next_tile(t, tn);
+            // unconditional (the current tile again when none follows): one
+            // load per tile on every path, so the wait for this tile's codes
+            // leaves the next tile's load in flight (vmcnt(1), not vmcnt(0))
+            load_codes(more ? tn : t, cb, cb_b);
+            tile(codes, codes_b, t);
+            ++tiles_done;
+            if (pending) copy_prev();   // after the segment's first tile: the atomic has returned
+            if (!more) break;
+            drain_mid();
+            advance(t, tn);
+            t = tn;
+            more = next_tile(t, tn);
+            load_codes(more ? tn : t, codes, codes_b);
+            tile(cb, cb_b, t);
+            ++tiles_done;
+            if (!more) break;
+            drain_mid();
+            advance(t, tn);
+            t = tn;
+          }
         }
       }
       if (whits) {
@@ -2742,7 +2849,9 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         whits = 0;
       }
       };
-      if constexpr (NRW) {
+      if constexpr (NRW == int(kNarrowOnly)) {
+        run_seg(std::true_type{});
+      } else if constexpr (NRW != 0) {
         if (leaf_w & kItemNarrow)
           run_seg(std::true_type{});
         else
@@ -3964,8 +4073,11 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
     else if (variant == 68)                                                                \
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 68>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
                          0, s, a);                                                         \
+    else if (narrow == kNarrowOnly)                                                        \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, int(kNarrowOnly)>), dim3(grid),         \
+                         dim3(64 * ScanWaves<KV>()), 0, s, a);                             \
     else if (narrow)                                                                       \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, true>), dim3(grid),                     \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, 1>), dim3(grid),                        \
                          dim3(64 * ScanWaves<KV>()), 0, s, a);                             \
     else                                                                                   \
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
@@ -3975,8 +4087,11 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
 #define SMX_SCAN_CASE(KV)                                                                  \
   case KV:                                                                                 \
     if (variant != 0) return hipErrorInvalidValue;                                         \
-    if (narrow)                                                                            \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, true>), dim3(grid),                     \
+    if (narrow == kNarrowOnly)                                                             \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, int(kNarrowOnly)>), dim3(grid),         \
+                         dim3(64 * ScanWaves<KV>()), 0, s, a);                             \
+    else if (narrow)                                                                       \
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, 1>), dim3(grid),                        \
                          dim3(64 * ScanWaves<KV>()), 0, s, a);                             \
     else                                                                                   \
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
@@ -3985,7 +4100,7 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
 #endif
 
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,
-                      hipStream_t s, bool narrow) {
+                      hipStream_t s, uint32_t narrow) {
   switch (ix.ksteps) {
     SMX_SCAN_CASE(4)
     SMX_SCAN_CASE(8)

@@ -154,10 +154,15 @@ struct smx_index {
   // a leaf's remainder of <= 16 queries on the 16-slot scan path
   // (v_smfmac_i32_16x16x128_i8); SMX_NARROW=0 keeps every query tile 32 wide
   bool narrow_tiles = true;
+  bool narrow_only = false;        // SMX_NARROW=2: 16-slot tiles only whatever the density
+  bool narrow_mixed_only = false;  // SMX_NARROW=3: never the 16-slot-only mode
   // SMX_SEED_MFMA=1: the per-query thresholds by the seed scan (MFMA,
   // seed_scan_kernel + seed_select_kernel) instead of the per-query
   // LDS-lookup kernel (measured slower at glove shape: 0.180 vs 0.164 ms)
   bool seed_mfma = false;
+  // above fused_worklist_leaves: the work-list launches on this stream before
+  // the seed (true) or on the side stream beside it (false)
+  bool serial_worklist = false;
   int grid = 0;                    // scan grid: resident one-wave workgroups (occupancy API)
   int cus = 0;                     // compute units of the device
   bool profiling = false;
@@ -497,9 +502,17 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   // 16-slot tiles where leaves see few queries on average (configs 3/4: ~8
   // per leaf); with ~100 (glove) the 32-slot-only kernel is faster (the
   // 16-slot path costs registers and code in the kernel that carries it)
-  const uint32_t narrow = (h->narrow_tiles && variant == 0 &&
-                           uint64_t(nq) * uint64_t(L) < uint64_t(smx::kNarrowQueriesPerLeaf) *
-                                                            uint64_t(ix.nl)) ? 1u : 0u;
+  // (fewer than 16 per leaf: 16-slot tiles only, the narrow-only kernel;
+  // SMX_NARROW=2 forces that mode, for the tests)
+  const uint64_t qpl_x = uint64_t(nq) * uint64_t(L);   // queries per leaf x nl
+  uint32_t narrow = 0;
+  if (h->narrow_tiles && variant == 0) {
+    if (h->narrow_only ||
+        (!h->narrow_mixed_only && qpl_x < uint64_t(smx::kNarrowSlots) * uint64_t(ix.nl)))
+      narrow = smx::kNarrowOnly;
+    else if (qpl_x < uint64_t(smx::kNarrowQueriesPerLeaf) * uint64_t(ix.nl))
+      narrow = 1;
+  }
   smx::Bounds bd;
   bd.nq = uint32_t(nq);
   bd.items = w.max_items;
@@ -527,6 +540,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sa.L = L;
   sa.seed = seed;
   sa.kk = kk;
+  sa.narrow = narrow;
   // the seed scan (MFMA) for 1..kSeedMaxMfma seed leaves; SMX_SEED_MFMA=0:
   // the per-query seed kernel and a separate pair scatter
   // (the seed lists hold query | seed index << 24: nq < 2^24)
@@ -669,6 +683,19 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
       else
         SMX_HIP(smx::LaunchSeed(ix, sa, nq, s, &wla));
       Mark(h, 4, s);
+    } else if (h->serial_worklist) {
+      // the work-list launches, then the seed, on one stream: beside the
+      // seed's blocks (which fill every CU) the side-stream launches are
+      // starved until the seed drains
+      SMX_HIP(smx::LaunchWorklist(ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes,
+                                  w.wave_start, h->grid, stats + 3, code_bytes, h->chunk_tiles,
+                                  narrow, w.wl_part, bd, s));
+      Mark(h, 3, s);
+      if (seed_mfma)
+        SMX_HIP(smx::LaunchSeedScan(ix, sa, 2 * h->cus, s));
+      else
+        SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
+      Mark(h, 4, s);
     } else {
       // Fork.  Side stream: the work list (and the empty slots' records);
       // this stream: the seed thresholds.  Write sets ("Two
@@ -700,7 +727,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     else
       SMX_HIP(smx::LaunchPairScatter(ix, sa, nq, s));
     Mark(h, 5, s);
-    SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s, narrow != 0));
+    SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s, narrow));
     Mark(h, 6, s);
     SMX_HIP(smx::LaunchFinalSelect(sel, nq, s));
     Mark(h, 7, s);
@@ -935,8 +962,15 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
   }
   if (const char* fw = std::getenv("SMX_FUSED_WORKLIST"))
     h->fused_worklist_leaves = std::min(std::atoi(fw), smx::kFusedWorklistLeaves);
-  if (const char* nw = std::getenv("SMX_NARROW")) h->narrow_tiles = nw[0] != '0';
+  if (const char* nw = std::getenv("SMX_NARROW")) {
+    // 0: 32-slot tiles only; 1: by density (default); 2: 16-slot tiles only
+    // whatever the density; 3: never 16-slot-only (the remainder tiles only)
+    h->narrow_tiles = nw[0] != '0';
+    h->narrow_only = nw[0] == '2';
+    h->narrow_mixed_only = nw[0] == '3';
+  }
   if (const char* sm = std::getenv("SMX_SEED_MFMA")) h->seed_mfma = sm[0] != '0';
+  if (const char* sw = std::getenv("SMX_SERIAL_WORKLIST")) h->serial_worklist = sw[0] != '0';
   const char* ng = std::getenv("SMX_NO_GRAPH");
   // Eager launches by default: six kernels a call queue back to back on the
   // stream, while consecutive replays of a captured graph left ~13 us

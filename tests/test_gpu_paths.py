@@ -7,8 +7,10 @@ a handle is created):
     (seed_scan_kernel + seed_select_kernel: 16-query MFMA tiles over each
     seed leaf, SeedClaims' row budgets) instead of one block per query
     (seed_tau_kernel + pair_scatter_kernel);
-  * SMX_NARROW -- 16-slot scan tiles (v_smfmac_i32_16x16x128_i8) for calls
-    with few queries per leaf.
+  * SMX_NARROW -- 16-slot scan tiles (v_smfmac_i32_16x16x128_i8): 0 none,
+    1 by density (a leaf's last <= 16 queries below 32 queries per leaf on
+    average, 16-slot tiles only below 16), 2 16-slot tiles only, 3 never the
+    16-slot-only mode.
 
 Every combination must give the oracle's ids and distance bits
 (tree_ah_hybrid_residual.cc:631-846).  The two seed paths rank the same
@@ -27,7 +29,7 @@ from tests.conftest import make_index
 
 pytestmark = pytest.mark.gpu
 
-PATHS = [{"SMX_SEED_MFMA": s, "SMX_NARROW": n} for s in "01" for n in "01"]
+PATHS = [{"SMX_SEED_MFMA": s, "SMX_NARROW": n} for s in "01" for n in "0123"]
 
 
 def _handle(ix, env):

@@ -9,7 +9,7 @@ import pytest
 import worklist_model as wm
 
 
-@pytest.mark.parametrize("small", [True, False])
+@pytest.mark.parametrize("small", [True, False, 2])
 @pytest.mark.parametrize("seed", range(10))
 def test_shares_cover_items_exactly_once(seed, small):
     rng = np.random.default_rng(seed)
@@ -30,7 +30,7 @@ def test_shares_cover_items_exactly_once(seed, small):
     ([4000] * 3, [200, 1, 64]),      # leaves of many chunks, full query tiles
 ])
 def test_edge_shapes(sizes, counts):
-    for small in (True, False):
+    for small in (True, False, 2):
         for grid in (8, 256, 3072):
             wm.check(sizes, counts, grid=grid, small=small)
 
@@ -51,3 +51,25 @@ def test_few_queries_per_leaf_take_16_slot_tiles(seed):
         assert w == (1 if (c - 32 * q) <= 16 else 2)
     assert wm.query_tiles(17) == (1, 0) and wm.query_tiles(16) == (0, 1)
     assert wm.query_tiles(48) == (1, 1) and wm.query_tiles(64) == (2, 0)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_16_slot_tiles_only(seed):
+    """Below 16 queries per leaf on average the work list holds 16-slot
+    tiles only (kNarrowOnly): a leaf with c queries has ceil(c / 16) query
+    tiles of weight 1, the pair of rank r sits in tile r // 16, slot r % 16,
+    and a share may start inside any of them."""
+    rng = np.random.default_rng(700 + seed)
+    nl = int(rng.integers(50, 2000))
+    sizes = rng.integers(0, 4000, nl)
+    counts = rng.poisson(rng.uniform(1, 40), nl)
+    wl = wm.check([int(x) for x in sizes], [int(x) for x in counts],
+                  grid=int(rng.choice([256, 3072, 8192])), chunk_tiles=20, small=2)
+    per_leaf = {}
+    for leaf, n, j0, j1, q, w in wl["work"]:
+        assert w == 1
+        per_leaf[leaf] = max(per_leaf.get(leaf, 0), q + 1)
+    for leaf, qt in per_leaf.items():
+        assert qt == (int(counts[leaf]) + 15) // 16
+    assert wm.query_tiles(17, 2) == (0, 2) and wm.query_tiles(16, 2) == (0, 1)
+    assert wm.query_tiles(0, 2) == (0, 0) and wm.query_tiles(64, 2) == (0, 4)

@@ -43,7 +43,10 @@ def leaf_order(sizes):
 
 def query_tiles(c, small=True):
     """(32-slot, 16-slot) query tiles of a leaf with c queries (LeafQueryTiles):
-    a remainder of at most 16 queries takes a 16-slot tile."""
+    a remainder of at most 16 queries takes a 16-slot tile; small == 2: every
+    query tile has 16 slots."""
+    if small == 2:
+        return 0, (c + 15) // 16
     full, r = divmod(c, 32)
     if r == 0:
         return full, 0
@@ -120,8 +123,9 @@ def build(sizes, counts, grid, chunk_tiles, small=True):
                 skip = 2 * j - ru
                 if j == tiles:
                     q, j = q + 1, 0
-            else:
-                q, j, skip = q32, off - 2 * tiles * q32, 0
+            else:                          # in the 16-slot tiles (1 unit each)
+                q16i, j = divmod(off - 2 * tiles * q32, tiles)
+                q, skip = q32 + q16i, 0
             ch = 0
             if q < q32 + q16:
                 while chunk_tiles_range(n, chunk_tiles, ch)[1] <= j:
