@@ -161,8 +161,9 @@ struct smx_index {
   // LDS-lookup kernel (measured slower at glove shape: 0.180 vs 0.164 ms)
   bool seed_mfma = false;
   // above fused_worklist_leaves: the work-list launches on this stream before
-  // the seed (true) or on the side stream beside it (false)
-  bool serial_worklist = false;
+  // the seed (true; SMX_SERIAL_WORKLIST=0: on the side stream beside it --
+  // same box A/B, configs[3]/[4]: 0.578 vs 0.584 and 1.478 vs 1.495 ms/step)
+  bool serial_worklist = true;
   int grid = 0;                    // scan grid: resident one-wave workgroups (occupancy API)
   int cus = 0;                     // compute units of the device
   bool profiling = false;

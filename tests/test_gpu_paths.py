@@ -1,7 +1,7 @@
 """The search's alternative device paths against the oracle and each other.
 
-Two switches select kernels without changing any result (both are read when
-a handle is created):
+These switches select kernels without changing any result (all are read
+when a handle is created):
 
   * SMX_SEED_MFMA -- the per-query seed thresholds from the seed scan
     (seed_scan_kernel + seed_select_kernel: 16-query MFMA tiles over each
@@ -10,7 +10,10 @@ a handle is created):
   * SMX_NARROW -- 16-slot scan tiles (v_smfmac_i32_16x16x128_i8): 0 none,
     1 by density (a leaf's last <= 16 queries below 32 queries per leaf on
     average, 16-slot tiles only below 16), 2 16-slot tiles only, 3 never the
-    16-slot-only mode.
+    16-slot-only mode;
+  * SMX_FUSED_WORKLIST=0 / SMX_SERIAL_WORKLIST=0 -- the work list from its
+    three launches (as above 4096 leaves), on the seed's stream or on the
+    side stream.
 
 Every combination must give the oracle's ids and distance bits
 (tree_ah_hybrid_residual.cc:631-846).  The two seed paths rank the same
@@ -29,7 +32,13 @@ from tests.conftest import make_index
 
 pytestmark = pytest.mark.gpu
 
-PATHS = [{"SMX_SEED_MFMA": s, "SMX_NARROW": n} for s in "01" for n in "0123"]
+PATHS = [{"SMX_SEED_MFMA": s, "SMX_NARROW": n} for s in "01" for n in "0123"] + [
+    # the work list by its three launches: before the seed on one stream, and
+    # on the side stream beside it (the paths above 4096 leaves)
+    {"SMX_SEED_MFMA": "0", "SMX_NARROW": "1", "SMX_FUSED_WORKLIST": "0"},
+    {"SMX_SEED_MFMA": "0", "SMX_NARROW": "1", "SMX_FUSED_WORKLIST": "0",
+     "SMX_SERIAL_WORKLIST": "0"},
+]
 
 
 def _handle(ix, env):
@@ -67,7 +76,8 @@ def _check(oracle, ix, q, L, pre, seed, reorder=True):
         np.testing.assert_array_equal(gc, oc, err_msg=tag)
         np.testing.assert_array_equal(gi, oi, err_msg=tag)
         np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32), err_msg=tag)
-        cands[(env["SMX_SEED_MFMA"], env["SMX_NARROW"])] = t["mean_candidates"]
+        if len(env) == 2:
+            cands[(env["SMX_SEED_MFMA"], env["SMX_NARROW"])] = t["mean_candidates"]
     return cands
 
 
