@@ -3418,6 +3418,7 @@ __global__ void __launch_bounds__(256) final_select_kernel(SelectArgs a) {
 // a.fallback and re-run by final_select_kernel.
 // ---------------------------------------------------------------------------
 constexpr int kSelMax = 256;
+constexpr uint32_t kBlockRankMin = 160;   // more keys: BlockRank256, fewer: counting rank
 constexpr int kFsBins = 256;
 
 // Exact distances of m candidates (rows + rowid[i] * dim) into dist[], 8
@@ -3608,9 +3609,17 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
   }
   SMX_PHASE(2, qi, 1);
   const uint32_t c = n <= uint32_t(kSelMax) ? n : min(s_c, uint32_t(kSelMax));
-  // counting rank (stable: equal keys, the SOAR copies of an index without
-  // the global top-N tie, take consecutive ranks)
-  if (uint32_t(tid) < c) {
+  if ((a.disjoint || a.shift > 0) && c > kBlockRankMin) {
+    // distinct keys (packed ids, or global ids without SOAR copies): the
+    // wave-sort block rank, empty slots padded above every distance (its
+    // fixed cost beats the counting rank's O(c) per key only for larger c:
+    // glove's ~100 keys measured 1 us slower)
+    const uint64_t key = uint32_t(tid) < c ? sel[tid] : (0xFFFFFFFF00000000ull | uint32_t(tid));
+    const uint32_t r = BlockRank256(key, out);   // (out: its scratch until it returns)
+    if (uint32_t(tid) < c) out[r] = key;
+  } else if (uint32_t(tid) < c) {
+    // counting rank (stable: equal keys, the SOAR copies of an index without
+    // the global top-N tie, take consecutive ranks)
     const uint64_t key = sel[tid];
     out[RankStable(sel, c, key, uint32_t(tid))] = key;
   }
@@ -3662,11 +3671,10 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
   if (!a.disjoint) {
     // group duplicate ids: rank (gid << 32 | slot); run starts keep the
     // averaged distance 0.5a + 0.5b (two copies at most), the rest drop out
-    if (uint32_t(tid) < m) {
-      const uint64_t key = (uint64_t(gid[tid]) << 32) | uint32_t(tid);
-      uint32_t r = 0;
-      for (uint32_t j = 0; j < m; ++j) r += ((uint64_t(gid[j]) << 32) | j) < key ? 1u : 0u;
-      sel[r] = key;
+    {   // (gid, slot) keys are distinct: the block rank (m <= kSelMax = 256)
+      const uint64_t key = uint32_t(tid) < m ? (uint64_t(gid[tid]) << 32) | uint32_t(tid) : ~0ull - uint32_t(tid);
+      const uint32_t r = BlockRank256(key, sel);
+      if (uint32_t(tid) < m) sel[r] = key;
     }
     __syncthreads();
     uint64_t o = ~0ull;
@@ -3685,11 +3693,11 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
     out[tid] = o;
     if (tid == 0) s_c = 0;
     __syncthreads();
-    if (o != ~0ull) {
-      uint32_t r = 0;
-      for (uint32_t j = 0; j < m; ++j) r += out[j] < o ? 1u : 0u;
-      atomicAdd(&s_c, 1u);
-      if (r < uint32_t(a.pre_nn)) {
+    {   // the run starts' (distance, id) keys are distinct; the rest padded above
+      const uint32_t r =
+          BlockRank256(o != ~0ull ? o : (0xFFFFFFFF00000000ull | uint32_t(tid)), out);
+      if (o != ~0ull) atomicAdd(&s_c, 1u);
+      if (o != ~0ull && r < uint32_t(a.pre_nn)) {
         gid[r] = uint32_t(o & 0xFFFFFFFFu);
         dist[r] = FromOrdered(uint32_t(o >> 32));
         rowid[r] = hist[tid];
@@ -3709,9 +3717,17 @@ __global__ void __launch_bounds__(256) final_select_rank_kernel(SelectArgs a) {
     sel[tid] = fkey;
   }
   __syncthreads();
+  // (distance, id) keys are distinct (one entry per id): the block rank for
+  // many keys, the counting rank for few
+  uint32_t r;
+  if (m > kBlockRankMin) {
+    __syncthreads();   // sel is the block rank's scratch
+    r = BlockRank256(uint32_t(tid) < m ? fkey : (0xFFFFFFFF00000000ull | uint32_t(tid)), sel);
+  } else {
+    r = uint32_t(tid) < m ? CountLess(sel, m, fkey) : 0u;
+  }
   if (uint32_t(tid) < m) {
     const uint64_t key = fkey;
-    const uint32_t r = CountLess(sel, m, key);
     if (r < keep) {
       a.out_idx[size_t(qi) * a.out_width + r] = uint32_t(key & 0xFFFFFFFFu);
       a.out_dist[size_t(qi) * a.out_width + r] = FromOrdered(uint32_t(key >> 32));
@@ -3796,11 +3812,10 @@ __global__ void __launch_bounds__(256) merge_shards_kernel(MergeArgs a) {
   }
   __syncthreads();
   if (!a.disjoint) {
-    if (uint32_t(tid) < m) {
-      const uint64_t key = (uint64_t(gid[tid]) << 32) | uint32_t(tid);
-      uint32_t r = 0;
-      for (uint32_t j = 0; j < m; ++j) r += ((uint64_t(gid[j]) << 32) | j) < key ? 1u : 0u;
-      sel[r] = key;
+    {   // (gid, slot) keys are distinct: the block rank (m <= kSelMax = 256)
+      const uint64_t key = uint32_t(tid) < m ? (uint64_t(gid[tid]) << 32) | uint32_t(tid) : ~0ull - uint32_t(tid);
+      const uint32_t r = BlockRank256(key, sel);
+      if (uint32_t(tid) < m) sel[r] = key;
     }
     __syncthreads();
     uint64_t o = ~0ull;

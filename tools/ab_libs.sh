@@ -9,8 +9,8 @@ for rep in 1 2; do
   for L in ${LIBS:-scann_amd/lib/libscann_mi355x.so}; do
     n=$(basename $L .so)
     step "$n rep $rep" &&
-    SMX_LIB=$L timeout -k 10 240 python3 bench.py --steps ${STEPS:-200} --warmup 10 --no-cpu-baseline \
-        --no-sweep >> $O/$n.json 2>> $O/bench.err || exit 1
+    SMX_LIB=$L timeout -k 10 ${LIMIT:-240} python3 bench.py --steps ${STEPS:-200} --warmup 10 --no-cpu-baseline \
+        --no-sweep ${BENCH_ARGS:-} >> $O/$n.json 2>> $O/bench.err || exit 1
   done
 done
 step done
