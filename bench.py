@@ -73,7 +73,8 @@ CONFIGS = {
     "soar100m": dict(n=100_000_000, leaves=10000, leaves_to_search=100, metric=0, seed=4,
                      generated=True, split=8, soar=1.5, dim=96, components=512, spread=1.6,
                      train_sample=250_000,
-                     sweep=[20, 40, 60, 100, 150, 200, [100, 256], [200, 256], [400, 256]],
+                     # (pre_reorder_nn <= 128: SOAR shard lists hold 2 x pre <= 256)
+                     sweep=[20, 40, 60, 100, 150, 200, [100, 128], [200, 128], [400, 128]],
                      parity_points=[(100, 100), (1000, 256)],
                      workload="configs[3]: synthetic 100M x 96 dot product + SOAR (lambda 1.5, "
                               "overretrieve 2), tree-AH 10000 leaves, LUT16 AH 48 blocks x 2 "
