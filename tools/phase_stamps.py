@@ -25,21 +25,42 @@ def main():
         from scann_amd import build
         print(build.build_time(force=True))
         return
+    # python tools/phase_stamps.py [seed] [config]: config soar100m / deep1b
+    # = rank 0's generated shard of that bench configuration as a
+    # standalone index (its select at the bench's leaves_to_search / k')
     seed = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    config = sys.argv[2] if len(sys.argv) > 2 else "glove"
     os.environ["SMX_LIB"] = LIB
     path = "/tmp/smx_phase.bin"
     os.environ["SMX_PHASE_FILE"] = path
     import torch
     from bench import LEAVES_TO_SEARCH, NQ, PRE_NN, FINAL_NN, build_index
     from scann_amd import _native
-    db, q, ix = build_index(1_183_514, seed=2)
-    nat = _native.NativeIndex(ix)
+    leaves, pre = LEAVES_TO_SEARCH, PRE_NN
+    if config == "glove":
+        db, q, ix = build_index(1_183_514, seed=2)
+        nat = _native.NativeIndex(ix)
+        nat.set_tuning(4096, seed, 0, 32)
+    else:
+        from bench import CONFIGS
+        from scann_amd import generate
+        cfg = CONFIGS[config]
+        ds = generate.GeneratedDataset(cfg["n"], cfg["dim"], cfg["seed"],
+                                       components=cfg["components"],
+                                       spread=cfg.get("spread", 0.9), device=torch.device("cuda"))
+        ix = generate.build_generated_shard(
+            ds, cfg["leaves"], 0, cfg["split"], soar_lambda=cfg["soar"], seed=cfg["seed"],
+            training_sample_size=cfg["train_sample"],
+            training_iterations=cfg.get("train_iterations", 8), counts_from_all_ranks=False)
+        q = ds.queries(NQ, cfg["seed"] + 1000)
+        leaves = cfg["leaves_to_search"]
+        nat = _native.NativeIndex(ix.standalone())
+        nat.set_tuning(0, seed)
     qd = torch.from_numpy(q).cuda()
     oi = torch.zeros((NQ, FINAL_NN), dtype=torch.int32, device="cuda")
     od = torch.zeros((NQ, FINAL_NN), dtype=torch.float32, device="cuda")
-    nat.set_tuning(4096, seed, 0, 32)
     for _ in range(4):
-        nat.search_batched_device(qd.data_ptr(), NQ, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True,
+        nat.search_batched_device(qd.data_ptr(), NQ, leaves, pre, FINAL_NN, True,
                                   oi.data_ptr(), od.data_ptr(), None)
     torch.cuda.synchronize()
     full = np.fromfile(path, dtype=np.uint64).reshape(3, 4096, 8).astype(np.int64)

@@ -1,7 +1,7 @@
 # Round-4 measurement pass (gpurun, repo root): smoke, glove and SIFT bench
 # lines with cpu_baseline, their rocprofv3 kernel traces and PMC passes.
 set -o pipefail
-O=gpurun_out/r04f
+O=gpurun_out/${TAG:-r04f}
 mkdir -p $O
 step() { echo "[r04_final] $(date +%T) $*" >&2; }
 step smoke && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 &&
