@@ -1422,28 +1422,34 @@ __device__ void WorklistFusedBlock(const WorklistArgs& w, int b) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // (phase stamps of block 0: start, leaf_item0 written, end)
   if (b == 0) SMX_PHASE(1, kPhaseQueries - 1, 0);
-  const int nl = w.nl, p0 = tid * kWlPerThread;
+  // per thread ceil(nl / 256) consecutive positions (not kWlPerThread: at
+  // glove's 1000 leaves 4 per thread instead of 16 on a quarter of them)
+  const int nl = w.nl, per = (nl + 255) / 256, p0 = tid * per;
   const int pb = b * kWlPosPerBlock, pe = min(nl, pb + kWlPosPerBlock);
   uint32_t leafv[kWlPerThread], itv[kWlPerThread], unv[kWlPerThread];
 #pragma unroll
-  for (int k = 0; k < kWlPerThread; ++k) leafv[k] = p0 + k < nl ? w.order[p0 + k] : 0u;
+  for (int k = 0; k < kWlPerThread; ++k) leafv[k] = k < per && p0 + k < nl ? w.order[p0 + k] : 0u;
   uint32_t ti = 0, tu = 0;
   unsigned long long tp = 0, tb = 0, tn = 0;
 #pragma unroll
   for (int k = 0; k < kWlPerThread; ++k) {
     itv[k] = unv[k] = 0;
-    if (p0 + k < nl) {
+    if (k < per && p0 + k < nl) {
       const uint32_t leaf = leafv[k];
       const uint32_t c = w.cnt[size_t(leaf) * kCounterStride], n = w.leaf_size[leaf];
       unv[k] = LeafUnits(c, n, w.chunk_tiles, w.narrow, itv[k]);
       tp += c;
       tb += 16ull * w.nb * ((n + 31u) / 32u) * c;   // algorithmic code bytes
-      tn += LeafQueryTiles(c, w.narrow).y * ((n + 31u) / 32u);
+      if (w.narrow) tn += LeafQueryTiles(c, w.narrow).y * ((n + 31u) / 32u);
     }
     ti += itv[k];
     tu += unv[k];
   }
-  s_last_un[tid] = unv[kWlPerThread - 1];
+  uint32_t last_un = 0;   // the units of this thread's last position
+#pragma unroll
+  for (int k = 0; k < kWlPerThread; ++k)
+    if (k == per - 1) last_un = unv[k];
+  s_last_un[tid] = last_un;
   const uint32_t inc_i = BlockInclusiveScan256(ti, wsum);
   __syncthreads();   // wsum is reused
   const uint32_t inc_u = BlockInclusiveScan256(tu, wsum);
@@ -1473,7 +1479,7 @@ __device__ void WorklistFusedBlock(const WorklistArgs& w, int b) {
 #pragma unroll
   for (int k = 0; k < kWlPerThread; ++k) {
     const int p = p0 + k;
-    if (p < nl) {
+    if (k < per && p < nl) {
       if (b == 0) {
         w.leaf_item0[leafv[k]] = ei;
         w.pos_unit0[p] = eu;
@@ -1674,6 +1680,13 @@ __device__ uint32_t BlockRank256(uint64_t key, uint64_t* sbuf) {
   return r + b;
 }
 
+// The ranks below: counting ranks by default; SMX_SEED_BLOCKRANK=1 ranks the
+// minima and the compacted values with BlockRank256 (phase stamps: select p50
+// 7.4 -> 6.3 us, but no gain in the seed launch, whose end is set by its
+// slowest blocks: same-box A/B).
+#ifndef SMX_SEED_BLOCKRANK
+#define SMX_SEED_BLOCKRANK 0
+#endif
 // The threshold key of a query from its seed distances (ordered bits, 16
 // per thread of a 256-thread block, 0xFFFFFFFF = none): the exact kk-th
 // smallest value v as (v << 32 | 0xFFFFFFFF), which admits every candidate
@@ -1699,7 +1712,13 @@ __device__ uint64_t ThresholdOfVals(const uint32_t (&vals)[kSeedPerThread], uint
 #pragma unroll
     for (int i = 0; i < kSeedPerThread; ++i) vmin = min(vmin, vals[i]);
     const uint64_t mk = (uint64_t(vmin) << 32) | uint32_t(tid);
+#if SMX_SEED_BLOCKRANK
     if (BlockRank256(mk, skey) == kk - 1u) s_thi = vmin;
+#else
+    skey[tid] = mk;
+    __syncthreads();
+    if (CountLess(skey, 256u, mk) == kk - 1u) s_thi = vmin;
+#endif
     __syncthreads();
     const uint32_t thi = s_thi;
 #pragma unroll
@@ -1710,7 +1729,7 @@ __device__ uint64_t ThresholdOfVals(const uint32_t (&vals)[kSeedPerThread], uint
       }
     __syncthreads();
     const uint32_t c = s_cnt;
-    if (c <= 256u) {   // block rank of the compacted keys (the rest padded above them)
+    if (SMX_SEED_BLOCKRANK && c <= 256u) {   // block rank of the compacted keys (the rest padded above them)
       const uint64_t key = uint32_t(tid) < c ? skey[tid] : (~0ull << 16) | uint32_t(tid);
       __syncthreads();   // skey is the rank's buffer
       if (BlockRank256(key, skey) == kk - 1u) s_T = (key & 0xFFFFFFFF00000000ull) | 0xFFFFFFFFull;
@@ -2155,7 +2174,7 @@ constexpr uint32_t kStealMin = 3;  // tiles left for a second wave to join a seg
 template <int K>
 constexpr int ScanWaves() { return K <= 26 ? SMX_SCAN_WAVES : 8; }
 #ifndef SMX_SCAN_R
-#define SMX_SCAN_R 3
+#define SMX_SCAN_R 2
 #endif
 
 // Diagnostic stamps (ABL & 8; a separate buffer that nothing else reads):
@@ -2415,8 +2434,10 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       auto slot_rec = [&](uint32_t sgi) {
         const uint32_t s0 = __builtin_amdgcn_readfirstlane(s_desc[sgi].slot0);
         const uint32_t ns = __builtin_amdgcn_readfirstlane(s_desc[sgi].nslots);
-        const bool nr = (__builtin_amdgcn_readfirstlane(s_desc[sgi].leaf) & kItemNarrow) != 0;
-        const uint32_t cs = nr ? uint32_t(lane & 15) : uint32_t(c);
+        uint32_t cs = uint32_t(c);
+        if constexpr (NRW != 0) {
+          if (__builtin_amdgcn_readfirstlane(s_desc[sgi].leaf) & kItemNarrow) cs = uint32_t(lane & 15);
+        }
         ItemLane r;
         if (cs < ns) {
           SMX_CHECK(s0 + cs, a.bd.recs, "slot record");

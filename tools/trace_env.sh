@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 for E in ${ENVS:-SMX_SEED_MFMA=0}; do
   echo "[trace_env] $(date +%T) $E" >&2
   mkdir -p "$O/$E"
-  (export ${E//,/ }; timeout -k 10 ${LIMIT:-300} rocprofv3 --kernel-trace --stats --output-format csv \
+  (export ${E//,/ }; export SMX_LIB=${SMX_LIB:+$ROOT/$SMX_LIB}; timeout -k 10 ${LIMIT:-300} rocprofv3 --kernel-trace --stats --output-format csv \
       -d "$O/$E" -o run -- python3 "$ROOT/bench.py" --no-cpu-baseline --no-sweep --no-parity \
       --steps ${STEPS:-50} ${BENCH_ARGS:-} > "$O/$E/bench.json" 2> "$O/$E/bench.err") || exit 1
 done
