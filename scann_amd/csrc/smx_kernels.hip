@@ -2287,6 +2287,27 @@ __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32
   }
 }
 
+// The lane id from v_mbcnt, opaque to the compiler (volatile asm), so that it
+// is rematerialised at every use instead of occupying a register.
+struct LaneId {
+  __device__ __forceinline__ operator int() const {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+  }
+};
+template <int MASK, int SHIFT>
+struct LaneField {
+  __device__ __forceinline__ operator int() const { return (int(LaneId()) >> SHIFT) & MASK; }
+};
+// ... or computed once and held in a register
+template <int MASK, int SHIFT>
+struct LaneVal {
+  int v;
+  __device__ __forceinline__ LaneVal() : v(int((threadIdx.x & 63u) >> SHIFT) & MASK) {}
+  __device__ __forceinline__ operator int() const { return v; }
+};
+
 // NRW: 0 = 32-slot items only (only that path is compiled in: fewer
 // registers and code), 1 = both kinds, kNarrowOnly = 16-slot items only.
 template <int K, int ABL = 0, int NRW = 0>
@@ -2308,9 +2329,16 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   __shared__ uint32_t s_nseg, s_claim, s_sw, s_su;
   // wave-uniform values in scalar registers (the B fragments need the VGPRs)
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int c = lane & 31;
-  const int h = lane >> 5;
+  // the lane id and its fields recomputed where they are used (two VALU ops)
+  // instead of held across the segment loop: held, the allocator spilled them
+  // and their reloads waited for the segment-record prefetch (vmcnt is in
+  // order)
+  // (the 16-slot-only kernel has registers to spare and is issue-bound: there
+  // the recomputation measured 4% slower, so it keeps them in registers)
+  constexpr bool kRemat = NRW != int(kNarrowOnly);
+  const std::conditional_t<kRemat, LaneId, LaneVal<63, 0>> lane;
+  const std::conditional_t<kRemat, LaneField<31, 0>, LaneVal<31, 0>> c;
+  const std::conditional_t<kRemat, LaneField<1, 5>, LaneVal<1, 5>> h;
   ScanWaveLds& wl = wl_[wv];
   if (threadIdx.x < 16) {   // group nibble g0 | g1 << 2: a 1 at values 2*g0, 8 + 2*g1
     const uint32_t g0 = threadIdx.x & 3u, g1 = threadIdx.x >> 2;
