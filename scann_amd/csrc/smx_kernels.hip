@@ -343,15 +343,22 @@ __device__ bool OrderSmallestByBins(const uint64_t* keys, uint32_t n, uint32_t m
 typedef float v16f __attribute__((ext_vector_type(16)));
 
 // A 256-thread block computes 64 queries x 64 centers (wave w: query half
-// w & 1, center half w >> 1); the operands are staged in LDS 32 dims at a time
-// with coalesced row loads (-q and c or 2c, zero-padded past dim), so every
-// MFMA reads its two floats per lane from LDS instead of a strided global row.
-constexpr int kPartTile = 64, kPartChunk = 32;
+// w & 1, center half w >> 1); the operands are staged in LDS CHUNK dims at a
+// time with coalesced row loads (-q and c or 2c, zero-padded past dim), so
+// every MFMA reads its two floats per lane from LDS instead of a strided
+// global row.  CHUNK = kPartFullDim (dim <= 128: glove, SIFT, Deep): the
+// whole tile in one round of loads, and the squared query norms from the
+// staged tile -- one load latency per block instead of one per 32 dims plus
+// a serial norm loop over global memory (at 256 blocks, one wave per SIMD,
+// nothing else hides them).
+constexpr int kPartTile = 64, kPartChunk = 32, kPartFullDim = 128;
 
+template <int CHUNK>
 __global__ void __launch_bounds__(256) partition_scores_kernel(
     const float* __restrict__ queries, int nq, int dim, const float* __restrict__ centers,
     const float* __restrict__ cnorm, int nl, int metric, float* __restrict__ scores,
     StateInit init) {
+  constexpr bool kFull = CHUNK == kPartFullDim;   // dim <= CHUNK: one staging round
   {
     // the search's per-call state (no separate memset nodes); nothing in this
     // launch reads it, the top-L launch that follows does
@@ -362,8 +369,8 @@ __global__ void __launch_bounds__(256) partition_scores_kernel(
     for (uint32_t i = gt; i < init.n_cand; i += gs) init.cand_count[size_t(i) * kCounterStride] = 0u;
     for (uint32_t i = gt; i < init.n_tau; i += gs) init.tau[i] = kNoThreshold;
   }
-  __shared__ float qs[kPartTile][kPartChunk + 1];
-  __shared__ float cs[kPartTile][kPartChunk + 1];
+  __shared__ float qs[kPartTile][CHUNK + 1];
+  __shared__ float cs[kPartTile][CHUNK + 1];
   __shared__ float qn[kPartTile];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, k = lane >> 5;
@@ -371,48 +378,113 @@ __global__ void __launch_bounds__(256) partition_scores_kernel(
   const int qw = (wave & 1) * 32, cw = (wave >> 1) * 32;   // this wave's sub-tile
   const int q0 = qt + qw, c0 = ct + cw;
   const int cb = min(c0 + r, nl - 1);     // B column (center) of this lane
+  // the squared query norm in double, dims ascending (exact squares)
+  auto init_acc = [&](v16f& acc) {
+    if (metric == 1) {
+      // C layout: col = lane & 31 (center), row = (i&3) + 8*(i>>2) + 4*(lane>>5)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = (i & 3) + 8 * (i >> 2) + 4 * k;
+        acc[i] = __fadd_rn(cnorm[cb], qn[qw + row]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+    }
+  };
   v16f acc;
-  if (metric == 1) {
-    if (tid < kPartTile) {
-      double s = 0.0;
-      const float* qq = queries + size_t(min(qt + tid, nq - 1)) * dim;
-      for (int d = 0; d < dim; ++d) s += double(qq[d]) * double(qq[d]);
-      qn[tid] = float(s);
+  if (!kFull) {
+    if (metric == 1) {
+      if (tid < kPartTile) {
+        double s = 0.0;
+        const float* qq = queries + size_t(min(qt + tid, nq - 1)) * dim;
+        for (int d = 0; d < dim; ++d) s += double(qq[d]) * double(qq[d]);
+        qn[tid] = float(s);
+      }
+      __syncthreads();
     }
-    __syncthreads();
-    // C layout: col = lane & 31 (center), row = (i&3) + 8*(i>>2) + 4*(lane>>5)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int row = (i & 3) + 8 * (i >> 2) + 4 * k;
-      acc[i] = __fadd_rn(cnorm[cb], qn[qw + row]);
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+    init_acc(acc);
   }
   const float cscale = metric == 1 ? 2.0f : 1.0f;
-  for (int d0 = 0; d0 < dim; d0 += kPartChunk) {
+  if constexpr (kFull) {
+    // row tid / 4, dims tid % 4 + 4 j: one buffer offset per operand and
+    // immediate offsets (64 loads with 64-bit addresses needed all 256
+    // VGPRs); the resources end at the tile's last row, so a read past it
+    // returns 0, and dims past dim (the next row's) are masked below.  (Rows
+    // by 128-byte runs, tid % 32 + 32 j, measured 8.7 us against 8.0 at
+    // glove's 100 dims, 12.6 against 13.1 at SIFT's 128.)
+    constexpr int kPer = kPartFullDim / 4;
+    const int row = tid >> 2, sub = tid & 3;
+    const uint32_t qrows = uint32_t(min(kPartTile, nq - qt)), crows = uint32_t(min(kPartTile, nl - ct));
+    const auto qrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(queries + size_t(qt) * dim), 0, int(qrows * uint32_t(dim) * 4u), 0x00020000);
+    const auto crs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(centers + size_t(ct) * dim), 0, int(crows * uint32_t(dim) * 4u), 0x00020000);
+    const int off = (row * dim + sub) * 4;
+    float qv[kPer], cv[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      qv[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(qrs, off + 16 * j, 0, 0));
+      cv[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(crs, off + 16 * j, 0, 0));
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int d = sub + 4 * j;
+      qs[row][d] = d < dim ? -qv[j] : -0.0f;
+      cs[row][d] = d < dim ? __fmul_rn(cv[j], cscale) : 0.0f;
+    }
+    __syncthreads();
+    if (metric == 1) {
+      if (tid < kPartTile) {   // (-q)^2 = q^2; the zero padding adds +0
+        double s = 0.0;
+        for (int d0 = 0; d0 < dim; d0 += 16) {
+          float x[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) x[u] = qs[tid][d0 + u];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) s += double(x[u]) * double(x[u]);
+        }
+        qn[tid] = float(s);
+      }
+      __syncthreads();
+    }
+    init_acc(acc);
+    // (steps by 16 dims: the zero padding up to 128 leaves acc unchanged, and
+    // the operand reads of 8 MFMAs go out together)
+    const int steps = (dim + 15) & ~15;
+    for (int s = 0; s < steps; s += 16) {
+      float av[8], bv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        av[u] = qs[qw + r][s + 2 * u + k];
+        bv[u] = cs[cw + r][s + 2 * u + k];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+    }
+  }
+  for (int d0 = 0; !kFull && d0 < dim; d0 += CHUNK) {
     __syncthreads();
     // all loads of the chunk in flight together: clamped indices, the
     // padding applied after (a guarded load waits on its own)
-    constexpr int kPer = (kPartTile * kPartChunk) / 256;
+    constexpr int kPer = (kPartTile * CHUNK) / 256;
     float qv[kPer], cv[kPer];
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = tid + i * 256;
-      const int row = e / kPartChunk, col = e % kPartChunk, d = min(d0 + col, dim - 1);
+      const int row = e / CHUNK, col = e % CHUNK, d = min(d0 + col, dim - 1);
       qv[i] = queries[size_t(min(qt + row, nq - 1)) * dim + d];
       cv[i] = centers[size_t(min(ct + row, nl - 1)) * dim + d];
     }
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = tid + i * 256;
-      const int row = e / kPartChunk, col = e % kPartChunk, d = d0 + col;
+      const int row = e / CHUNK, col = e % CHUNK, d = d0 + col;
       qs[row][col] = d < dim ? -qv[i] : -0.0f;
       cs[row][col] = d < dim ? __fmul_rn(cv[i], cscale) : 0.0f;
     }
     __syncthreads();
-    const int steps = min(kPartChunk, ((dim - d0) + 1) & ~1);
+    const int steps = min(CHUNK, ((dim - d0) + 1) & ~1);
     for (int s = 0; s < steps; s += 2)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qs[qw + r][s + k], cs[cw + r][s + k], acc, 0, 0,
                                                  0);
@@ -3475,7 +3547,14 @@ constexpr int kFsBins = 256;
 // (dims l, l+8, ...) and the folds follow ExactDistance exactly.  256
 // threads; ends with a barrier.
 constexpr int kXMax = 16;   // dims per lane held in registers (dim <= 128)
-constexpr int kXPass = 2;   // 32-candidate passes whose rows are in flight together
+#ifndef SMX_XPASS
+#define SMX_XPASS 2
+#endif
+constexpr int kXPass = SMX_XPASS;   // 32-candidate passes whose rows are in flight together
+#ifndef SMX_XPASS_EXACT
+#define SMX_XPASS_EXACT 4
+#endif
+constexpr int kXPassExact = SMX_XPASS_EXACT;   // the same at dims of exactly 12 or 16 steps
 
 __device__ void ExactDistances8(const SelectArgs& a, const float* rows, const uint32_t* rowid,
                                 uint32_t m, float* dist, int qi) {
@@ -3511,42 +3590,60 @@ __device__ void ExactDistances8(const SelectArgs& a, const float* rows, const ui
     return r;
   };
   const int c4 = min(j8 + (l & 3), dim - 1), c2 = min(j2 + (l & 1), dim - 1), c1 = min(j1, dim - 1);
-  if (dim <= 8 * kXMax) {
-    // every load of kXPass passes is issued before the first use (clamped
-    // indices; the accumulation below stops at j8)
-    float qv[kXMax];
+  // NJ 8-dim steps held in registers, NP 32-candidate passes whose rows are in
+  // flight together.  kExact: dim's steps are exactly NJ, so lane l's loads
+  // x[l + 8k] stay inside the row and share one address (immediate offsets);
+  // otherwise they are clamped and the accumulation stops at j8.
+  auto passes = [&](auto nj_c, auto np_c, auto exact_c) {
+    constexpr int NJ = decltype(nj_c)::value, NP = decltype(np_c)::value;
+    constexpr bool kExact = decltype(exact_c)::value;
+    float qv[NJ];
+    const float* ql = q + l;
 #pragma unroll
-    for (int k = 0; k < kXMax; ++k) qv[k] = q[min(l + 8 * k, dim - 1)];
+    for (int k = 0; k < NJ; ++k) qv[k] = kExact ? ql[8 * k] : q[min(l + 8 * k, dim - 1)];
     const float q4 = q[c4], q2 = q[c2], q1 = q[c1];
     const int nj = j8 >> 3;
-    for (uint32_t base = 0; base < m; base += 32 * kXPass) {
-      float xv[kXPass][kXMax], x4[kXPass], x2[kXPass], x1[kXPass];
+    for (uint32_t base = 0; base < m; base += 32 * NP) {
+      float xv[NP][NJ], x4[NP], x2[NP], x1[NP];
 #pragma unroll
-      for (int p = 0; p < kXPass; ++p) {
+      for (int p = 0; p < NP; ++p) {
         const uint32_t i = min(base + 32 * p + uint32_t(tid >> 3), m - 1);
         const float* x = rows + size_t(rowid[i]) * dim;
+        const float* xl = x + l;
 #pragma unroll
-        for (int k = 0; k < kXMax; ++k) xv[p][k] = x[min(l + 8 * k, dim - 1)];
+        for (int k = 0; k < NJ; ++k) xv[p][k] = kExact ? xl[8 * k] : x[min(l + 8 * k, dim - 1)];
         x4[p] = x[c4];
         x2[p] = x[c2];
         x1[p] = x[c1];
       }
-      float r[kXPass];
+      float r[NP];
 #pragma unroll
-      for (int p = 0; p < kXPass; ++p) {
+      for (int p = 0; p < NP; ++p) {
         float acc = 0.0f;
 #pragma unroll
-        for (int k = 0; k < kXMax; ++k)
-          if (k < nj) acc = term(acc, qv[k], xv[p][k]);
+        for (int k = 0; k < NJ; ++k)
+          if (kExact || k < nj) acc = term(acc, qv[k], xv[p][k]);
         r[p] = finish(acc, q4, x4[p], q2, x2[p], q1, x1[p]);
       }
       __syncthreads();   // every read of rowid/dist for these passes is done
 #pragma unroll
-      for (int p = 0; p < kXPass; ++p) {
+      for (int p = 0; p < NP; ++p) {
         const uint32_t i = base + 32 * p + uint32_t(tid >> 3);
         if (l == 0 && i < m) dist[i] = r[p];
       }
     }
+  };
+  using I12 = std::integral_constant<int, 12>;
+  using I16 = std::integral_constant<int, 16>;
+  using P2 = std::integral_constant<int, kXPass>;
+  using P4 = std::integral_constant<int, kXPassExact>;
+  using P3 = std::integral_constant<int, kXPassExact - 1>;
+  if (j8 == 96) {
+    passes(I12{}, P4{}, std::true_type{});   // dims 96..103 (glove-100, deep-96)
+  } else if (j8 == 128) {
+    passes(I16{}, P3{}, std::true_type{});   // dims 128..135 (sift-128)
+  } else if (dim <= 8 * kXMax) {
+    passes(I16{}, P2{}, std::false_type{});
   } else {
     for (uint32_t base = 0; base < m; base += 32) {
       const uint32_t i = base + uint32_t(tid >> 3);
@@ -4008,10 +4105,13 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
     hipLaunchKernelGGL(partition_scores_a8_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s,
                        queries, nq, ix.dim, ix.centers, ix.nl, ix.metric, scores, f.init);
   } else {
-    hipLaunchKernelGGL(partition_scores_kernel,
-                       dim3((nq + kPartTile - 1) / kPartTile, (ix.nl + kPartTile - 1) / kPartTile),
-                       dim3(256), 0, s, queries, nq, ix.dim, ix.centers, ix.cnorm, ix.nl, ix.metric,
-                       scores, f.init);
+    const dim3 grid((nq + kPartTile - 1) / kPartTile, (ix.nl + kPartTile - 1) / kPartTile);
+    if (ix.dim <= kPartFullDim)
+      hipLaunchKernelGGL(partition_scores_kernel<kPartFullDim>, grid, dim3(256), 0, s, queries, nq,
+                         ix.dim, ix.centers, ix.cnorm, ix.nl, ix.metric, scores, f.init);
+    else
+      hipLaunchKernelGGL(partition_scores_kernel<kPartChunk>, grid, dim3(256), 0, s, queries, nq,
+                         ix.dim, ix.centers, ix.cnorm, ix.nl, ix.metric, scores, f.init);
   }
   // static LDS of the kernel besides the dynamic key buffers: the LUT build's
   // raw table and reduction (~5 KB) and the selection's words
