@@ -610,6 +610,7 @@ struct TopLTail {
   uint32_t* seed_nunits;
   const uint32_t* leaf_size;
   int seed;
+  int lut_split;   // topl_block_kernel: the LUTs by their own blocks [nq, 2 nq)
 };
 
 // The query's first `seed` leaves claim slots in those leaves' seed lists
@@ -887,7 +888,7 @@ __device__ __forceinline__ void TopLBlock(const float* __restrict__ scores, int 
   }
   SMX_PHASE(0, qi, 4);
   SeedClaims(qi, m, srt, tail);
-  if (tail.lut.lut) BuildLut(qi, tail.lut);
+  if (tail.lut.lut && !tail.lut_split) BuildLut(qi, tail.lut);
   SMX_PHASE(0, qi, 5);
 }
 
@@ -895,6 +896,12 @@ template <int VPT, int NT>
 __global__ void __launch_bounds__(NT) topl_block_kernel(const float* __restrict__ scores, int nl,
                                                         int L, int32_t* __restrict__ out_leaf,
                                                         float* __restrict__ out_dist, TopLTail tail) {
+  // (split: the query LUTs, which need no score, by blocks beside the
+  // selections instead of after each one)
+  if (tail.lut_split && blockIdx.x >= gridDim.x / 2) {
+    BuildLut(int(blockIdx.x - gridDim.x / 2), tail.lut);
+    return;
+  }
   TopLBlock<VPT, NT>(scores, nl, L, out_leaf, out_dist, tail);
 }
 
@@ -4116,12 +4123,16 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   // static LDS of the kernel besides the dynamic key buffers: the LUT build's
   // raw table and reduction (~5 KB) and the selection's words
   constexpr size_t kStaticLds = 6 * 1024;
-  if (L <= kWaveTopL && ix.nl <= 256 * 4) {
-    hipLaunchKernelGGL((topl_block_kernel<4, 256>), dim3(nq), dim3(256), 0, s, scores, ix.nl, L,
-                       out_leaf, out_dist, tail);
-  } else if (L <= kWaveTopL && ix.nl <= 256 * 8) {
-    hipLaunchKernelGGL((topl_block_kernel<8, 256>), dim3(nq), dim3(256), 0, s, scores, ix.nl, L,
-                       out_leaf, out_dist, tail);
+  static const int lut_split = [] { const char* e = std::getenv("SMX_LUT_SPLIT"); return e ? std::atoi(e) : 1; }();
+  if (L <= kWaveTopL && ix.nl <= 256 * 8) {
+    tail.lut_split = lut_split && tail.lut.lut ? 1 : 0;
+    const dim3 grid(unsigned(nq) * (tail.lut_split ? 2u : 1u));
+    if (ix.nl <= 256 * 4)
+      hipLaunchKernelGGL((topl_block_kernel<4, 256>), grid, dim3(256), 0, s, scores, ix.nl, L,
+                         out_leaf, out_dist, tail);
+    else
+      hipLaunchKernelGGL((topl_block_kernel<8, 256>), grid, dim3(256), 0, s, scores, ix.nl, L,
+                         out_leaf, out_dist, tail);
   } else if (ix.nl > kSampleTopLMinLeaves && L <= 4096) {
     // many leaves (configs[3]'s 10^4, configs[4]'s 5 x 10^4): the sampled
     // threshold, exact (same box A/B at 10^4 leaves, L = 100: partition
