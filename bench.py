@@ -116,9 +116,7 @@ def queries_for_rank(dim, rank):
     from scann_amd import synthetic
     if CFG["metric"] == 0:
         return synthetic.mixture(NQ, dim, 2000, 0.9, seed=2 + 100 + 7919 * rank, means_seed=2)
-    x = synthetic.mixture(NQ, dim, 1000, 0.6, 3 + 100 + 7919 * rank, normalize=False,
-                          means_seed=3)
-    return np.clip(np.rint(np.abs(x) * 256.0), 0, 255).astype(np.float32)
+    return synthetic.sift_draw(NQ, 3 + 100 + 7919 * rank, seed=3, d=dim)
 
 
 def build_index(n, seed):
@@ -200,6 +198,23 @@ def scan_roofline(code_bytes, scan_ms, timings, num_blocks):
         # 32 datapoints x B codes -> 2 lookups per byte
         "lookups_per_s": round(2.0 * code_bytes / sec, 1),
     }
+
+
+def scan_traffic(config):
+    """HBM read bytes per scan launch from this config's own PMC FETCH_SIZE
+    pass (tools/profile_bench.sh -> tools/pmc_traffic.py ->
+    profiles/scan_traffic_<config>.json), only when it was measured on the
+    same kernel source; None otherwise."""
+    import hashlib
+    tpath = os.path.join(ROOT, "profiles", f"scan_traffic_{config}.json")
+    if not os.path.exists(tpath):
+        return None
+    with open(tpath) as f:
+        tr = json.load(f)
+    with open(os.path.join(ROOT, "scann_amd", "csrc", "smx_kernels.hip"), "rb") as f:
+        if hashlib.sha256(f.read()).hexdigest() != tr.get("smx_kernels_sha256"):
+            return None
+    return tr["hbm_read_bytes_per_launch"]
 
 
 def cpu_info():
@@ -497,14 +512,7 @@ def main():
     bytes_per_launch = float(np.mean(scan_bytes))
     roof = scan_roofline(bytes_per_launch, avg_scan_ms, t_last, ix.num_blocks)
     traffic = None
-    tpath = os.path.join(ROOT, "profiles", "scan_traffic.json")
-    if os.path.exists(tpath) and args.config == "glove":   # measured on the glove workload
-        import hashlib
-        with open(tpath) as f:
-            tr = json.load(f)
-        with open(os.path.join(ROOT, "scann_amd", "csrc", "smx_kernels.hip"), "rb") as f:
-            if hashlib.sha256(f.read()).hexdigest() == tr.get("smx_kernels_sha256"):
-                traffic = tr["hbm_read_bytes_per_launch"]
+    traffic = scan_traffic(args.config)
 
     if rank == 0:
         result = {
@@ -703,6 +711,7 @@ def main_generated(args, rank, world, local, dist, dev):
     avg_scan_ms = float(np.mean(scan_ms))
     bytes_per_launch = float(np.mean(scan_bytes))
     roof = scan_roofline(bytes_per_launch, avg_scan_ms, stages, ix.num_blocks)
+    traffic = scan_traffic(args.config)
     if rank == 0:
         result = {
             "metric": CFG["metric_name"],
@@ -736,7 +745,9 @@ def main_generated(args, rank, world, local, dist, dev):
             "merge_ms": round(merge_s * 1000.0 / args.steps, 4),
             "merge_input": (f"all-gather of {split} ranks" if world == split else
                             f"{split} copies of this rank's [nq][{k}] list"),
-            "roofline": dict(roof, traffic=None),
+            "roofline": dict(roof, traffic=traffic,
+                             hbm_GBps_measured=(round(traffic / (avg_scan_ms * 1e-3) / 1e9, 1)
+                                                if traffic else None)),
             "stage_ms": {k2: round(stages[k2], 4) for k2 in
                          ("partition_ms", "invert_ms", "seed_scan_ms", "scan_ms", "select_ms",
                           "total_ms")},

@@ -17,17 +17,13 @@ constexpr int kQueriesPerTile = 32;
 constexpr int kNarrowSlots = 16;
 // WorklistArgs::totals[kTotalsTiles16]: the call's 16-slot tiles (stats[12])
 constexpr int kTotalsTiles16 = 9;
-// The seed scan (the per-query thresholds on MFMA): each leaf lists at most
-// kSeedSlots of the queries it seeds (the top-L kernel claims the slots), each
-// query keeps at most kSeedKeys seed distances (SeedTau's kSeedCap).
-constexpr int kSeedSlots = 64;
+// Each query's seed threshold ranks at most kSeedKeys seed distances
+// (seed_tau_kernel; the threshold select's stage entry point takes sets of
+// this size).
 #ifndef SMX_SEED_PER_THREAD
 #define SMX_SEED_PER_THREAD 16   // seed rows per query / 256 (a build-time knob)
 #endif
 constexpr int kSeedKeys = 256 * SMX_SEED_PER_THREAD;
-constexpr int kSeedMaxMfma = 32;   // seed leaves per query on the seed scan
-// a seed-scan unit: one wave, 16 queries of a leaf x 256 rows (8 tiles)
-constexpr int kSeedSpans = kSeedKeys / 256;
 constexpr uint32_t kItemNarrow = 1u << 31;
 // WorklistArgs::narrow / SeedArgs::narrow: 0 = 32-slot tiles only, 1 = a
 // leaf's last <= 16 queries in a 16-slot tile, kNarrowOnly = 16-slot tiles only
@@ -175,15 +171,6 @@ struct ScanArgs {
 struct SeedArgs {
   const int32_t* topl_leaf;   // [nq][L]
   const float* topl_dist;     // [nq][L]
-  // the seed scan (mfma != 0): per leaf its seeding queries, per query its
-  // granted seed leaves and their distances
-  int mfma;
-  const uint32_t* seed_count; // [nl] strided (kCounterStride)
-  const uint64_t* seed_list;  // [nl][kSeedSlots] query | seed index << 24 | (o | c << 16) << 32
-  const uint32_t* seed_total;  // [nq][2] rows spanned, rows granted
-  uint32_t* seed_keys;         // [nq][kSeedKeys] ordered distances (SeedClaims' layout)
-  const uint32_t* seed_units;  // leaf << 6 | group << 4 | span, one per wave unit
-  const uint32_t* seed_nunits; // their number (a counter)
   uint32_t narrow;             // the work list's tile mode (kNarrowOnly: 16-slot query tiles)
   int nl;
   // the inversion (pair scatter): every (query, leaf) pair's slot in its
@@ -330,14 +317,6 @@ struct FrontArgs {
   float* mult = nullptr;            // [nq]
   float* inv = nullptr;             // [nq]
   int one_to_many = 0;              // the single-query partition scores (A.8 order)
-  // the seed scan's claims (NULL: the per-query seed kernel)
-  uint32_t* seed_count = nullptr;   // [nl] strided, zeroed by init
-  uint64_t* seed_list = nullptr;    // [nl][kSeedSlots]
-  uint32_t* seed_total = nullptr;   // [nq][2]
-  uint32_t* seed_keys = nullptr;    // [nq][kSeedKeys] (dropped seed leaves' ranges)
-  uint32_t* seed_units = nullptr;   // [nq * kSeedMaxMfma * kSeedSpans] the seed scan's units
-  uint32_t* seed_nunits = nullptr;  // their count (zeroed by init)
-  int seed = 0;                     // seed leaves per query (<= kSeedMaxMfma)
 };
 hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int nq,
                                int L, int32_t* out_leaf, float* out_dist,
@@ -375,15 +354,6 @@ WorklistArgs MakeWorklistArgs(const DeviceIndex& ix, const uint32_t* leaf_count,
 // builds the whole work list (ix.nl <= kFusedWorklistLeaves).
 hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s,
                       const WorklistArgs* wl = nullptr);
-// The seed scan (MFMA): every listed (leaf, seeding query) pair's distances
-// into seed_keys; with `wl`, extra blocks build the whole work list
-// (ix.nl <= kFusedWorklistLeaves).  Needs 1 <= a.seed <= kSeedMaxMfma;
-// `blocks` 4-wave blocks walk the call's seed units.
-hipError_t LaunchSeedScan(const DeviceIndex& ix, const SeedArgs& a, int blocks, hipStream_t s,
-                          const WorklistArgs* wl = nullptr);
-// Per query its threshold from the seed scan's distances, then its pairs'
-// lane records (after the work list: they need leaf_item0).
-hipError_t LaunchSeedSelect(const SeedArgs& a, int nq, hipStream_t s);
 hipError_t LaunchKthKeys(const uint32_t* vals, int sets, int kk, uint64_t* out, hipStream_t s);
 // Every (query, leaf) pair's lane record into its leaf's work items (after
 // LaunchWorklist and the seed thresholds: each record carries its sum limit).

@@ -602,81 +602,8 @@ struct TopLTail {
   uint32_t* leaf_count;   // or NULL
   uint32_t* rank;
   LutParams lut;          // lut.lut NULL: no LUT
-  uint32_t* seed_count;   // the seed scan's claims, or NULL
-  uint64_t* seed_list;
-  uint32_t* seed_total;
-  uint32_t* seed_keys;
-  uint32_t* seed_units;
-  uint32_t* seed_nunits;
-  const uint32_t* leaf_size;
-  int seed;
   int lut_split;   // topl_block_kernel: the LUTs by their own blocks [nq, 2 nq)
 };
-
-// The query's first `seed` leaves claim slots in those leaves' seed lists
-// (the seed scan, seed_scan_kernel).  The seed values are SeedTau's: the
-// leaves in the query's order, leaf i's first c_i rows, c_i = min(size_i,
-// kSeedKeys - o_i), o_i = the rows of the leaves before it, so that the
-// query's keys seed_keys[q][o_i + dp] are exactly the values SeedTau would
-// rank.  A returning atomic on the leaf's seed counter gives the slot; a leaf
-// lists at most kSeedSlots seeding queries, and a query without a slot goes
-// without that leaf: its range is filled with "no value" here (the k'-th of a
-// subset of the candidates still bounds the final k'-th from above).
-// seed_total[q] = {rows spanned, rows granted}.  Block-wide (every thread
-// calls; seed <= kSeedMaxMfma <= 64).
-__device__ void SeedClaims(int qi, uint32_t m, const uint64_t* keys, const TopLTail& tail) {
-  if (!tail.seed_count) return;   // (uniform)
-  __shared__ uint32_t s_drop, s_off[kSeedMaxMfma], s_cnt[kSeedMaxMfma];
-  const int lane = threadIdx.x & 63;
-  if (threadIdx.x < 64) {
-    const int nseed = min(tail.seed, int(min(m, uint32_t(kSeedMaxMfma))));
-    const bool has = lane < nseed;
-    const uint32_t leaf = has ? uint32_t(keys[lane] & 0xFFFFFFFFu) : 0u;
-    const uint32_t sz = has ? tail.leaf_size[leaf] : 0u;
-    uint32_t inc = sz;
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t t = uint32_t(__shfl_up(int(inc), off));
-      if (lane >= off) inc += t;
-    }
-    const uint32_t o = inc - sz;
-    const uint32_t c = o < uint32_t(kSeedKeys) ? min(sz, uint32_t(kSeedKeys) - o) : 0u;
-    bool dropped = false;
-    if (c > 0) {
-      const uint32_t slot = atomicAdd(&tail.seed_count[size_t(leaf) * kCounterStride], 1u);
-      if (slot < uint32_t(kSeedSlots)) {
-        tail.seed_list[size_t(leaf) * kSeedSlots + slot] =
-            (uint64_t(o | (c << 16)) << 32) | (uint32_t(qi) | (uint32_t(lane) << 24));
-        if (slot % 16u == 0) {   // a new group of 16: its wave units, 256 rows each
-          const uint32_t spans = (min(sz, uint32_t(kSeedKeys)) + 255u) / 256u;
-          const uint32_t u0 = atomicAdd(tail.seed_nunits, spans);
-          for (uint32_t sp = 0; sp < spans; ++sp)
-            tail.seed_units[u0 + sp] = (leaf << 6) | ((slot / 16u) << 4) | sp;
-        }
-      } else {
-        dropped = true;
-      }
-    }
-    uint32_t granted = dropped ? 0u : c;
-    for (int off = 32; off > 0; off >>= 1) granted += uint32_t(__shfl_xor(int(granted), off));
-    const uint64_t drop = __ballot(dropped);
-    if (lane < kSeedMaxMfma) {
-      s_off[lane] = o;
-      s_cnt[lane] = c;
-    }
-    const uint32_t span = min(uint32_t(__shfl(int(inc), 63)), uint32_t(kSeedKeys));
-    if (lane == 0) {
-      s_drop = uint32_t(drop);
-      tail.seed_total[2 * size_t(qi)] = span;
-      tail.seed_total[2 * size_t(qi) + 1] = granted;
-    }
-  }
-  __syncthreads();
-  for (uint32_t d = s_drop; d; d &= d - 1) {   // (block-uniform; rare)
-    const int i = __builtin_ctz(d);
-    for (uint32_t j = threadIdx.x; j < s_cnt[i]; j += blockDim.x)
-      tail.seed_keys[size_t(qi) * kSeedKeys + s_off[i] + j] = 0xFFFFFFFFu;
-  }
-}
 
 __device__ void TopLFinish(int qi, int L, uint32_t m, const uint64_t* sel, int32_t* out_leaf,
                            float* out_dist, const TopLTail& tail) {
@@ -703,7 +630,6 @@ __device__ void TopLFinish(int qi, int L, uint32_t m, const uint64_t* sel, int32
       if (tail.leaf_count && uint32_t(i) < m) tail.rank[size_t(qi) * L + i] = rk[u];
     }
   }
-  SeedClaims(qi, m, sel, tail);
   if (tail.lut.lut) {
     __syncthreads();
     BuildLut(qi, tail.lut);
@@ -887,7 +813,6 @@ __device__ __forceinline__ void TopLBlock(const float* __restrict__ scores, int 
     if (tail.leaf_count && has) tail.rank[size_t(qi) * L + i] = atomicAdd(&tail.leaf_count[size_t(leaf) * kCounterStride], 1u);
   }
   SMX_PHASE(0, qi, 4);
-  SeedClaims(qi, m, srt, tail);
   if (tail.lut.lut && !tail.lut_split) BuildLut(qi, tail.lut);
   SMX_PHASE(0, qi, 5);
 }
@@ -3005,161 +2930,6 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   }
 }
 
-// ---------------------------------------------------------------------------
-// The seed scan: every query's threshold from its first `seed` leaves on the
-// 16-slot MFMA path instead of per-query LDS lookups.  The top-L kernel has
-// listed, per leaf, the queries it seeds with each one's row budget
-// (SeedClaims: at most kSeedSlots records {query, seed index, offset o, rows
-// c}) and, per group of 16 of them, one wave unit per 256 rows of the leaf
-// (up to kSeedKeys).  The launch's waves walk the units: a unit's wave issues
-// the code loads of its 8 tiles at once, then runs them for its 16 queries up
-// to the group's largest budget, storing each query's distances of rows dp <
-// c as ordered bits at seed_keys[q][o + dp] -- the same values, in the same
-// places, as SeedTau ranks: d = fl(fl(S inv) + bias), the scan's distance, so
-// the kk-th of them bounds the final kk-th from above.  Wave w of the seed
-// blocks takes units w, w + stride, ..., their records loaded ahead.  Blocks below
-// `wl_blocks` build the work list (WorklistFusedBlock), as the per-query seed
-// launch does -- first, so that they are resident beside the seed waves.
-// ---------------------------------------------------------------------------
-static_assert(kSeedSpans <= 16 && kSeedSlots / 16 <= 4, "seed unit fields");
-
-template <int K>
-__global__ void __launch_bounds__(256) seed_scan_kernel(SeedArgs a, WorklistArgs w,
-                                                        int wl_blocks) {
-  if (int(blockIdx.x) < wl_blocks) {   // the fused work-list blocks
-    WorklistFusedBlock(w, int(blockIdx.x));
-    return;
-  }
-  constexpr int NW = ((((K + 1) / 2) + 3) / 4);
-  constexpr int W = 4 * NW;
-  constexpr int K16 = (K + 3) / 4;
-  constexpr int T = 8;   // tiles per unit
-  __shared__ __align__(256) v4i opnd_tab[32];
-  v4i* const grp_tab = opnd_tab;
-  int* const pos_tab = reinterpret_cast<int*>(opnd_tab + 16);
-  if (threadIdx.x < 16) {   // the scan's operand tables (lut16_scan_kernel)
-    const uint32_t g0 = threadIdx.x & 3u, g1 = threadIdx.x >> 2;
-    v4i t = {0, 0, 0, 0};
-    t[g0 >> 1] = int(1u << (16 * (g0 & 1u)));
-    t[2 + (g1 >> 1)] = int(1u << (16 * (g1 & 1u)));
-    grp_tab[threadIdx.x] = t;
-    pos_tab[4 * threadIdx.x] = int((threadIdx.x & 3u) * 0x5555u | ((threadIdx.x >> 2) * 0x5555u) << 16);
-    pos_tab[4 * threadIdx.x + 1] = 0;
-  }
-  __syncthreads();   // (the last barrier)
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint32_t nunits = *a.seed_nunits;
-  const uint32_t lane_off = uint32_t((lane >> 5) * 32 + (lane & 15)) * uint32_t(W);
-  const uint32_t sh = uint32_t((lane >> 4) & 1) * 8u;
-  const uint32_t rg = uint32_t(lane >> 4);   // D rows 4 rg + e of column lane % 16
-  // units u0, u0 + stride, ... of this wave, two stages ahead: the unit
-  // record of the one after next and the leaf records of the next are in
-  // flight while this one runs
-  const uint32_t stride = (gridDim.x - uint32_t(wl_blocks)) * 4u;
-  uint32_t u = (blockIdx.x - uint32_t(wl_blocks)) * 4u + uint32_t(wid);
-  const uint32_t sl16 = uint32_t(lane & 15);
-  auto unit_rec = [&](uint32_t v) { return v < nunits ? a.seed_units[v] : 0u; };
-  struct LeafRecs {
-    uint32_t ur, cnt;
-    uint64_t rec, toff;
-  };
-  auto leaf_recs = [&](uint32_t ur) {   // (slots past the count hold stale records)
-    const uint32_t leaf = ur >> 6, g = ((ur >> 4) & 3u) * 16u;
-    return LeafRecs{ur, a.seed_count[size_t(leaf) * kCounterStride],
-                    a.seed_list[size_t(leaf) * kSeedSlots + g + sl16], a.tile_off[leaf]};
-  };
-  LeafRecs nxt = leaf_recs(unit_rec(u));
-  uint32_t ur2 = unit_rec(u + stride);
-  for (; u < nunits; u += stride) {   // (wave-uniform)
-    const LeafRecs cur = nxt;
-    nxt = leaf_recs(ur2);
-    ur2 = unit_rec(u + 2u * stride);
-    const uint32_t g = ((cur.ur >> 4) & 3u) * 16u, row0 = (cur.ur & 15u) * 256u;
-    const uint32_t cnt = min(cur.cnt, uint32_t(kSeedSlots));
-    const bool valid = g + sl16 < cnt;
-    const uint64_t rec = valid ? cur.rec : 0ull;
-    const uint32_t qi = uint32_t(rec) & 0xFFFFFFu, si = uint32_t(rec) >> 24;
-    const uint32_t o = uint32_t(rec >> 32) & 0xFFFFu, c = uint32_t(rec >> 48);
-    uint32_t need = c;   // the group's largest budget
-    for (int off = 8; off > 0; off >>= 1) need = max(need, uint32_t(__shfl_xor(int(need), off)));
-    if (need <= row0) continue;
-    const uint32_t tiles = min(uint32_t(T), (need - row0 + 31u) / 32u);
-    const uint8_t* tseg = a.tiles + (cur.toff + row0 / 32u) * 64ull * W;
-    uint32_t ca[T][NW], cb[T][NW];
-#pragma unroll
-    for (int i = 0; i < T; ++i) {
-      const uint32_t t = min(uint32_t(i), tiles - 1u);   // (clamped: no branch)
-      const uint8_t* tp = tseg + size_t(t) * (64 * W) + lane_off;
-      LoadCodes<K>(tp, ca[i]);
-      LoadCodes<K>(tp + 16 * W, cb[i]);
-    }
-    const float bias = (valid && a.residual) ? a.topl_dist[size_t(qi) * a.L + si] : 0.0f;
-    const float inv = a.inv[qi];
-    uint32_t* out = a.seed_keys + size_t(qi) * kSeedKeys + o;
-    v8i b[K16];
-    const v8i* bp = reinterpret_cast<const v8i*>(reinterpret_cast<const uint8_t*>(a.lut) +
-                                                  size_t(qi) * (LutRows(K) * 16) +
-                                                  uint32_t(lane >> 4) * 32u);
-#pragma unroll
-    for (int s2 = 0; s2 < K16; ++s2) b[s2] = bp[4 * s2];
-#pragma unroll
-    for (int i = 0; i < T; ++i) {
-      if (uint32_t(i) >= tiles) break;   // (wave-uniform)
-      uint32_t xa[NW], xb[NW];
-#pragma unroll
-      for (int j = 0; j < NW; ++j) {
-        xa[j] = ca[i][j] >> sh;
-        xb[j] = cb[i][j] >> sh;
-      }
-      v4i acc_a, acc_b;
-      TileSmfmac16<K, 3>(xa, xb, b, grp_tab, pos_tab, acc_a, acc_b);
-      // rows row0 + 32 i + 16 ch + 4 rg + e of chain ch: 4 contiguous keys each
-      const uint32_t d0 = row0 + uint32_t(i) * 32u + 4u * rg;
-#pragma unroll
-      for (int ch = 0; ch < 2; ++ch) {
-        const v4i& acc = ch ? acc_b : acc_a;
-        const uint32_t dp = d0 + 16u * uint32_t(ch);
-        uint32_t k4[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) k4[e] = OrderedBits(DistOf(acc[e], inv, bias));
-        if (dp + 3u < c && ((o + dp) & 3u) == 0) {
-          *reinterpret_cast<uint4*>(out + dp) = make_uint4(k4[0], k4[1], k4[2], k4[3]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (dp + uint32_t(e) < c) out[dp + e] = k4[e];
-        }
-      }
-    }
-  }
-}
-
-// Per query (one 256-thread block): its threshold key from the seed scan's
-// distances (seed_keys[q][0, span), "no value" where a seed leaf was not
-// granted; SeedTau's rule when at least kk were), then every one of its
-// (query, leaf) pairs into the scan's work items with its sum limit -- the
-// pair scatter of the per-query path, one launch for both.
-__global__ void __launch_bounds__(256) seed_select_kernel(SeedArgs a) {
-  const int qi = int(blockIdx.x);
-  const int tid = threadIdx.x;
-  const uint32_t span = a.seed_total[2 * size_t(qi)], granted = a.seed_total[2 * size_t(qi) + 1];
-  uint64_t T = kNoThreshold;
-  const uint32_t kk = uint32_t(a.kk);
-  if (kk > 0 && granted >= kk) {   // (block-uniform)
-    const uint32_t* keys = a.seed_keys + size_t(qi) * kSeedKeys;
-    uint32_t vals[kSeedPerThread];
-#pragma unroll
-    for (int k = 0; k < kSeedPerThread; ++k) {
-      const uint32_t idx = uint32_t(tid) + 256u * uint32_t(k);
-      vals[k] = idx < span ? keys[idx] : 0xFFFFFFFFu;
-    }
-    T = ThresholdOfVals(vals, kk);
-  }
-  if (tid == 0) a.tau_key[qi] = T;
-  for (int i = tid; i < a.L; i += 256)
-    PairScatterTau(a, size_t(qi) * a.L + size_t(i), a.leaf_item0, T);
-}
-
 // Stage entry point of the threshold select: per set of kSeedKeys ordered
 // distance bits (0xFFFFFFFF = none), ThresholdOfVals' key, or kNoThreshold
 // when the set holds fewer than kk values (SeedTau's rule).
@@ -4097,14 +3867,6 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   static const int dbg = [] { const char* e = std::getenv("SMX_DBG_FRONT"); return e ? std::atoi(e) : 0; }();
   tail.leaf_count = (dbg & 1) ? nullptr : f.leaf_count;
   tail.rank = f.rank;
-  tail.seed_count = f.seed_count;
-  tail.seed_list = f.seed_list;
-  tail.seed_total = f.seed_total;
-  tail.seed_keys = f.seed_keys;
-  tail.seed_units = f.seed_units;
-  tail.seed_nunits = f.seed_nunits;
-  tail.leaf_size = ix.leaf_size;
-  tail.seed = f.seed;
   tail.lut = LutParams{queries, ix.dim, ix.codebook, ix.nb, ix.dpb, LutRows(ix.ksteps), ix.metric,
                        ix.residual, (dbg & 2) ? nullptr : f.lut, f.mult, f.inv, nullptr};
   if (f.one_to_many) {
@@ -4371,42 +4133,6 @@ hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStrea
     default:
       return hipErrorInvalidValue;
   }
-  return hipGetLastError();
-}
-
-#define SMX_SEED_SCAN_CASE(KV)                                                              \
-  case KV:                                                                                 \
-    hipLaunchKernelGGL(seed_scan_kernel<KV>, dim3(sb + nwl), dim3(256), 0, s, a,            \
-                       wl ? *wl : WorklistArgs{}, nwl);                                     \
-    break;
-
-hipError_t LaunchSeedScan(const DeviceIndex& ix, const SeedArgs& a, int blocks, hipStream_t s,
-                          const WorklistArgs* wl) {
-  static_assert(256 * kSeedPerThread == kSeedKeys, "the seed select holds kSeedKeys values");
-  if (wl && wl->nl > kFusedWorklistLeaves) return hipErrorInvalidValue;
-  if (a.seed < 1 || a.seed > kSeedMaxMfma) return hipErrorInvalidValue;
-  const int sb = std::max(blocks, 1);   // 4-wave blocks walking the seed units
-  const int nwl = wl ? (wl->nl + kWlPosPerBlock - 1) / kWlPosPerBlock : 0;
-  switch (ix.ksteps) {
-    SMX_SEED_SCAN_CASE(4)
-    SMX_SEED_SCAN_CASE(8)
-    SMX_SEED_SCAN_CASE(12)
-    SMX_SEED_SCAN_CASE(16)
-    SMX_SEED_SCAN_CASE(20)
-    SMX_SEED_SCAN_CASE(24)
-    SMX_SEED_SCAN_CASE(26)
-    SMX_SEED_SCAN_CASE(28)
-    SMX_SEED_SCAN_CASE(32)
-    default:
-      return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
-}
-#undef SMX_SEED_SCAN_CASE
-
-hipError_t LaunchSeedSelect(const SeedArgs& a, int nq, hipStream_t s) {
-  if (nq == 0) return hipSuccess;
-  hipLaunchKernelGGL(seed_select_kernel, dim3(nq), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -75,15 +75,12 @@ int EffectiveKSteps(int nb) {
 }
 
 // Per-call counters (one buffer, zeroed by the partition kernel):
-//   [0, nl)            pairs per leaf
-//   [nl, 2 nl)         seeding queries per leaf (the seed scan's claims)
+//   [0, nl)            pairs per leaf (strided, kCounterStride)
 //   [stats, +32)       stats words (SelectArgs::overflow and the work-list totals)
 struct CounterLayout {
-  uint32_t seeds, units, stats, words;
+  uint32_t stats, words;
   explicit CounterLayout(int nl) {
-    seeds = uint32_t(nl) * smx::kCounterStride;       // nl strided leaf counters first
-    units = 2u * uint32_t(nl) * smx::kCounterStride;  // then the seed counters, the seed units'
-    stats = units + smx::kCounterStride;
+    stats = uint32_t(nl) * smx::kCounterStride;
     words = stats + 32u;
   }
 };
@@ -105,10 +102,6 @@ struct Workspace {
   float* mult = nullptr;
   float* inv = nullptr;
   uint32_t* counters = nullptr;     // see CounterLayout
-  uint64_t* seed_list = nullptr;    // [nl][kSeedSlots] the leaves' seeding queries
-  uint32_t* seed_total = nullptr;   // [nq][2] seed rows spanned, granted
-  uint32_t* seed_units = nullptr;   // [nq * kSeedMaxMfma * kSeedSpans] seed-scan wave units
-  uint32_t* seed_keys = nullptr;    // [nq][kSeedKeys] seed distances
   uint32_t* rank = nullptr;         // [nq*L] each pair's position in its leaf's list
   uint32_t* leaf_item0 = nullptr;   // [nl] each leaf's first work item
   smx::WorkItem* work = nullptr;    // [max_items]
@@ -127,7 +120,7 @@ struct Workspace {
   void Release() {
     DFree(queries); DFree(topl_leaf); DFree(topl_dist); DFree(scores); DFree(lut); DFree(mult);
     DFree(inv);
-    DFree(counters); DFree(seed_list); DFree(seed_total); DFree(seed_units); DFree(seed_keys); DFree(rank); DFree(leaf_item0); DFree(lanes); DFree(wave_start);
+    DFree(counters); DFree(rank); DFree(leaf_item0); DFree(lanes); DFree(wave_start);
     DFree(pos_unit0); DFree(gunits); DFree(wl_part);
     DFree(work); DFree(tau); DFree(cand); DFree(cand_count); DFree(out_idx);
     DFree(out_dist);
@@ -156,10 +149,6 @@ struct smx_index {
   bool narrow_tiles = true;
   bool narrow_only = false;        // SMX_NARROW=2: 16-slot tiles only whatever the density
   bool narrow_mixed_only = false;  // SMX_NARROW=3: never the 16-slot-only mode
-  // SMX_SEED_MFMA=1: the per-query thresholds by the seed scan (MFMA,
-  // seed_scan_kernel + seed_select_kernel) instead of the per-query
-  // LDS-lookup kernel (measured slower at glove shape: 0.180 vs 0.164 ms)
-  bool seed_mfma = false;
   // above fused_worklist_leaves: the work-list launches on this stream before
   // the seed (true; SMX_SERIAL_WORKLIST=0: on the side stream beside it --
   // same box A/B, configs[3]/[4]: 0.578 vs 0.584 and 1.478 vs 1.495 ms/step)
@@ -390,10 +379,15 @@ uint32_t AutoCap(int L, int kk, int seed) {
 }
 
 // Work items the workspace holds for `pairs` (query, leaf) pairs: one per
-// (leaf, 32-query tile, chunk of >= 8 tiles).
+// (leaf, query tile, chunk of >= 8 tiles).  A leaf with c queries has at most
+// ceil(c / 16) query tiles (the 16-slot-only mode, kNarrowOnly: every tile 16
+// wide; the other modes use fewer), so sum_leaf ceil(c / 16) <= pairs / 16 +
+// nl; a leaf of n rows has ceil(ceil(n / 32) / chunk_tiles) chunks, at most
+// the bound below for any chunk_tiles smx_set_tuning accepts (>= 8).
+// (tests/worklist_model.py: max_items, asserted against every built list)
 uint32_t MaxItems(const smx::DeviceIndex& ix, size_t pairs) {
   const uint32_t chunks = (uint32_t((ix.max_leaf + 31) / 32) + 7) / 8 + 1;  // chunk >= 8
-  return uint32_t((pairs / smx::kQueriesPerTile + ix.nl + 1) * chunks);
+  return uint32_t((pairs / smx::kNarrowSlots + ix.nl + 1) * chunks);
 }
 
 int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
@@ -429,10 +423,6 @@ int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
       (rc = DAlloc(&w.topl_dist, apairs)) || (rc = DAlloc(&w.scores, size_t(anq) * nl)) ||
       (rc = DAlloc(&w.lut, size_t(anq) * smx::LutRows(ix.ksteps) * 16)) || (rc = DAlloc(&w.mult, anq)) ||
       (rc = DAlloc(&w.inv, anq)) || (rc = DAlloc(&w.counters, CounterLayout(nl).words)) ||
-      (rc = DAlloc(&w.seed_list, size_t(nl) * smx::kSeedSlots)) ||
-      (rc = DAlloc(&w.seed_total, 2 * size_t(anq))) ||
-      (rc = DAlloc(&w.seed_units, size_t(anq) * smx::kSeedMaxMfma * smx::kSeedSpans)) ||
-      (rc = DAlloc(&w.seed_keys, size_t(anq) * smx::kSeedKeys)) ||
       (rc = DAlloc(&w.rank, apairs)) || (rc = DAlloc(&w.leaf_item0, size_t(nl))) ||
       (rc = DAlloc(&w.lanes, size_t(max_items) * smx::kQueriesPerTile)) ||
       (rc = DAlloc(&w.wave_start, size_t(std::max(h->grid, 1)))) ||
@@ -542,18 +532,6 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sa.seed = seed;
   sa.kk = kk;
   sa.narrow = narrow;
-  // the seed scan (MFMA) for 1..kSeedMaxMfma seed leaves; SMX_SEED_MFMA=0:
-  // the per-query seed kernel and a separate pair scatter
-  // (the seed lists hold query | seed index << 24: nq < 2^24)
-  const bool seed_mfma = h->seed_mfma && seed >= 1 && seed <= smx::kSeedMaxMfma &&
-                         nq < (1 << 24);
-  sa.mfma = seed_mfma ? 1 : 0;
-  sa.seed_count = w.counters + lay.seeds;
-  sa.seed_list = w.seed_list;
-  sa.seed_total = w.seed_total;
-  sa.seed_keys = w.seed_keys;
-  sa.seed_units = w.seed_units;
-  sa.seed_nunits = w.counters + lay.units;
   sa.nl = nl;
   sa.residual = ix.residual;
 
@@ -648,7 +626,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     // front end: state reset, partition scores, top-L + ranks + LUTs
     smx::FrontArgs f;
     f.init.counters = w.counters;
-    f.init.n_counters = 2u * uint32_t(nl) + 1u;   // pair, seed and seed-unit counters
+    f.init.n_counters = uint32_t(nl);   // the pair counters
     f.init.stats = stats;
     f.init.n_stats = 32u;
     f.init.cand_count = w.cand_count;
@@ -661,15 +639,6 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     f.mult = w.mult;
     f.inv = w.inv;
     f.one_to_many = single ? 1 : 0;
-    if (seed_mfma) {
-      f.seed_count = w.counters + lay.seeds;
-      f.seed_list = w.seed_list;
-      f.seed_total = w.seed_total;
-      f.seed_keys = w.seed_keys;
-      f.seed_units = w.seed_units;
-      f.seed_nunits = w.counters + lay.units;
-      f.seed = seed;
-    }
     SMX_HIP(smx::LaunchPartitionTopL(ix, queries, nq, L, w.topl_leaf, w.topl_dist, w.scores, s, &f));
     Mark(h, 1, s);
     if (ix.nl <= h->fused_worklist_leaves) {
@@ -679,10 +648,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
           ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes, w.wave_start, h->grid,
           stats + 3, code_bytes, h->chunk_tiles, narrow, bd);
       Mark(h, 3, s);
-      if (seed_mfma)
-        SMX_HIP(smx::LaunchSeedScan(ix, sa, 2 * h->cus, s, &wla));
-      else
-        SMX_HIP(smx::LaunchSeed(ix, sa, nq, s, &wla));
+      SMX_HIP(smx::LaunchSeed(ix, sa, nq, s, &wla));
       Mark(h, 4, s);
     } else if (h->serial_worklist) {
       // the work-list launches, then the seed, on one stream: beside the
@@ -692,10 +658,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
                                   w.wave_start, h->grid, stats + 3, code_bytes, h->chunk_tiles,
                                   narrow, w.wl_part, bd, s));
       Mark(h, 3, s);
-      if (seed_mfma)
-        SMX_HIP(smx::LaunchSeedScan(ix, sa, 2 * h->cus, s));
-      else
-        SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
+      SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
       Mark(h, 4, s);
     } else {
       // Fork.  Side stream: the work list (and the empty slots' records);
@@ -708,10 +671,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
       // graph keeps it on the launch queue with the kernels before and after
       // it; the shorter work-list branch pays the cross-queue edges.
       SMX_HIP(hipEventRecord(h->fork_ev, s));
-      if (seed_mfma)
-        SMX_HIP(smx::LaunchSeedScan(ix, sa, 2 * h->cus, s));
-      else
-        SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
+      SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
       Mark(h, 4, s);
       SMX_HIP(hipStreamWaitEvent(h->side, h->fork_ev, 0));
       SMX_HIP(smx::LaunchWorklist(ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes,
@@ -722,11 +682,8 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
       SMX_HIP(hipStreamWaitEvent(s, h->join_ev, 0));   // join
     }
     // every pair's lane record with its sum limit (needs the work list and
-    // the seed thresholds; the seed scan's select computes those first)
-    if (seed_mfma)
-      SMX_HIP(smx::LaunchSeedSelect(sa, nq, s));
-    else
-      SMX_HIP(smx::LaunchPairScatter(ix, sa, nq, s));
+    // the seed thresholds)
+    SMX_HIP(smx::LaunchPairScatter(ix, sa, nq, s));
     Mark(h, 5, s);
     SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s, narrow));
     Mark(h, 6, s);
@@ -970,7 +927,6 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
     h->narrow_only = nw[0] == '2';
     h->narrow_mixed_only = nw[0] == '3';
   }
-  if (const char* sm = std::getenv("SMX_SEED_MFMA")) h->seed_mfma = sm[0] != '0';
   if (const char* sw = std::getenv("SMX_SERIAL_WORKLIST")) h->serial_worklist = sw[0] != '0';
   const char* ng = std::getenv("SMX_NO_GRAPH");
   // Eager launches by default: six kernels a call queue back to back on the

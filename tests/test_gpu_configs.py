@@ -9,8 +9,8 @@ queries of the batch, so a subset is a complete check of those queries.
 
   configs[1] glove-100-angular: 1,183,514 x 100 dot, 1000 leaves, L=100,
              nq=1000, reorder 100, k=10 (lut16_scan_kernel<26>)
-  configs[2] SIFT1M: squared L2, non-residual, 2000 leaves, D=128
-             (lut16_scan_kernel<32>), 300k rows
+  configs[2] SIFT1M: 1,000,000 x 128 squared L2, non-residual, 2000
+             leaves (lut16_scan_kernel<32>), the bench workload
   configs[3] 100M x 96 dot + SOAR, 10000 leaves, range split over 8 ranks:
              the 8 shards and the merge kernel on one GPU (K=24), 400k rows
   configs[4] Deep1B 96-d, 50000 leaves (global-memory top-L, 16-bit global
@@ -75,18 +75,30 @@ def test_glove_full_shape(oracle):
 
 
 def test_sift_shape(oracle):
-    """configs[2]: squared L2, non-residual (pipeline B), B=64 -> K=32."""
+    """configs[2] at full size, the bench workload itself: 1,000,000 x 128
+    squared L2, non-residual (pipeline B), 2000 leaves (~500 rows per leaf),
+    B=64 -> K=32; the whole 1000-query batch at L = 100 (the configured
+    leaves_to_search) and at the recall gate's L = 20, 128 queries checked
+    against the oracle at each."""
     from scann_amd import _native, index_builder, synthetic
-    db, q = synthetic.sift_like(n=300_000, seed=3)
-    ix = index_builder.build_tree_ah(db, 1, 2000, 2, training_iterations=6,
-                                     ah_training_iterations=6, seed=3)
+    db, q = synthetic.sift_like(seed=3)
+    ix = index_builder.build_tree_ah(db, 1, 2000, 2, training_iterations=12,
+                                     ah_training_iterations=10, seed=3)
     assert ix.num_blocks == 64 and not ix.residual and ix.global_topn_shift_value() == 0
+    assert ix.num_datapoints == 1_000_000 and ix.leaf_sizes().mean() == 500
     nat = _native.NativeIndex(ix)
-    for leaves, reorder in ((100, True), (40, False)):
+    truth = synthetic.brute_force_topk(db, q, 10, 1)
+    recall = {}
+    for leaves, reorder in ((100, True), (20, True), (10, True), (40, False)):
         gi, gd, gc = nat.search_batched(q, leaves, 100, 10, reorder)
         oi, od, oc = oracle.search(ix, q[:SUB], leaves, 100, 10, reorder, oracle.MODE_IDEAL, 16)
         np.testing.assert_array_equal(gc[:SUB], oc)
         _check(gi[:SUB], gd[:SUB], oi, od)
+        if reorder:
+            recall[leaves] = synthetic.recall_at_k(gi.astype(np.int64), truth, 10)
+    # the data discriminates leaves_to_search: below the gate at L = 10
+    assert recall[10] < 0.95 <= recall[100], recall
+    assert recall[10] < recall[20] <= recall[100], recall
     pi, pd, pc = nat.search_pre_reorder(q[:SUB], 100, 100)
     oi, od, oc = oracle.search_pre_reorder(ix, q[:SUB], 100, 100, oracle.MODE_IDEAL, 16)
     _check(pi, pd, oi, od)

@@ -73,3 +73,23 @@ def test_16_slot_tiles_only(seed):
         assert qt == (int(counts[leaf]) + 15) // 16
     assert wm.query_tiles(17, 2) == (0, 2) and wm.query_tiles(16, 2) == (0, 1)
     assert wm.query_tiles(0, 2) == (0, 0) and wm.query_tiles(64, 2) == (0, 4)
+
+
+@pytest.mark.parametrize("chunk_tiles", [8, 16])
+@pytest.mark.parametrize("seed", range(4))
+def test_item_capacity_at_small_chunks(seed, chunk_tiles):
+    """The item buffer (MaxItems) holds every list at the smallest chunk
+    smx_set_tuning accepts, in the 16-slot-only mode (ceil(c / 16) query
+    tiles per leaf): e.g. 48 queries on every 64-tile leaf needs 3 x 8 = 24
+    items per leaf, more than the 22.5 per leaf a pairs / 32 bound gave."""
+    rng = np.random.default_rng(900 + seed)
+    nl = int(rng.integers(20, 400))
+    sizes = [64 * 32] * nl if seed == 0 else [int(x) for x in rng.integers(0, 4000, nl)]
+    counts = [48] * nl if seed == 0 else [int(x) for x in rng.poisson(rng.uniform(1, 60), nl)]
+    for small in (True, False, 2):
+        wm.check(sizes, counts, grid=256, chunk_tiles=chunk_tiles, small=small)
+    if seed == 0:
+        wl = wm.build(sizes, counts, 256, 8, 2)
+        assert len(wl["work"]) == 24 * nl
+        # the old pairs / 32 bound, at the chunk count this list really has
+        assert len(wl["work"]) > (sum(counts) / 32 + nl) * 8

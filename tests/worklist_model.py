@@ -168,8 +168,18 @@ def list_segments(wl, b, max_segs=512):
     return segs
 
 
+def max_items(sizes, pairs):
+    """The workspace's item capacity (smx_searcher.hip MaxItems): (pairs / 16
+    + nl + 1) x (ceil(max_tiles / 8) + 1)."""
+    max_leaf = max(sizes) if len(sizes) else 0
+    chunks = ((max_leaf + 31) // 32 + 7) // 8 + 1
+    return (pairs // 16 + len(sizes) + 1) * chunks
+
+
 def check(sizes, counts, grid=256, chunk_tiles=20, small=True):
     wl = build(sizes, counts, grid, chunk_tiles, small)
+    cap = max_items(sizes, int(sum(counts)))
+    assert len(wl["work"]) <= cap, f"{len(wl['work'])} items > MaxItems {cap}"
     assert all(w is not None for w in wl["wave_start"]), "a workgroup's share is not written"
     seen = {}
     for b in range(grid):

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of environment switches of the product library on one box: the bench
 # line of each setting, interleaved twice.
-#   ENVS="SMX_NARROW=0 SMX_NARROW=1,SMX_SEED_MFMA=0" TAG=x STEPS=200 BENCH_ARGS="--config deep1b" bash tools/ab_env.sh
+#   ENVS="SMX_NARROW=0 SMX_NARROW=1,SMX_LUT_SPLIT=0" TAG=x STEPS=200 BENCH_ARGS="--config deep1b" bash tools/ab_env.sh
 # A setting is one or more VAR=value joined by commas.
 # Output: gpurun_out/$TAG/<setting>.json (one line per repetition).
 set -o pipefail

@@ -1,6 +1,7 @@
-"""Turn a rocprofv3 --pmc FETCH_SIZE counter collection into profiles/scan_traffic.json.
+"""Turn a rocprofv3 --pmc FETCH_SIZE counter collection into
+profiles/scan_traffic_<config>.json (bench.py --config <config>).
 
-    python tools/pmc_traffic.py gpurun_out/pmc1/bench_counter_collection.csv
+    python tools/pmc_traffic.py gpurun_out/pmc1/run_counter_collection.csv [config]
 
 FETCH_SIZE is in KiB and, on gfx950, reads exactly half of the bytes of a
 wide coalesced streaming read (MI355X_MICROARCH.md, HBM section), so the
@@ -22,7 +23,8 @@ def kernel_sha():
         return hashlib.sha256(f.read()).hexdigest()
 
 
-def main(path, out=os.path.join(ROOT, "profiles", "scan_traffic.json")):
+def main(path, config="glove"):
+    out = os.path.join(ROOT, "profiles", f"scan_traffic_{config}.json")
     vals = []
     with open(path) as f:
         for row in csv.DictReader(f):
@@ -31,7 +33,7 @@ def main(path, out=os.path.join(ROOT, "profiles", "scan_traffic.json")):
     if not vals:
         raise SystemExit("no FETCH_SIZE rows for the scan kernel")
     avg_kib = sum(vals) / len(vals)
-    res = dict(kernel=KERNEL, launches=len(vals), fetch_size_kib_avg=avg_kib,
+    res = dict(kernel=KERNEL, config=config, launches=len(vals), fetch_size_kib_avg=avg_kib,
                hbm_read_bytes_per_launch=2.0 * avg_kib * 1024.0,
                correction="x2: gfx950 FETCH_SIZE counts half of wide coalesced reads",
                source=os.path.relpath(path, ROOT), smx_kernels_sha256=kernel_sha())

@@ -1,13 +1,13 @@
 #!/bin/bash
 # Kernel trace + stats of the bench per environment setting (GPU box, repo root):
-#   ENVS="SMX_SEED_MFMA=0 SMX_SEED_MFMA=1" TAG=x BENCH_ARGS="--config deep1b" bash tools/trace_env.sh
+#   ENVS="SMX_NARROW=1 SMX_NARROW=2" TAG=x BENCH_ARGS="--config deep1b" bash tools/trace_env.sh
 # Output: gpurun_out/$TAG/<setting>/run_kernel_stats.csv (+ the trace, bench line)
 set -o pipefail
 ROOT=$(pwd)
 O=$ROOT/gpurun_out/${TAG:-trace}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-for E in ${ENVS:-SMX_SEED_MFMA=0}; do
+for E in ${ENVS:-SMX_NARROW=1}; do
   echo "[trace_env] $(date +%T) $E" >&2
   mkdir -p "$O/$E"
   (export ${E//,/ }; export SMX_LIB=${SMX_LIB:+$ROOT/$SMX_LIB}; timeout -k 10 ${LIMIT:-300} rocprofv3 --kernel-trace --stats --output-format csv \
