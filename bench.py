@@ -65,7 +65,7 @@ CONFIGS = {
                  workload="SIFT1M shape: 1,000,000x128 squared L2, tree + AH (non-residual) "
                           "2000 leaves, LUT16 AH 64 blocks x 2 dims, leaves_to_search=100, "
                           "reorder 100, k=10, batch=1000 queries per GPU",
-                 data="synthetic (SIFT1M-shaped seeded non-negative rounded mixture; no "
+                 data="synthetic (SIFT1M-shaped: 30-component low-rank mixture, |x| x 256 rounded to bytes; no "
                       "datasets offline)",
                  metric_name="QPS at recall@10, SIFT1M shape (BASELINE.json configs[2]), batch=1000"),
     # configs[3] / configs[4]: generated on the device (scann_amd/generate.py),
@@ -783,13 +783,16 @@ def _generated_truth(ds, q, r0, r1, dev):
 
 
 def shard_parity(ix, eng, q, points, threads, device):
-    """parity_vs_oracle of a shard line at workload size: rank 0's shard as a
-    standalone index (TreeAHIndex.standalone: the same leaves, codes, ties
-    and float rows) searched on the GPU and by the oracle (ideal mode) on
-    PARITY_QUERIES queries, per (leaves_to_search, pre_reorder_nn) point:
-    ids and distance bits must be equal.  For a disjoint index the shard
-    engine's own list (search_shard + merge of the one list) must give the
-    same neighbors by global id."""
+    """parity_vs_oracle of a shard line at workload size, per (leaves_to_search,
+    pre_reorder_nn) point on PARITY_QUERIES queries:
+    * the benchmarked path itself -- this rank's shard engine (search_shard +
+      the merge of its one list) -- against the oracle (ideal mode) on the
+      shard: the whole index's ties (leaf << shift | leaf_row_base + row),
+      spill factor and SOAR dedupe, the reorder from the members' own rows;
+      global ids and distance bits must be equal;
+    * the shard viewed as a standalone index (TreeAHIndex.standalone: members
+      renumbered, a SOAR shard's copies distinct) through search_batched
+      against the oracle on that view."""
     import torch
     from oracle import binding as oracle
     from scann_amd import _native
@@ -801,30 +804,38 @@ def shard_parity(ix, eng, q, points, threads, device):
     try:
         for lv, pre in points:
             t = time.perf_counter()
-            gi, gd, gc = nv.search_batched(sub, lv, pre, FINAL_NN, True)
-            oi, od, oc = oracle.search(view, sub, lv, pre, FINAL_NN, True, oracle.MODE_IDEAL,
-                                       threads)
+            oi, od, oc = oracle.search(ix, sub, lv, pre, FINAL_NN, True, oracle.MODE_IDEAL, threads)
+            qd = torch.from_numpy(sub).to(eng.device)
+            k = eng.shard_width(lv, pre, FINAL_NN, True)
+            le = torch.empty((sub.shape[0], k, 2), dtype=torch.int64, device=eng.device)
+            eng.search_shard(qd, lv, pre, FINAL_NN, True, le)
+            si, sd, sc = eng.merge(1, le.unsqueeze(0), sub.shape[0], lv, pre, FINAL_NN, True)
+            torch.cuda.synchronize()
+            si = si.cpu().numpy().astype(np.uint32)
+            sd = sd.cpu().numpy()
+            sc = sc.cpu().numpy()
             ent = {"leaves_to_search": lv, "pre_reorder_nn": pre, "queries": int(sub.shape[0]),
-                   "id_mismatch": float((gi != oi).mean()),
-                   "dist_bits_mismatch": float((gd.view(np.uint32) != od.view(np.uint32)).mean()),
-                   "count_mismatch": int((gc != oc).sum()),
-                   "max_rel_dist_err": float(np.max(np.abs(gd - od) /
+                   "id_mismatch": float((si != oi).mean()),
+                   "dist_bits_mismatch": float((sd.view(np.uint32) != od.view(np.uint32)).mean()),
+                   "count_mismatch": int((sc != oc).sum()),
+                   "max_rel_dist_err": float(np.max(np.abs(sd - od) /
                                                     np.maximum(np.abs(od), 1e-30)))}
-            if ix.disjoint:
-                qd = torch.from_numpy(sub).to(eng.device)
-                k = eng.shard_width(lv, pre, FINAL_NN, True)
-                le = torch.empty((sub.shape[0], k, 2), dtype=torch.int64, device=eng.device)
-                eng.search_shard(qd, lv, pre, FINAL_NN, True, le)
-                si, sd, _ = eng.merge(1, le.unsqueeze(0), sub.shape[0], lv, pre, FINAL_NN, True)
-                torch.cuda.synchronize()
-                ent["shard_engine_id_mismatch"] = float(
-                    (si.cpu().numpy().astype(np.uint32) != ix.leaf_members[oi]).mean())
+            vi, vd, vc = oracle.search(view, sub, lv, pre, FINAL_NN, True, oracle.MODE_IDEAL,
+                                       threads)
+            gi, gd, gc = nv.search_batched(sub, lv, pre, FINAL_NN, True)
+            ent["standalone_view"] = {
+                "id_mismatch": float((gi != vi).mean()),
+                "dist_bits_mismatch": float((gd.view(np.uint32) != vd.view(np.uint32)).mean()),
+                "count_mismatch": int((gc != vc).sum())}
             ent["oracle_s"] = round(time.perf_counter() - t, 2)
             log(f"parity L={lv} pre={pre}: {ent}")
             out.append(ent)
     finally:
         nv.close()
-    return {"index": "rank 0's shard as a standalone index (TreeAHIndex.standalone)",
+    return {"path": "this rank's shard engine (search_shard + merge of its list) vs the oracle "
+                    "on the shard (whole-index ties, SOAR dedupe, member-row reorder); "
+                    "standalone_view: the shard renumbered as an index of its own through "
+                    "search_batched vs the oracle on that view",
             "mode": "oracle ideal mode (oracle/scann_oracle.cc) vs the GPU, bit-exact ids and "
                     "distances", "points": out}
 

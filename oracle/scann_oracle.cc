@@ -594,6 +594,7 @@ static float ExactDistance(const float* q, const float* x, int dim, int metric) 
 struct Cand {
   uint32_t tie;  // packed (leaf << shift | local) or global id
   float d;
+  uint64_t slot = 0;   // member index (ideal mode: the shard reorder's row)
 };
 static inline bool CandLess(const Cand& a, const Cand& b) {
   if (a.d != b.d) return a.d < b.d;
@@ -615,6 +616,12 @@ struct IndexView {
   const orc_index* ix;
   int shift;            // global top-N shift; 0 = per-leaf path
   bool disjoint;
+  // a range-split shard (is_shard, smx_index_desc's tail): leaf l's rows are
+  // rows [row_base[l], row_base[l] + n) of the whole index's leaf, so the
+  // packed tie is leaf << shift | (row_base[l] + local); NULL otherwise
+  const uint32_t* row_base = nullptr;
+  // the shard's own float rows per member (reorder source), or NULL
+  const float* member_rows = nullptr;
   std::vector<float> cnorms;
   std::vector<int> leaf_rank_by_norm;  // position in leaf_tokens_by_norm_
 };
@@ -633,6 +640,8 @@ static void BuildView(const orc_index* ix, IndexView* v) {
   v->shift = ix->is_shard ? ix->global_topn_shift : GlobalShift(ix);
   const uint64_t nmem = ix->leaf_offsets[ix->num_leaves];
   v->disjoint = ix->is_shard ? !ix->global_spilled : (nmem == ix->num_datapoints);
+  v->row_base = ix->is_shard ? ix->leaf_row_base : nullptr;
+  v->member_rows = ix->is_shard ? ix->member_rows : nullptr;
   if (v->disjoint && !ix->is_shard) {
     std::vector<uint8_t> seen(ix->num_datapoints, 0);
     for (uint64_t i = 0; i < nmem; ++i) {
@@ -872,9 +881,11 @@ static void PipelineBGeneric(const IndexView& v, const std::vector<int>& leaves,
 
 // One query's pre-reorder candidates (global ids), unsorted.  `generic`:
 // pipeline B's emulate mode takes the per-query path (PipelineBGeneric).
+// slots (ideal mode, may be NULL): global id -> member index of the kept
+// candidates, for a shard's reorder from its own member rows.
 static void QueryPreReorder(const IndexView& v, const float* q, int L,
                             int pre_nn, int mode, bool generic, std::vector<float>* scratch,
-                            NN* out) {
+                            NN* out, std::unordered_map<uint32_t, uint64_t>* slots = nullptr) {
   const orc_index* ix = v.ix;
   const int nl = ix->num_leaves, nb = ix->num_blocks, dim = ix->dim;
   scratch->resize(nl);
@@ -965,25 +976,23 @@ static void QueryPreReorder(const IndexView& v, const float* q, int L,
       const float bias = residual ? biases[li] : 0.0f;
       const uint64_t beg = ix->leaf_offsets[leaf];
       const uint32_t n = uint32_t(ix->leaf_offsets[leaf + 1] - beg);
+      // a shard's rows keep the whole index's row numbers in the tie
+      const uint32_t rb = v.row_base ? v.row_base[leaf] : 0u;
       for (uint32_t i = 0; i < n; ++i) {
         const int32_t a = Accumulate(ix->member_codes + (beg + i) * nb, nb, lut.u8.data());
         const float p = static_cast<float>(a) * inv;
         const float d = residual ? p + bias : p;
-        const uint32_t tie = shift > 0 ? ((uint32_t(leaf) << shift) | i)
+        const uint32_t tie = shift > 0 ? ((uint32_t(leaf) << shift) | (rb + i))
                                        : ix->leaf_members[beg + i];
-        cands.push_back({tie, d});
+        cands.push_back({tie, d, beg + i});
       }
     }
     const size_t keep = std::min<size_t>(size_t(std::max(kk, 0)), cands.size());
     std::partial_sort(cands.begin(), cands.begin() + keep, cands.end(), CandLess);
     out->resize(keep);
     for (size_t i = 0; i < keep; ++i) {
-      uint32_t g = cands[i].tie;
-      if (shift > 0) {
-        const uint32_t leaf = g >> shift;
-        const uint32_t local = g & ((1u << shift) - 1);
-        g = ix->leaf_members[ix->leaf_offsets[leaf] + local];
-      }
+      const uint32_t g = ix->leaf_members[cands[i].slot];
+      if (slots) slots->emplace(g, cands[i].slot);   // (a SOAR id's copies: the same row)
       (*out)[i] = {g, cands[i].d};
     }
   }
@@ -1022,7 +1031,9 @@ static int SearchImpl(const orc_index* ix, const float* queries, int nq,
   if (!ix || nq < 0 || leaves <= 0 || final_nn < 0) return -1;
   IndexView v;
   BuildView(ix, &v);
-  const bool reorder = do_reorder && ix->dataset != nullptr;
+  const bool reorder = do_reorder && (ix->dataset != nullptr || v.member_rows != nullptr);
+  // a shard reorders from its members' own rows (ideal mode only)
+  if (reorder && !ix->dataset && (mode & 3) != ORC_MODE_IDEAL) return -2;
   // scann.cc:406-430: without reordering pre_nn = final_nn.
   const int pnn = reorder ? pre_nn : final_nn;
   const int width = pre_only ? pnn : final_nn;
@@ -1034,14 +1045,18 @@ static int SearchImpl(const orc_index* ix, const float* queries, int nq,
     std::vector<float> scratch;
     const float* q = queries + size_t(qi) * ix->dim;
     NN r;
-    QueryPreReorder(v, q, leaves, pnn, mode, generic, &scratch, &r);
+    std::unordered_map<uint32_t, uint64_t> slots;
+    const bool by_member = reorder && !ix->dataset;
+    QueryPreReorder(v, q, leaves, pnn, mode, generic, &scratch, &r, by_member ? &slots : nullptr);
     if (pre_only) {
       std::sort(r.begin(), r.end(), NNLess);
     } else {
       if (reorder)
-        for (auto& p : r)
-          p.second = ExactDistance(q, ix->dataset + size_t(p.first) * ix->dim,
-                                   ix->dim, ix->metric);
+        for (auto& p : r) {
+          const float* row = by_member ? v.member_rows + size_t(slots.at(p.first)) * ix->dim
+                                       : ix->dataset + size_t(p.first) * ix->dim;
+          p.second = ExactDistance(q, row, ix->dim, ix->metric);
+        }
       RemovePastLimitAndSort(&r, reorder ? size_t(final_nn) : r.size());
       if (!reorder && r.size() > size_t(final_nn)) r.resize(final_nn);
     }

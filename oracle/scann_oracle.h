@@ -56,8 +56,11 @@ typedef struct orc_index {
   int32_t global_topn_shift;
   int32_t global_spilled;
   int32_t reserved2;
-  const uint32_t* leaf_row_base;   /* unused by the oracle */
-  const float* member_rows;        /* unused by the oracle (reorders from dataset) */
+  /* ideal mode: leaf l's rows are rows [leaf_row_base[l], +n) of the whole
+   * index's leaf (the packed tie, tree_ah_hybrid_residual.h:234-247) */
+  const uint32_t* leaf_row_base;
+  /* ideal mode with a NULL dataset: the reorder rows per member */
+  const float* member_rows;
 } orc_index;
 
 /* Partition scores, transposed many-to-many numerics

@@ -3155,7 +3155,8 @@ __global__ void __launch_bounds__(256) partition_scores_a8_kernel(
 // LDS: keys[cap_pow2] u64 | q[dim] f32 | gid/dist scratch.
 // ---------------------------------------------------------------------------
 // The float row of a candidate known by its global id: the shard's own copy
-// (member_rows[row_of[gid]]) or the dataset's row.
+// (member_rows[row_of[gid]]; row_of exists for shards at shift 0 and spilled
+// shards only) or the dataset's row.
 __device__ __forceinline__ const float* RowOfId(const SelectArgs& a, uint32_t gid) {
   if (a.member_rows) {
     const uint32_t slot = a.row_of[gid];
@@ -3219,15 +3220,17 @@ __device__ void FinalSelectQuery(const SelectArgs& a, int qi) {
       e.exact = 0.0f;
       if (i < m) {
         uint64_t key = keys[i];
-        const float* x = a.reorder ? RowOfId(a, gid[i]) : nullptr;
+        const float* x = nullptr;
         if (a.shift > 0) {
           const uint32_t tie = uint32_t(key & 0xFFFFFFFFu);
           const uint32_t leaf = tie >> a.shift;
           const uint32_t local = tie & ((1u << a.shift) - 1u);
+          // the member's own row by its slot (row_of is kept for shift 0 only)
           if (a.member_rows) x = a.member_rows + (a.member_off[leaf] + local) * uint64_t(a.dim);
           if (a.row_base)
             key = (key & 0xFFFFFFFF00000000ull) | ((leaf << a.shift) | (local + a.row_base[leaf]));
         }
+        if (a.reorder && !x) x = RowOfId(a, gid[i]);
         e.key = key;
         e.id = gid[i];
         e.exact = a.reorder ? ExactDistance(q, x, a.dim, a.metric) : dist[i];
@@ -3279,8 +3282,19 @@ __device__ void FinalSelectQuery(const SelectArgs& a, int qi) {
     __syncthreads();
   }
   if (a.reorder && !a.pre_only) {
-    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
-      dist[i] = ExactDistance(q, RowOfId(a, gid[i]), a.dim, a.metric);
+    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+      const float* x;
+      if (a.member_rows && a.shift > 0 && a.disjoint) {
+        // keys[i] still holds candidate i's packed tie (no dedupe ran): its
+        // member slot (a disjoint shard keeps no global-id -> slot table)
+        const uint32_t tie = uint32_t(keys[i] & 0xFFFFFFFFu);
+        x = a.member_rows +
+            (a.member_off[tie >> a.shift] + (tie & ((1u << a.shift) - 1u))) * uint64_t(a.dim);
+      } else {
+        x = RowOfId(a, gid[i]);
+      }
+      dist[i] = ExactDistance(q, x, a.dim, a.metric);
+    }
     __syncthreads();
   }
   // Sort by (distance, global id) and keep the output width.

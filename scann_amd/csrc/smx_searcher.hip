@@ -281,11 +281,15 @@ int UploadIndex(const smx_index_desc* d, smx_index* h) {
       if ((rc = DAlloc(&ix.member_rows, size_t(M) * dim))) return rc;
       SMX_HIP(hipMemcpy(ix.member_rows, d->member_rows, sizeof(float) * size_t(M) * dim,
                         hipMemcpyHostToDevice));
-      // global id -> member slot, for the candidates known by global id (the
-      // non-global-top-N fallback: ties are global ids, shift 0; and the
-      // block select).  A SOAR id held twice keeps either slot: same row.
-      if ((rc = DAlloc(&ix.row_of, size_t(d->num_datapoints)))) return rc;
-      SMX_HIP(hipMemset(ix.row_of, 0xFF, sizeof(uint32_t) * size_t(d->num_datapoints)));
+      // global id -> member slot, for the candidates known by global id only:
+      // ties by global id (shift 0), and a spilled shard's candidates after
+      // the block select's SOAR dedupe.  A disjoint shard with the global
+      // top-N finds every row from its packed tie (no table: 4 GB per rank at
+      // the Deep1B shape).  A SOAR id held twice keeps either slot: same row.
+      if (ix.shift == 0 || !ix.disjoint) {
+        if ((rc = DAlloc(&ix.row_of, size_t(d->num_datapoints)))) return rc;
+        SMX_HIP(hipMemset(ix.row_of, 0xFF, sizeof(uint32_t) * size_t(d->num_datapoints)));
+      }
     }
   }
   SMX_HIP(hipMemcpy(ix.centers, d->centers, sizeof(float) * nl * dim, hipMemcpyHostToDevice));

@@ -1,8 +1,8 @@
 """Seeded synthetic stand-ins for the BASELINE.json datasets (no network).
 
 glove-100-angular is replaced by a unit-normalised Gaussian mixture of the
-same shape; SIFT1M by non-negative rounded mixture
-vectors (config 3).  Queries are fresh draws from the same mixture.
+same shape; SIFT1M by non-negative rounded vectors
+of a low-rank mixture (config 3).  Queries are fresh draws from the same mixture.
 """
 from __future__ import annotations
 
@@ -10,13 +10,16 @@ import numpy as np
 
 GLOVE_N, GLOVE_D = 1_183_514, 100
 SIFT_N, SIFT_D = 1_000_000, 128
-# SIFT1M stand-in: 100 broad components (noise norm 0.8 against unit means,
-# then |x| * 256 rounded to bytes), so that a query's neighbourhood spans
-# several of the 2000 leaves and recall rises with leaves_to_search
-# (partition recall of the true top-10 at L = 10 / 20 / 50: 0.83 / 0.99 /
-# 0.998, against 1.0 already at L = 10 with round 4's 1000 tight
-# components, which made the recall sweep flat)
-SIFT_COMPONENTS, SIFT_SPREAD = 100, 0.8
+# SIFT1M stand-in: 30 components, each a unit mean plus a 16-dimensional
+# random-subspace spread of norm 0.8 and an isotropic spread of norm 0.2, then
+# |x| * 256 rounded to bytes.  The low intrinsic dimension gives neighbours
+# distinct distances (as in SIFT descriptors), so that 4-bit AH + a 100-point
+# reorder reaches recall@10 ~0.998, while a component spans ~70 of the 2000
+# leaves, so recall rises with leaves_to_search (oracle, 200 queries:
+# 0.895 / 0.982 / 0.995 at L = 10 / 20 / 30).  Round 4's 1000 tight isotropic
+# components gave 0.98 already at L = 10 (a flat sweep); isotropic broad
+# ones plateau below 0.95 (AH cannot rank near-equidistant neighbours).
+SIFT_COMPONENTS, SIFT_RANK, SIFT_SPREAD, SIFT_NOISE = 30, 16, 0.8, 0.2
 
 
 def mixture(n: int, d: int, components: int, spread: float, seed: int,
@@ -46,18 +49,38 @@ def glove_like(n: int = GLOVE_N, nq: int = 1000, d: int = GLOVE_D, seed: int = 2
     return db, q
 
 
-def sift_draw(m: int, s: int, seed: int = 3, d: int = SIFT_D,
-              components: int = SIFT_COMPONENTS, spread: float = SIFT_SPREAD) -> np.ndarray:
+def lowrank_mixture(n: int, d: int, components: int, rank: int, spread: float,
+                    noise: float, seed: int, means_seed: int, chunk: int = 1 << 17) -> np.ndarray:
+    """Rows = unit mean_c + spread * U_c z / sqrt(rank) + N(0, noise^2 / d),
+    U_c a [d][rank] N(0, 1/d) basis per component, z ~ N(0, I_rank)."""
+    mrng = np.random.default_rng(means_seed)
+    means = mrng.standard_normal((components, d)).astype(np.float32)
+    means /= np.linalg.norm(means, axis=1, keepdims=True)
+    basis = (mrng.standard_normal((components, d, rank)) / np.sqrt(d)).astype(np.float32)
+    rng = np.random.default_rng(seed + 1)
+    out = np.empty((n, d), np.float32)
+    for s in range(0, n, chunk):
+        m = min(chunk, n - s)
+        z = rng.integers(0, components, m)
+        lat = rng.standard_normal((m, rank), dtype=np.float32) * np.float32(spread / np.sqrt(rank))
+        x = means[z] + np.float32(noise / np.sqrt(d)) * rng.standard_normal((m, d), dtype=np.float32)
+        for c in range(components):
+            sel = np.nonzero(z == c)[0]
+            if sel.size:
+                x[sel] += lat[sel] @ basis[c].T
+        out[s:s + m] = x
+    return out
+
+
+def sift_draw(m: int, s: int, seed: int = 3, d: int = SIFT_D) -> np.ndarray:
     """m SIFT-like rows (non-negative, rounded to bytes) drawn with seed `s`
-    from the mixture whose means come from `seed`."""
-    x = mixture(m, d, components, spread, s, normalize=False, means_seed=seed)
+    from the mixture whose components come from `seed`."""
+    x = lowrank_mixture(m, d, SIFT_COMPONENTS, SIFT_RANK, SIFT_SPREAD, SIFT_NOISE, s, seed)
     return np.clip(np.rint(np.abs(x) * 256.0), 0, 255).astype(np.float32)
 
 
-def sift_like(n: int = SIFT_N, nq: int = 1000, d: int = SIFT_D, seed: int = 3,
-              components: int = SIFT_COMPONENTS, spread: float = SIFT_SPREAD):
-    return (sift_draw(n, seed, seed, d, components, spread),
-            sift_draw(nq, seed + 100, seed, d, components, spread))
+def sift_like(n: int = SIFT_N, nq: int = 1000, d: int = SIFT_D, seed: int = 3):
+    return sift_draw(n, seed, seed, d), sift_draw(nq, seed + 100, seed, d)
 
 
 def brute_force_topk(db: np.ndarray, q: np.ndarray, k: int, metric: int,

@@ -15,9 +15,12 @@ GPU as bench.py builds it (scann_amd/generate.py), then:
   * the same with 512-entry candidate lists and no seed threshold, so that
     lists overflow and are rescanned on the device (the timings report the
     rescan passes);
-  * (disjoint index) the shard engine's own list -- search_shard + merge of
-    that one list, the bench's N = 1 path -- gives the same neighbors by
-    global id.
+  * the shard engine's own list -- search_shard + merge of that one list,
+    the bench's N = 1 path -- == the oracle (ideal mode) on the shard itself:
+    the whole index's ties (leaf << shift | leaf_row_base + row), its spill
+    factor and SOAR dedupe by global id, the reorder from the members' own
+    rows; global ids and distance bits, for the disjoint and the spilled
+    (SOAR) shard alike.
 """
 import numpy as np
 import pytest
@@ -48,7 +51,7 @@ def _check_points(oracle, ix, q, points, min_rows_per_leaf, multi_chunk_leaves):
     assert int((sizes > 20 * 32).sum()) >= multi_chunk_leaves, int((sizes > 640).sum())
     view = ix.standalone()
     nv = _native.NativeIndex(view)
-    eng = NativeShardEngine(ix) if ix.disjoint else None
+    eng = NativeShardEngine(ix)
     try:
         for lv, pre in points:
             oi, od, oc = oracle.search(view, q, lv, pre, 10, True, oracle.MODE_IDEAL, 16)
@@ -66,21 +69,22 @@ def _check_points(oracle, ix, q, points, min_rows_per_leaf, multi_chunk_leaves):
                 np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
                 if cap:
                     assert t["overflow_retries"] > 0, t
-            if eng is not None:
-                qd = torch.from_numpy(q).cuda()
-                k = eng.shard_width(lv, pre, 10, True)
-                le = torch.empty((NQ, k, 2), dtype=torch.int64, device="cuda")
-                eng.search_shard(qd, lv, pre, 10, True, le)
-                si, sd, sc = eng.merge(1, le.unsqueeze(0), NQ, lv, pre, 10, True)
-                torch.cuda.synchronize()
-                np.testing.assert_array_equal(si.cpu().numpy().astype(np.uint32),
-                                              ix.leaf_members[oi])
-                np.testing.assert_array_equal(sd.cpu().numpy().view(np.uint32),
-                                              od.view(np.uint32))
+            si_o, sd_o, sc_o = oracle.search(ix, q, lv, pre, 10, True, oracle.MODE_IDEAL, 16)
+            if ix.disjoint:   # the view's top-k is the shard's, renumbered
+                np.testing.assert_array_equal(si_o, ix.leaf_members[oi])
+            qd = torch.from_numpy(q).cuda()
+            k = eng.shard_width(lv, pre, 10, True)
+            le = torch.empty((NQ, k, 2), dtype=torch.int64, device="cuda")
+            eng.search_shard(qd, lv, pre, 10, True, le)
+            si, sd, sc = eng.merge(1, le.unsqueeze(0), NQ, lv, pre, 10, True)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(sc.cpu().numpy(), sc_o)
+            np.testing.assert_array_equal(si.cpu().numpy().astype(np.uint32), si_o,
+                                          err_msg=f"shard engine L={lv} pre={pre}")
+            np.testing.assert_array_equal(sd.cpu().numpy().view(np.uint32), sd_o.view(np.uint32))
     finally:
         nv.close()
-        if eng is not None:
-            eng.nat.close()
+        eng.nat.close()
 
 
 def test_deep1b_shard_at_workload_density(oracle):
