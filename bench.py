@@ -75,7 +75,8 @@ CONFIGS = {
                      train_sample=250_000,
                      # (pre_reorder_nn <= 128: SOAR shard lists hold 2 x pre <= 256)
                      sweep=[20, 40, 60, 100, 150, 200, [100, 128], [200, 128], [400, 128]],
-                     parity_points=[(100, 100), (1000, 256)],
+                     # (a SOAR shard's list holds k' = 2 x pre <= 256 entries)
+                     parity_points=[(100, 100), (200, 128)],
                      workload="configs[3]: synthetic 100M x 96 dot product + SOAR (lambda 1.5, "
                               "overretrieve 2), tree-AH 10000 leaves, LUT16 AH 48 blocks x 2 "
                               "dims, leaves_to_search=100, reorder 100, k=10, batch=1000, "
