@@ -131,6 +131,39 @@ struct Workspace {
   }
 };
 
+// One stream's share of a handle: its per-call buffers and what orders
+// them.  Calls on different streams use different slots, so batches issued on
+// two streams run concurrently on the device (one batch's latency-bound
+// front end and select beside the other's scan; see DESIGN.md "Batches in
+// flight"); calls on one stream are ordered by that stream.  A slot reused
+// from another stream (more streams than kMaxStreamSlots) first waits for
+// its previous stream's work.
+struct StreamSlot {
+  hipStream_t key = nullptr;          // the stream this slot serves
+  Workspace ws;
+  hipGraphExec_t graph_exec = nullptr;
+  uint64_t graph_key[16] = {};
+  hipEvent_t done_ev = nullptr;       // cross-stream ordering (recorded at a stream switch)
+  hipStream_t last_stream = nullptr;
+  hipStream_t side = nullptr;         // the fork/join branch (SMX_SERIAL_WORKLIST=0)
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+};
+constexpr int kMaxStreamSlots = 4;
+
+void DestroySlot(StreamSlot* sl) {
+  if (sl->last_stream) (void)hipStreamSynchronize(sl->last_stream);
+  if (sl->graph_exec) (void)hipGraphExecDestroy(sl->graph_exec);
+  sl->ws.Release();
+  if (sl->done_ev) (void)hipEventDestroy(sl->done_ev);
+  if (sl->fork_ev) (void)hipEventDestroy(sl->fork_ev);
+  if (sl->join_ev) (void)hipEventDestroy(sl->join_ev);
+  if (sl->side) {
+    (void)hipStreamSynchronize(sl->side);
+    (void)hipStreamDestroy(sl->side);
+  }
+  delete sl;
+}
+
 }  // namespace
 
 struct smx_index {
@@ -138,7 +171,7 @@ struct smx_index {
   int device = 0;
   hipStream_t stream = nullptr;
   std::mutex mu;
-  Workspace ws;
+  std::vector<StreamSlot*> slots;   // one per stream the handle has searched on
   uint32_t cap_per_query = 0;      // candidate list capacity; 0 = sized per call (AutoCap)
   int seed_leaves = 4;
   int scan_variant = 0;            // see smx::LaunchScan
@@ -157,16 +190,10 @@ struct smx_index {
   int cus = 0;                     // compute units of the device
   bool profiling = false;
   bool use_graph = false;          // SMX_GRAPH=1: replay the pipeline as a hipGraph
-  hipGraphExec_t graph_exec = nullptr;
-  uint64_t graph_key[16] = {};
   uint64_t ws_generation = 0;
   uint32_t* host_stats = nullptr;  // pinned copy of the stats words
   smx_timings timings{};
   hipEvent_t ev[16] = {};
-  hipEvent_t done_ev = nullptr;      // cross-stream ordering (recorded at a stream switch)
-  hipStream_t side = nullptr;        // the fork/join branch of every call
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-  hipStream_t last_stream = nullptr;
   // scan variant 8 (diagnostics): per-item stamps, dumped to $SMX_STAMPS
   unsigned long long* stamps = nullptr;
   uint32_t* stamp_count = nullptr;
@@ -394,8 +421,38 @@ uint32_t MaxItems(const smx::DeviceIndex& ix, size_t pairs) {
   return uint32_t((pairs / smx::kNarrowSlots + ix.nl + 1) * chunks);
 }
 
-int EnsureWorkspace(smx_index* h, int nq, int L, int kk, int width) {
-  Workspace& w = h->ws;
+// The slot of stream s: its own, a new one (up to kMaxStreamSlots), or else
+// the least recently created one, which then waits for its last stream.
+int SlotFor(smx_index* h, hipStream_t s, StreamSlot** out) {
+  for (StreamSlot* sl : h->slots)
+    if (sl->key == s) {
+      *out = sl;
+      return SMX_OK;
+    }
+  StreamSlot* sl = nullptr;
+  if (int(h->slots.size()) < kMaxStreamSlots) {
+    sl = new StreamSlot;
+    if (hipEventCreateWithFlags(&sl->done_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&sl->fork_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&sl->join_ev, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&sl->side, hipStreamNonBlocking) != hipSuccess) {
+      DestroySlot(sl);
+      return Fail(SMX_DEVICE_ERROR, "stream slot: hipEventCreate / hipStreamCreate failed");
+    }
+    sl->last_stream = s;
+    h->slots.push_back(sl);
+  } else {
+    sl = h->slots.front();   // rotated to the back: reused in creation order
+    h->slots.erase(h->slots.begin());
+    h->slots.push_back(sl);
+  }
+  sl->key = s;
+  *out = sl;
+  return SMX_OK;
+}
+
+int EnsureWorkspace(smx_index* h, StreamSlot* sl, int nq, int L, int kk, int width) {
+  Workspace& w = sl->ws;
   const smx::DeviceIndex& ix = h->ix;
   // cap >= 2 k': when a list overflows, its k'-th stored key is strictly
   // below the threshold (keys are unique and all <= it), so every
@@ -479,9 +536,11 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   const int pnn = reorder ? pre_nn : final_nn;
   const int kk = std::max(1, SpillK(ix, pnn));
   const int width = shard_out ? 1 : pre_only ? pnn : final_nn;
-  int rc = EnsureWorkspace(h, nq, L, kk, width);
+  StreamSlot* sl = nullptr;
+  int rc = SlotFor(h, s, &sl);
   if (rc) return rc;
-  Workspace& w = h->ws;
+  if ((rc = EnsureWorkspace(h, sl, nq, L, kk, width))) return rc;
+  Workspace& w = sl->ws;
   const int nl = ix.nl;
   const CounterLayout lay(nl);
   uint32_t* cnt = w.counters;
@@ -674,16 +733,16 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
       // The seed (the longer branch) is captured first, so that a replayed
       // graph keeps it on the launch queue with the kernels before and after
       // it; the shorter work-list branch pays the cross-queue edges.
-      SMX_HIP(hipEventRecord(h->fork_ev, s));
+      SMX_HIP(hipEventRecord(sl->fork_ev, s));
       SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
       Mark(h, 4, s);
-      SMX_HIP(hipStreamWaitEvent(h->side, h->fork_ev, 0));
+      SMX_HIP(hipStreamWaitEvent(sl->side, sl->fork_ev, 0));
       SMX_HIP(smx::LaunchWorklist(ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes,
                                   w.wave_start, h->grid, stats + 3, code_bytes, h->chunk_tiles,
-                                  narrow, w.wl_part, bd, h->side));
-      Mark(h, 3, h->side);
-      SMX_HIP(hipEventRecord(h->join_ev, h->side));
-      SMX_HIP(hipStreamWaitEvent(s, h->join_ev, 0));   // join
+                                  narrow, w.wl_part, bd, sl->side));
+      Mark(h, 3, sl->side);
+      SMX_HIP(hipEventRecord(sl->join_ev, sl->side));
+      SMX_HIP(hipStreamWaitEvent(s, sl->join_ev, 0));   // join
     }
     // every pair's lane record with its sum limit (needs the work list and
     // the seed thresholds)
@@ -717,10 +776,10 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   // The event is recorded on the last stream only at such a switch (it then
   // covers all of that stream's calls so far): a record per call put a
   // barrier packet between consecutive graph replays (~4 us per call).
-  if (h->last_stream != s) {
-    SMX_HIP(hipEventRecord(h->done_ev, h->last_stream));
-    SMX_HIP(hipStreamWaitEvent(s, h->done_ev, 0));
-    h->last_stream = s;
+  if (sl->last_stream != s) {
+    SMX_HIP(hipEventRecord(sl->done_ev, sl->last_stream));
+    SMX_HIP(hipStreamWaitEvent(s, sl->done_ev, 0));
+    sl->last_stream = s;
   }
   bool ran = false;
   // (profiled calls run eagerly: HIP events recorded inside a captured graph
@@ -734,24 +793,24 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
         uint64_t(reinterpret_cast<uintptr_t>(out_count)), uint64_t(reinterpret_cast<uintptr_t>(shard_out)),
         uint64_t(reinterpret_cast<uintptr_t>(s)), w.gen, uint64_t(w.cap), uint64_t(seed),
         uint64_t(h->chunk_tiles), uint64_t(variant)};
-    if (!h->graph_exec || std::memcmp(key, h->graph_key, sizeof(key)) != 0) {
-      if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
-      h->graph_exec = nullptr;
+    if (!sl->graph_exec || std::memcmp(key, sl->graph_key, sizeof(key)) != 0) {
+      if (sl->graph_exec) (void)hipGraphExecDestroy(sl->graph_exec);
+      sl->graph_exec = nullptr;
       if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess) {
         const int prc = first_pass();
         hipGraph_t g = nullptr;
         const hipError_t e = hipStreamEndCapture(s, &g);
         if (prc == SMX_OK && e == hipSuccess && g &&
-            hipGraphInstantiate(&h->graph_exec, g, nullptr, nullptr, 0) == hipSuccess)
-          std::memcpy(h->graph_key, key, sizeof(key));
+            hipGraphInstantiate(&sl->graph_exec, g, nullptr, nullptr, 0) == hipSuccess)
+          std::memcpy(sl->graph_key, key, sizeof(key));
         else
-          h->graph_exec = nullptr;   // capture unsupported here: run eagerly
+          sl->graph_exec = nullptr;   // capture unsupported here: run eagerly
         if (g) (void)hipGraphDestroy(g);
         (void)hipGetLastError();
       }
     }
-    if (h->graph_exec) {
-      SMX_HIP(hipGraphLaunch(h->graph_exec, s));
+    if (sl->graph_exec) {
+      SMX_HIP(hipGraphLaunch(sl->graph_exec, s));
       ran = true;
     }
   }
@@ -901,15 +960,6 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
     return Fail(SMX_DEVICE_ERROR, "hipStreamCreate failed");
   }
   for (auto& e : h->ev) (void)hipEventCreate(&e);
-  if (hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->done_ev, hipEventDisableTiming) != hipSuccess) {
-    smx_index_destroy(h);
-    return Fail(SMX_DEVICE_ERROR, "hipEventCreate failed");
-  }
-  SMX_HIP(hipEventRecord(h->done_ev, h->stream));
-  h->last_stream = h->stream;
   hipDeviceProp_t prop;
   SMX_HIP(hipGetDeviceProperties(&prop, device));
   {
@@ -947,21 +997,14 @@ int smx_index_destroy(smx_index* h) {
   if (!h) return SMX_OK;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
+  for (StreamSlot* sl : h->slots) DestroySlot(sl);
+  h->slots.clear();
   if (h->host_stats) (void)hipHostFree(h->host_stats);
-  h->ws.Release();
   DFree(h->stamps);
   DFree(h->stamp_count);
   FreeIndex(h->ix);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
-  if (h->done_ev) (void)hipEventDestroy(h->done_ev);
-  if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
-  if (h->join_ev) (void)hipEventDestroy(h->join_ev);
-  if (h->side) {
-    (void)hipStreamSynchronize(h->side);
-    (void)hipStreamDestroy(h->side);
-  }
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return SMX_OK;
@@ -1008,10 +1051,12 @@ int SearchHost(smx_index* h, const float* queries, int32_t nq, int32_t dim,
   hipStream_t s = h->stream;
   const int width = p->final_nn;
   const int pnn = p->reorder ? p->pre_reorder_nn : p->final_nn;
-  rc = EnsureWorkspace(h, nq, std::min(p->leaves_to_search, h->ix.nl),
+  StreamSlot* sl = nullptr;
+  if ((rc = SlotFor(h, s, &sl))) return rc;
+  rc = EnsureWorkspace(h, sl, nq, std::min(p->leaves_to_search, h->ix.nl),
                        std::max(1, SpillK(h->ix, pnn)), width);
   if (rc) return rc;
-  Workspace& w = h->ws;
+  Workspace& w = sl->ws;
   SMX_HIP(hipMemcpyAsync(w.queries, queries, sizeof(float) * size_t(nq) * dim,
                          hipMemcpyHostToDevice, s));
   rc = RunSearch(h, w.queries, nq, p->leaves_to_search, p->pre_reorder_nn, p->final_nn,
@@ -1233,10 +1278,12 @@ int smx_search_pre_reorder(smx_index* h, const float* queries, int32_t nq, int32
   std::lock_guard<std::mutex> lock(h->mu);
   SMX_HIP(hipSetDevice(h->device));
   hipStream_t s = h->stream;
-  rc = EnsureWorkspace(h, nq, std::min(leaves, h->ix.nl), std::max(1, SpillK(h->ix, pre_nn)),
+  StreamSlot* sl = nullptr;
+  if ((rc = SlotFor(h, s, &sl))) return rc;
+  rc = EnsureWorkspace(h, sl, nq, std::min(leaves, h->ix.nl), std::max(1, SpillK(h->ix, pre_nn)),
                        pre_nn);
   if (rc) return rc;
-  Workspace& w = h->ws;
+  Workspace& w = sl->ws;
   SMX_HIP(hipMemcpyAsync(w.queries, queries, sizeof(float) * size_t(nq) * h->ix.dim,
                          hipMemcpyHostToDevice, s));
   rc = RunSearch(h, w.queries, nq, leaves, pre_nn, pre_nn, true, true, w.out_idx, w.out_dist,
