@@ -404,7 +404,7 @@ def main():
     ap.add_argument("--sweep-steps", type=int, default=20)
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the oracle check of the generated-shard lines")
-    ap.add_argument("--in-flight", type=int, default=2,
+    ap.add_argument("--in-flight", type=int, default=3,
                     help="query batches in flight (streams, one library workspace each)")
     args = ap.parse_args()
     global CFG, LEAVES, LEAVES_TO_SEARCH

@@ -114,7 +114,8 @@ struct Bounds {
   uint32_t grid = 0;        // scan workgroups (wave_start entries)
   uint32_t nl = 0;          // leaves
   uint32_t datapoints = 0;  // dataset rows
-  uint32_t recs = 0;        // slot records (lanes / leaf slots)
+  uint32_t recs = 0;        // leaf slots (leaf_pair entries: nl x the call's slot stride)
+  uint32_t pairs = 0;       // (query, leaf) pairs (pair_rec entries)
   uint64_t members = 0;     // leaf members (members[], member_rows)
   uint64_t tiles = 0;       // code tiles
 };
@@ -128,18 +129,21 @@ struct WorkItem {
   uint32_t j0, jend;     // tile range
   uint64_t tile_off;     // the leaf's first code tile
   uint64_t member_off;   // the leaf's first member
+  uint32_t slot0;        // the query tile's first leaf slot (leaf_pair index)
+  uint32_t nslots;       // its filled slots (the rest of the tile is empty)
 };
 
-// Per (work item, query slot c < 32): the (query, leaf) pair -- the query
-// (kNoQuery for an empty slot), the partition distance (residual bias) and
-// the query's 1/multiplier; one dwordx4 per lane.  Written by the pair
-// scatter (beside the seed pass, which owns the thresholds); the scan derives
-// the slot's sum limit from the query's threshold key at a segment's start.
+// Per (query, leaf) pair p = query * L + i: the query (kNoQuery for an empty
+// slot), the partition distance (residual bias), the query's 1/multiplier
+// and the pair's sum limit -- the largest LUT16 sum whose distance can pass
+// the query's seed threshold.  One dwordx4, written by the query's seed block
+// once its threshold is known; the scan reads a query tile's slots through
+// leaf_pair (leaf slot -> pair, written by the top-L kernel with the rank).
 struct ItemLane {
   uint32_t qid;
   float bias;
   float inv;
-  int32_t amax;   // the slot's sum limit (pair scatter, after the seed)
+  int32_t amax;   // the pair's sum limit
 };
 constexpr uint32_t kNoQuery = 0xFFFFFFFFu;     // ItemLane::qid of an empty slot
 
@@ -151,7 +155,8 @@ struct ScanArgs {
   const int8_t* lut;          // [nq][2K][16]
   const float* inv;           // [nq]
   const WorkItem* work;       // [work items]
-  const ItemLane* lanes;      // [work items][32]
+  const uint32_t* leaf_pair;  // [nl][slot stride] leaf slot -> pair
+  const ItemLane* pair_rec;   // [nq][L] per-pair records
   uint32_t chunk_tiles;
   const uint4* wave_start;    // [grid] {first item, first tile, tiles, first position}
   uint32_t num_items;
@@ -171,14 +176,8 @@ struct ScanArgs {
 struct SeedArgs {
   const int32_t* topl_leaf;   // [nq][L]
   const float* topl_dist;     // [nq][L]
-  uint32_t narrow;             // the work list's tile mode (kNarrowOnly: 16-slot query tiles)
   int nl;
-  // the inversion (pair scatter): every (query, leaf) pair's slot in its
-  // leaf's work items
-  const uint32_t* rank;       // [nq][L] position inside the leaf's list
-  const uint32_t* leaf_item0; // [nl] the leaf's first work item
-  ItemLane* lanes;            // [work items][32]
-  uint32_t chunk_tiles;
+  ItemLane* pair_rec;         // [nq][L] every pair's record, with its sum limit
   const int8_t* lut;          // [nq][2K][16]
   const float* inv;
   const uint8_t* tiles;
@@ -212,7 +211,7 @@ struct WorklistArgs {
   uint32_t* totals;            // [3] pairs, items, units; [kTotalsTiles16] 16-slot tiles
   unsigned long long* code_bytes;
   WorkItem* work;
-  ItemLane* lanes;
+  uint32_t slot_stride;        // leaf slots per leaf in leaf_pair (the call's nq)
   uint4* wave_start;           // [grid]
   Bounds bd;                  // debug-build index checks
 };
@@ -312,7 +311,8 @@ struct StateInit {
 struct FrontArgs {
   StateInit init;
   uint32_t* leaf_count = nullptr;   // [nl] strided (kCounterStride), zeroed by init
-  uint32_t* rank = nullptr;         // [nq][L]
+  uint32_t* leaf_pair = nullptr;    // [nl][slot_stride]: each pair at its leaf's slot (its rank)
+  uint32_t slot_stride = 0;
   int8_t* lut = nullptr;            // [nq][2K][16]
   float* mult = nullptr;            // [nq]
   float* inv = nullptr;             // [nq]
@@ -325,13 +325,13 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
 hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq,
                           int8_t* lut, float* mult, float* inv, uint8_t* lut_u8,
                           hipStream_t s);
-// Leaf lists -> the scan's work items (8 XCD groups of equal MFMA work),
-// each leaf's first item, the empty query slots' lanes and every scan
-// wave's static share of its group's tiles (three launches).
+// Leaf lists -> the scan's work items (8 XCD groups of equal MFMA work,
+// each item with its query tile's leaf slots), each leaf's first item and
+// every scan wave's static share of its group's tiles (three launches).
 hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count,
                           WorkItem* work /*[max items]*/, uint32_t* leaf_item0 /*[nl]*/,
                           uint32_t* pos_unit0 /*[nl+1]*/, uint32_t* gunits /*[9]*/,
-                          ItemLane* lanes /*[max items][32]*/, uint4* wave_start /*[grid]*/,
+                          uint32_t slot_stride, uint4* wave_start /*[grid]*/,
                           int grid, uint32_t* totals /*[3]*/,
                           unsigned long long* code_bytes /*[1]*/, uint32_t chunk_tiles,
                           uint32_t narrow,
@@ -347,17 +347,14 @@ hipError_t ScanBlocksPerCU(const DeviceIndex& ix, int* blocks);
 // The per-query thresholds (tau_key) from the seed leaves.
 WorklistArgs MakeWorklistArgs(const DeviceIndex& ix, const uint32_t* leaf_count, WorkItem* work,
                               uint32_t* leaf_item0, uint32_t* pos_unit0, uint32_t* gunits,
-                              ItemLane* lanes, uint4* wave_start, int grid, uint32_t* totals,
+                              uint32_t slot_stride, uint4* wave_start, int grid, uint32_t* totals,
                               unsigned long long* code_bytes, uint32_t chunk_tiles,
                               uint32_t narrow, const Bounds& bd);
-// The seed thresholds (one block per query); with `wl`, one more block
-// builds the whole work list (ix.nl <= kFusedWorklistLeaves).
+// The seed thresholds and every pair's record (one block per query); with
+// `wl`, more blocks build the whole work list (ix.nl <= kFusedWorklistLeaves).
 hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s,
                       const WorklistArgs* wl = nullptr);
 hipError_t LaunchKthKeys(const uint32_t* vals, int sets, int kk, uint64_t* out, hipStream_t s);
-// Every (query, leaf) pair's lane record into its leaf's work items (after
-// LaunchWorklist and the seed thresholds: each record carries its sum limit).
-hipError_t LaunchPairScatter(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s);
 // The rank kernel (one block per query, <= kSelMax keys in LDS) for k' <=
 // kSelMax, the block kernel otherwise; both rescan overflowed lists first.
 hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s);

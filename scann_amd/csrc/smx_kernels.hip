@@ -600,7 +600,8 @@ __global__ void __launch_bounds__(256) lut_build_kernel(LutParams p) { BuildLut(
 // selected pairs' ranks in their leaves' lists, then the query's LUT.
 struct TopLTail {
   uint32_t* leaf_count;   // or NULL
-  uint32_t* rank;
+  uint32_t* leaf_pair;    // [nl][slot_stride]: pair p at slot rank of its leaf
+  uint32_t slot_stride;
   LutParams lut;          // lut.lut NULL: no LUT
   int lut_split;   // topl_block_kernel: the LUTs by their own blocks [nq, 2 nq)
 };
@@ -627,7 +628,9 @@ __device__ void TopLFinish(int qi, int L, uint32_t m, const uint64_t* sel, int32
     for (int u = 0; u < U; ++u) {
       const int i = i0 + u * int(blockDim.x);
       if (i >= L) break;
-      if (tail.leaf_count && uint32_t(i) < m) tail.rank[size_t(qi) * L + i] = rk[u];
+      if (tail.leaf_count && uint32_t(i) < m)
+        tail.leaf_pair[size_t(sel[i] & 0xFFFFFFFFu) * tail.slot_stride + rk[u]] =
+            uint32_t(qi) * uint32_t(L) + uint32_t(i);
     }
   }
   if (tail.lut.lut) {
@@ -810,7 +813,10 @@ __device__ __forceinline__ void TopLBlock(const float* __restrict__ scores, int 
     const int32_t leaf = has ? int32_t(srt[i] & 0xFFFFFFFFu) : -1;
     out_leaf[size_t(qi) * L + i] = leaf;
     out_dist[size_t(qi) * L + i] = has ? FromOrdered(uint32_t(srt[i] >> 32)) : __int_as_float(0x7fc00000);
-    if (tail.leaf_count && has) tail.rank[size_t(qi) * L + i] = atomicAdd(&tail.leaf_count[size_t(leaf) * kCounterStride], 1u);
+    if (tail.leaf_count && has) {
+      const uint32_t rk = atomicAdd(&tail.leaf_count[size_t(leaf) * kCounterStride], 1u);
+      tail.leaf_pair[size_t(leaf) * tail.slot_stride + rk] = uint32_t(qi) * uint32_t(L) + uint32_t(i);
+    }
   }
   SMX_PHASE(0, qi, 4);
   if (tail.lut.lut && !tail.lut_split) BuildLut(qi, tail.lut);
@@ -1131,11 +1137,13 @@ __device__ __forceinline__ uint2 ChunkTiles(uint32_t n, uint32_t chunk_tiles, ui
 // Invert (query -> leaves) into (leaf -> queries): InvertCentersToSearch
 // (tree_ah_hybrid_residual.cc:610-622).  The top-L kernel gives every
 // (query, leaf) pair its rank inside the leaf's list (an atomic on the leaf's
-// count); worklist_kernel turns the counts into list offsets and the scan's
-// work items; the seed kernel scatters each query's pairs to
-// pair_off[leaf] + rank.  The order of the queries inside a leaf's list is
-// therefore not the query order; nothing depends on it (every result is an
-// exact top-k under a total order).
+// count) and stores the pair at that slot of the leaf (leaf_pair[leaf *
+// stride + rank], stride = the call's query count); the work list turns the
+// counts into the scan's work items, each with its query tile's slots; the
+// seed kernel writes each pair's record once its query's threshold is
+// known.  The order of the queries inside a leaf's list is therefore not the
+// query order; nothing depends on it (every result is an exact top-k under a
+// total order).
 //
 // Work items = (leaf, query tile, chunk of <= chunk_tiles tiles), listed
 // largest leaf first, cut into 8 XCD groups of consecutive leaves with equal
@@ -1375,30 +1383,21 @@ __device__ void ItemsCore(const WorklistArgs& w, int p, int lane, const uint32_t
   const uint64_t toff = w.tile_off[leaf], moff = w.member_off[leaf];
   for (uint32_t u = lane; u < qt * chunks; u += 64) {
     const uint2 cr = ChunkTiles(n, chunk_tiles, u % chunks);
+    const uint32_t q = u / chunks;
+    // the query tile's ranks: 32-slot tiles first, then the 16-slot ones
+    const uint32_t r0 = q < qts.x ? q * uint32_t(kQueriesPerTile)
+                                  : qts.x * uint32_t(kQueriesPerTile) + (q - qts.x) * uint32_t(kNarrowSlots);
+    const uint32_t width = q < qts.x ? uint32_t(kQueriesPerTile) : uint32_t(kNarrowSlots);
     WorkItem it;
-    it.leaf = leaf | (u / chunks >= qts.x ? kItemNarrow : 0u);
+    it.leaf = leaf | (q >= qts.x ? kItemNarrow : 0u);
     it.n = n;
     it.j0 = cr.x;
     it.jend = cr.y;
     it.tile_off = toff;
     it.member_off = moff;
+    it.slot0 = leaf * w.slot_stride + r0;
+    it.nslots = min(width, c - r0);
     SMX_GUARD(item0 + u, w.bd.items, "work item") w.work[item0 + u] = it;
-  }
-  if (qt) {
-    const uint32_t slots = qts.y ? uint32_t(kNarrowSlots) : uint32_t(kQueriesPerTile);
-    // empty slots [first, slots) of the last query tile
-    const uint32_t first = qts.y ? c - qts.x * kQueriesPerTile - (qts.y - 1u) * kNarrowSlots
-                                 : c - (qt - 1) * kQueriesPerTile;
-    const uint32_t ne = slots - first;
-    for (uint32_t e = lane; e < ne * chunks; e += 64) {
-      ItemLane v;
-      v.qid = kNoQuery;
-      v.bias = 0.0f;
-      v.inv = 0.0f;
-      v.amax = kNoSum;   // never passes
-      SMX_GUARD(item0 + (qt - 1) * chunks + e / ne, w.bd.items, "empty-slot lane")
-      w.lanes[size_t(item0 + (qt - 1) * chunks + e / ne) * kQueriesPerTile + first + e % ne] = v;
-    }
   }
   WaveStarts(w, p, gunits, item0, ua, ub, n, c, uint32_t(lane), 64u);
 }
@@ -1889,11 +1888,18 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
   return T;
 }
 
-// Per query: its threshold key (SeedTau); blocks from nq on build the work
-// list (WorklistFusedBlock).  (Work-list blocks first, with the pair scatter
-// in the seed blocks behind a release flag from block 0, measured slower:
-// block 0 published leaf_item0 only 48.7 us after its start beside the seed
-// blocks -- tools/phase_stamps.py)
+// Per query: its threshold key (SeedTau), then every one of its (query,
+// leaf) pairs' records -- the query, the pair's bias, the query's
+// 1/multiplier and the pair's sum limit: the largest LUT16 sum whose distance
+// can pass the threshold (d is monotone in the sum), so the scan's setup needs
+// neither the threshold nor a search.  The scan finds a pair through its
+// leaf's slot (leaf_pair, written by the top-L kernel with the rank): the
+// inversion of InvertCentersToSearch (tree_ah_hybrid_residual.cc:610-622)
+// without a scatter launch.  Blocks from nq on build the work list
+// (WorklistFusedBlock).  (Work-list blocks first, with the old per-item
+// record scatter in the seed blocks behind a release flag from block 0,
+// measured slower: block 0 published its prefixes only 48.7 us after its
+// start beside the seed blocks -- tools/phase_stamps.py)
 template <int K>
 __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a, WorklistArgs w, int nq) {
   const int qi = blockIdx.x;
@@ -1901,56 +1907,21 @@ __global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a, WorklistArgs 
     WorklistFusedBlock(w, qi - nq);
     return;
   }
-  const uint64_t T = SeedTau<K>(a, qi);
-  if (threadIdx.x == 0) a.tau_key[qi] = T;
-}
-
-// Every (query, leaf) pair into the scan's work-item lanes -- slot rank % 32
-// of query tile rank / 32, in every chunk of the leaf -- with the pair's bias
-// and the query's 1/multiplier: the scatter half of InvertCentersToSearch
-// (tree_ah_hybrid_residual.cc:610-622), with the slot's sum limit from the
-// query's seed threshold.  One thread per pair; runs after the seed pass and
-// the work list.
-__device__ __forceinline__ void PairScatterTau(const SeedArgs& a, size_t p,
-                                               const uint32_t* __restrict__ leaf_item0,
-                                               uint64_t tau);
-__device__ __forceinline__ void PairScatter(const SeedArgs& a, size_t p, int nq,
-                                            const uint32_t* __restrict__ leaf_item0) {
-  if (p >= size_t(nq) * a.L) return;
-  PairScatterTau(a, p, leaf_item0, a.tau_key[p / a.L]);
-}
-// pair p's records with its query's threshold key tau
-__device__ __forceinline__ void PairScatterTau(const SeedArgs& a, size_t p,
-                                               const uint32_t* __restrict__ leaf_item0,
-                                               uint64_t tau) {
-  const int32_t leaf = a.topl_leaf[p];
-  if (leaf < 0) return;
-  const uint32_t qi = uint32_t(p / a.L);
-  const uint32_t r = a.rank[p];
-  const uint32_t n = a.leaf_size[leaf];
-  const uint32_t chunks = LeafChunks(n, a.chunk_tiles);
-  ItemLane v;
-  v.qid = qi;
-  v.bias = a.residual ? a.topl_dist[p] : 0.0f;
-  v.inv = a.inv[qi];
-  // the slot's sum limit: the largest LUT16 sum whose distance can pass the
-  // query's threshold (d is monotone in the sum), so the scan's setup needs
-  // neither the threshold nor a search
-  v.amax = tau == kNoThreshold ? 128 * a.nb
-                               : SumLimit(FromOrdered(uint32_t(tau >> 32)), v.inv, v.bias,
-                                          -128 * a.nb, 128 * a.nb);
-  SMX_CHECK(leaf, a.bd.nl, "pair leaf");
-  // query tile r / ts, slot r % ts (16-slot tiles only: ts = 16)
-  const uint32_t ts = a.narrow == kNarrowOnly ? uint32_t(kNarrowSlots) : uint32_t(kQueriesPerTile);
-  const uint32_t w0 = leaf_item0[leaf] + (r / ts) * chunks;
-  for (uint32_t ch = 0; ch < chunks; ++ch) {
-    SMX_GUARD(w0 + ch, a.bd.items, "pair lane")
-    a.lanes[size_t(w0 + ch) * kQueriesPerTile + (r % ts)] = v;
+  const uint64_t tau = SeedTau<K>(a, qi);
+  if (threadIdx.x == 0) a.tau_key[qi] = tau;
+  const float inv = a.inv[qi];
+  for (int i = threadIdx.x; i < a.L; i += 256) {
+    const size_t p = size_t(qi) * a.L + size_t(i);
+    if (a.topl_leaf[p] < 0) continue;
+    ItemLane v;
+    v.qid = uint32_t(qi);
+    v.bias = a.residual ? a.topl_dist[p] : 0.0f;
+    v.inv = inv;
+    v.amax = tau == kNoThreshold ? 128 * a.nb
+                                 : SumLimit(FromOrdered(uint32_t(tau >> 32)), inv, v.bias,
+                                            -128 * a.nb, 128 * a.nb);
+    SMX_GUARD(p, a.bd.pairs, "pair record") a.pair_rec[p] = v;
   }
-}
-
-__global__ void __launch_bounds__(256) pair_scatter_kernel(SeedArgs a, int nq) {
-  PairScatter(a, size_t(blockIdx.x) * blockDim.x + threadIdx.x, nq, a.leaf_item0);
 }
 
 // One tile: S[dp][q] for 32 datapoints x 32 queries with the item's B
@@ -2231,8 +2202,8 @@ struct SegDesc {
   uint64_t member_off;
   uint32_t n;
   uint32_t leaf;
-  uint32_t slot0;    // the item's first slot record (a.lanes)
-  uint32_t nslots;   // records [slot0, slot0 + nslots); the other slots are empty
+  uint32_t slot0;    // the item's first leaf slot (a.leaf_pair)
+  uint32_t nslots;   // slots [slot0, slot0 + nslots); the other slots are empty
 };
 
 // Wave 0 of a scan workgroup: the next segments of the share (item, first
@@ -2272,8 +2243,8 @@ __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32
       dsc.member_off = it.member_off;
       dsc.n = it.n;
       dsc.leaf = it.leaf;   // (with its kItemNarrow flag)
-      dsc.slot0 = idx * uint32_t(kQueriesPerTile);
-      dsc.nslots = kQueriesPerTile;
+      dsc.slot0 = it.slot0;
+      dsc.nslots = it.nslots;
       s_desc[pos] = dsc;
     }
     const uint32_t nused = uint32_t(__popcll(__ballot(used)));
@@ -2472,8 +2443,10 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         }
         ItemLane r;
         if (cs < ns) {
-          SMX_CHECK(s0 + cs, a.bd.recs, "slot record");
-          r = a.lanes[size_t(s0) + cs];
+          SMX_CHECK(s0 + cs, a.bd.recs, "leaf slot");
+          const uint32_t p = a.leaf_pair[s0 + cs];
+          SMX_CHECK(p, a.bd.pairs, "slot pair");
+          r = a.pair_rec[p];
         } else {
           r.qid = kNoQuery;
           r.bias = 0.0f;
@@ -3880,7 +3853,8 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
   TopLTail tail{};
   static const int dbg = [] { const char* e = std::getenv("SMX_DBG_FRONT"); return e ? std::atoi(e) : 0; }();
   tail.leaf_count = (dbg & 1) ? nullptr : f.leaf_count;
-  tail.rank = f.rank;
+  tail.leaf_pair = f.leaf_pair;
+  tail.slot_stride = f.slot_stride;
   tail.lut = LutParams{queries, ix.dim, ix.codebook, ix.nb, ix.dpb, LutRows(ix.ksteps), ix.metric,
                        ix.residual, (dbg & 2) ? nullptr : f.lut, f.mult, f.inv, nullptr};
   if (f.one_to_many) {
@@ -3952,7 +3926,7 @@ hipError_t LaunchLutBuild(const DeviceIndex& ix, const float* queries, int nq, i
 
 WorklistArgs MakeWorklistArgs(const DeviceIndex& ix, const uint32_t* leaf_count, WorkItem* work,
                               uint32_t* leaf_item0, uint32_t* pos_unit0, uint32_t* gunits,
-                              ItemLane* lanes, uint4* wave_start, int grid, uint32_t* totals,
+                              uint32_t slot_stride, uint4* wave_start, int grid, uint32_t* totals,
                               unsigned long long* code_bytes, uint32_t chunk_tiles,
                               uint32_t narrow, const Bounds& bd) {
   WorklistArgs w;
@@ -3973,14 +3947,14 @@ WorklistArgs MakeWorklistArgs(const DeviceIndex& ix, const uint32_t* leaf_count,
   w.totals = totals;
   w.code_bytes = code_bytes;
   w.work = work;
-  w.lanes = lanes;
+  w.slot_stride = slot_stride;
   w.wave_start = wave_start;
   return w;
 }
 
 hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, WorkItem* work,
                           uint32_t* leaf_item0, uint32_t* pos_unit0, uint32_t* gunits,
-                          ItemLane* lanes, uint4* wave_start, int grid, uint32_t* totals,
+                          uint32_t slot_stride, uint4* wave_start, int grid, uint32_t* totals,
                           unsigned long long* code_bytes, uint32_t chunk_tiles, uint32_t narrow,
                           unsigned long long* part, const Bounds& bd, hipStream_t s) {
   const int nblk = (ix.nl + 255) / 256;   // (worklist_kernel loops over any count)
@@ -3991,8 +3965,8 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
                      ix.leaf_size, ix.nl, ix.nb, chunk_tiles, narrow, wp, leaf_item0, pos_unit0,
                      gunits, totals, code_bytes);
   const WorklistArgs w = MakeWorklistArgs(ix, leaf_count, work, leaf_item0, pos_unit0, gunits,
-                                          lanes, wave_start, grid, totals, code_bytes, chunk_tiles,
-                                          narrow, bd);
+                                          slot_stride, wave_start, grid, totals, code_bytes,
+                                          chunk_tiles, narrow, bd);
   hipLaunchKernelGGL(items_kernel, dim3(ix.nl), dim3(64), 0, s, w);
   return hipGetLastError();
 }
@@ -4153,15 +4127,6 @@ hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStrea
 hipError_t LaunchKthKeys(const uint32_t* vals, int sets, int kk, uint64_t* out, hipStream_t s) {
   if (sets <= 0) return hipSuccess;
   hipLaunchKernelGGL(kth_keys_kernel, dim3(sets), dim3(256), 0, s, vals, uint32_t(kk), out);
-  return hipGetLastError();
-}
-
-hipError_t LaunchPairScatter(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s) {
-  (void)ix;
-  const size_t pairs = size_t(nq) * size_t(a.L);
-  if (pairs == 0) return hipSuccess;
-  hipLaunchKernelGGL(pair_scatter_kernel, dim3(unsigned((pairs + 255) / 256)), dim3(256), 0, s, a,
-                     nq);
   return hipGetLastError();
 }
 

@@ -102,10 +102,10 @@ struct Workspace {
   float* mult = nullptr;
   float* inv = nullptr;
   uint32_t* counters = nullptr;     // see CounterLayout
-  uint32_t* rank = nullptr;         // [nq*L] each pair's position in its leaf's list
+  uint32_t* leaf_pair = nullptr;    // [nl][nq] each leaf's pairs by rank (top-L kernel)
+  smx::ItemLane* pair_rec = nullptr;   // [nq*L] every pair's record (seed kernel)
   uint32_t* leaf_item0 = nullptr;   // [nl] each leaf's first work item
   smx::WorkItem* work = nullptr;    // [max_items]
-  smx::ItemLane* lanes = nullptr;   // [max_items][32]
   uint4* wave_start = nullptr;      // [grid] each scan wave's static share
   uint32_t* pos_unit0 = nullptr;    // [nl+1] work units before each leaf (work order)
   uint32_t* gunits = nullptr;       // [16] the XCD groups' unit boundaries
@@ -120,7 +120,7 @@ struct Workspace {
   void Release() {
     DFree(queries); DFree(topl_leaf); DFree(topl_dist); DFree(scores); DFree(lut); DFree(mult);
     DFree(inv);
-    DFree(counters); DFree(rank); DFree(leaf_item0); DFree(lanes); DFree(wave_start);
+    DFree(counters); DFree(leaf_pair); DFree(pair_rec); DFree(leaf_item0); DFree(wave_start);
     DFree(pos_unit0); DFree(gunits); DFree(wl_part);
     DFree(work); DFree(tau); DFree(cand); DFree(cand_count); DFree(out_idx);
     DFree(out_dist);
@@ -484,8 +484,8 @@ int EnsureWorkspace(smx_index* h, StreamSlot* sl, int nq, int L, int kk, int wid
       (rc = DAlloc(&w.topl_dist, apairs)) || (rc = DAlloc(&w.scores, size_t(anq) * nl)) ||
       (rc = DAlloc(&w.lut, size_t(anq) * smx::LutRows(ix.ksteps) * 16)) || (rc = DAlloc(&w.mult, anq)) ||
       (rc = DAlloc(&w.inv, anq)) || (rc = DAlloc(&w.counters, CounterLayout(nl).words)) ||
-      (rc = DAlloc(&w.rank, apairs)) || (rc = DAlloc(&w.leaf_item0, size_t(nl))) ||
-      (rc = DAlloc(&w.lanes, size_t(max_items) * smx::kQueriesPerTile)) ||
+      (rc = DAlloc(&w.leaf_pair, size_t(nl) * size_t(anq))) ||
+      (rc = DAlloc(&w.pair_rec, apairs)) || (rc = DAlloc(&w.leaf_item0, size_t(nl))) ||
       (rc = DAlloc(&w.wave_start, size_t(std::max(h->grid, 1)))) ||
       (rc = DAlloc(&w.pos_unit0, size_t(nl + 1))) || (rc = DAlloc(&w.gunits, 16)) ||
       (rc = DAlloc(&w.wl_part, size_t(smx::kWorklistPartWords) * ((nl + 255) / 256))) ||
@@ -536,6 +536,8 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   const int pnn = reorder ? pre_nn : final_nn;
   const int kk = std::max(1, SpillK(ix, pnn));
   const int width = shard_out ? 1 : pre_only ? pnn : final_nn;
+  if (uint64_t(ix.nl) * uint64_t(nq) > 0xFFFFFFFFull)
+    return Fail(SMX_INVALID_ARGUMENT, "num_leaves x batch size must be below 2^32 (leaf slots)");
   StreamSlot* sl = nullptr;
   int rc = SlotFor(h, s, &sl);
   if (rc) return rc;
@@ -575,15 +577,13 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   bd.datapoints = ix.num_datapoints;
   bd.members = ix.num_members;
   bd.tiles = ix.num_tiles;
-  bd.recs = w.max_items * uint32_t(smx::kQueriesPerTile);
+  bd.recs = uint32_t(nl) * uint32_t(nq);
+  bd.pairs = uint32_t(nq) * uint32_t(L);
   smx::SeedArgs sa{};
   sa.bd = bd;
   sa.topl_leaf = w.topl_leaf;
   sa.topl_dist = w.topl_dist;
-  sa.rank = w.rank;
-  sa.leaf_item0 = w.leaf_item0;
-  sa.lanes = w.lanes;
-  sa.chunk_tiles = h->chunk_tiles;
+  sa.pair_rec = w.pair_rec;
   sa.nb = ix.nb;
   sa.lut = w.lut;
   sa.inv = w.inv;
@@ -594,7 +594,6 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sa.L = L;
   sa.seed = seed;
   sa.kk = kk;
-  sa.narrow = narrow;
   sa.nl = nl;
   sa.residual = ix.residual;
 
@@ -605,7 +604,8 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   a.lut = w.lut;
   a.inv = w.inv;
   a.work = w.work;
-  a.lanes = w.lanes;
+  a.leaf_pair = w.leaf_pair;
+  a.pair_rec = w.pair_rec;
   a.chunk_tiles = h->chunk_tiles;
   a.wave_start = w.wave_start;
   a.num_items = w.max_items;   // bound of the one-ahead descriptor prefetch
@@ -697,7 +697,8 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
     f.init.tau = w.tau;
     f.init.n_tau = uint32_t(nq);
     f.leaf_count = cnt;
-    f.rank = w.rank;
+    f.leaf_pair = w.leaf_pair;
+    f.slot_stride = uint32_t(nq);
     f.lut = w.lut;
     f.mult = w.mult;
     f.inv = w.inv;
@@ -708,7 +709,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
       // the work list is built by extra blocks of the seed launch (one
       // stream: a fork/join costs 5-10 us per cross-queue edge)
       const smx::WorklistArgs wla = smx::MakeWorklistArgs(
-          ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes, w.wave_start, h->grid,
+          ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, uint32_t(nq), w.wave_start, h->grid,
           stats + 3, code_bytes, h->chunk_tiles, narrow, bd);
       Mark(h, 3, s);
       SMX_HIP(smx::LaunchSeed(ix, sa, nq, s, &wla));
@@ -717,17 +718,17 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
       // the work-list launches, then the seed, on one stream: beside the
       // seed's blocks (which fill every CU) the side-stream launches are
       // starved until the seed drains
-      SMX_HIP(smx::LaunchWorklist(ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes,
-                                  w.wave_start, h->grid, stats + 3, code_bytes, h->chunk_tiles,
-                                  narrow, w.wl_part, bd, s));
+      SMX_HIP(smx::LaunchWorklist(ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits,
+                                  uint32_t(nq), w.wave_start, h->grid, stats + 3, code_bytes,
+                                  h->chunk_tiles, narrow, w.wl_part, bd, s));
       Mark(h, 3, s);
       SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
       Mark(h, 4, s);
     } else {
       // Fork.  Side stream: the work list (and the empty slots' records);
       // this stream: the seed thresholds.  Write sets ("Two
-      // streams"): side = leaf_item0, pos_unit0, gunits, work, lanes (empty
-      // slots), wave_start, stats[3..7]; seed = tau.  Both only read the
+      // streams"): side = leaf_item0, pos_unit0, gunits, work, wave_start,
+      // stats[3..7]; seed = tau, pair_rec.  Both only read the
       // front end's outputs, written before the fork; the per-call state
       // reset happens in the partition kernel, before the fork as well.
       // The seed (the longer branch) is captured first, so that a replayed
@@ -737,16 +738,13 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
       SMX_HIP(smx::LaunchSeed(ix, sa, nq, s));
       Mark(h, 4, s);
       SMX_HIP(hipStreamWaitEvent(sl->side, sl->fork_ev, 0));
-      SMX_HIP(smx::LaunchWorklist(ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, w.lanes,
-                                  w.wave_start, h->grid, stats + 3, code_bytes, h->chunk_tiles,
-                                  narrow, w.wl_part, bd, sl->side));
+      SMX_HIP(smx::LaunchWorklist(ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits,
+                                  uint32_t(nq), w.wave_start, h->grid, stats + 3, code_bytes,
+                                  h->chunk_tiles, narrow, w.wl_part, bd, sl->side));
       Mark(h, 3, sl->side);
       SMX_HIP(hipEventRecord(sl->join_ev, sl->side));
       SMX_HIP(hipStreamWaitEvent(s, sl->join_ev, 0));   // join
     }
-    // every pair's lane record with its sum limit (needs the work list and
-    // the seed thresholds)
-    SMX_HIP(smx::LaunchPairScatter(ix, sa, nq, s));
     Mark(h, 5, s);
     SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s, narrow));
     Mark(h, 6, s);

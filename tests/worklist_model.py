@@ -88,6 +88,7 @@ def build(sizes, counts, grid, chunk_tiles, small=True):
             for gg in range(gp + 1, GROUPS + 1):
                 gunits[gg] = total_w
     work = [None] * int(sum(items_p))
+    slots = [None] * len(work)
     wave_start = [None] * grid
     for i in range(grid):
         g = i & (GROUPS - 1)
@@ -103,6 +104,11 @@ def build(sizes, counts, grid, chunk_tiles, small=True):
             j0, j1 = chunk_tiles_range(n, chunk_tiles, u % chunks)
             q = u // chunks
             work[item0 + u] = (leaf, n, j0, j1, q, 2 if q < q32 else 1)
+            # the query tile's leaf slots (ItemsCore: slot0 = leaf * stride +
+            # first rank, nslots = min(width, c - first rank))
+            r0 = 32 * q if q < q32 else 32 * q32 + 16 * (q - q32)
+            width = 32 if q < q32 else 16
+            slots[item0 + u] = (r0, min(width, c - r0))
         ua, ub = int(ex_u[p]), int(ex_u[p]) + units_p[p]
         if ua >= ub:
             continue
@@ -132,8 +138,8 @@ def build(sizes, counts, grid, chunk_tiles, small=True):
                     ch += 1
             wave_start[GROUPS * k + g] = (item0 + q * chunks + ch, j, max(0, ue - us - skip))
             k += 1
-    return dict(order=order, work=work, wave_start=wave_start, gunits=gunits, total_w=total_w,
-                chunk_tiles=chunk_tiles)
+    return dict(order=order, work=work, slots=slots, wave_start=wave_start, gunits=gunits,
+                total_w=total_w, chunk_tiles=chunk_tiles)
 
 
 def list_segments(wl, b, max_segs=512):
@@ -195,5 +201,13 @@ def check(sizes, counts, grid=256, chunk_tiles=20, small=True):
             assert (idx, t) in seen, f"tile {t} of item {idx} (leaf {leaf}) never scanned"
         tiles += j1 - j0
     assert len(seen) == tiles
+    # every chunk's query tiles cover the leaf's ranks 0..c-1 exactly once
+    cover = {}
+    for idx, (leaf, n, j0, j1, qt, w) in enumerate(wl["work"]):
+        r0, ns = wl["slots"][idx]
+        assert 0 < ns <= (32 if w == 2 else 16)
+        cover.setdefault((leaf, j0), []).extend(range(r0, r0 + ns))
+    for (leaf, j0), ranks in cover.items():
+        assert sorted(ranks) == list(range(counts[leaf])), (leaf, j0)
     assert sum((j1 - j0) * w for (_, _, j0, j1, _, w) in wl["work"]) == wl["total_w"]
     return wl
