@@ -404,12 +404,14 @@ def main():
     ap.add_argument("--sweep-steps", type=int, default=20)
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the oracle check of the generated-shard lines")
+    ap.add_argument("--leaves-to-search", type=int, default=0,
+                    help="override the configuration's leaves_to_search (0: as configured)")
     ap.add_argument("--in-flight", type=int, default=3,
                     help="query batches in flight (streams, one library workspace each)")
     args = ap.parse_args()
     global CFG, LEAVES, LEAVES_TO_SEARCH
     CFG = CONFIGS[args.config]
-    LEAVES, LEAVES_TO_SEARCH = CFG["leaves"], CFG["leaves_to_search"]
+    LEAVES, LEAVES_TO_SEARCH = CFG["leaves"], args.leaves_to_search or CFG["leaves_to_search"]
     if args.config != "glove" and args.n == 1_183_514:
         args.n = CFG["n"]
 
