@@ -25,10 +25,9 @@ constexpr int kTotalsTiles16 = 9;
 #endif
 constexpr int kSeedKeys = 256 * SMX_SEED_PER_THREAD;
 constexpr uint32_t kItemNarrow = 1u << 31;
-// WorklistArgs::narrow / SeedArgs::narrow: 0 = 32-slot tiles only, 1 = a
-// leaf's last <= 16 queries in a 16-slot tile, kNarrowOnly = 16-slot tiles only
+// WorklistArgs::narrow: 0 = 32-slot tiles only, kNarrowOnly = 16-slot tiles only
 constexpr uint32_t kNarrowOnly = 2;
-// 16-slot tiles are used when a call averages fewer queries per leaf
+// 16-slot tiles (only) are used when a call averages fewer queries per leaf
 // (nq * L / num_leaves) than this
 constexpr int kNarrowQueriesPerLeaf = 32;
 constexpr int kDpPerTile = 32;
@@ -204,7 +203,7 @@ struct WorklistArgs {
   int nb;
   uint32_t chunk_tiles;
   int grid;                    // scan workgroups
-  uint32_t narrow;             // 16-slot tiles for remainders of <= 16 queries
+  uint32_t narrow;             // kNarrowOnly: 16-slot query tiles, 0: 32-slot
   uint32_t* leaf_item0;        // [nl]
   uint32_t* pos_unit0;         // [nl + 1]
   uint32_t* gunits;            // [9]

@@ -1155,14 +1155,14 @@ __device__ __forceinline__ uint2 ChunkTiles(uint32_t n, uint32_t chunk_tiles, ui
 // 2 units, a 16-slot item's 1; the shares cut the units, and a tile belongs
 // to the share that holds its first unit.
 // ---------------------------------------------------------------------------
-// 32-slot and 16-slot query tiles of a leaf with c queries (narrow 1: a
-// remainder of at most 16 queries in a 16-slot tile; 2: 16-slot tiles only).
+// 32-slot and 16-slot query tiles of a leaf with c queries (narrow 0:
+// 32-slot tiles only; kNarrowOnly: 16-slot tiles only).  (Round 4's mixed
+// mode -- a remainder of <= 16 queries in one 16-slot tile, scanned by a
+// kernel carrying both paths -- lost to one of these at every density
+// measured and was removed: DESIGN.md section 3.)
 __device__ __forceinline__ uint2 LeafQueryTiles(uint32_t c, uint32_t narrow) {
   if (narrow == kNarrowOnly) return make_uint2(0u, (c + kNarrowSlots - 1u) / kNarrowSlots);
-  const uint32_t full = c / uint32_t(kQueriesPerTile), r = c % uint32_t(kQueriesPerTile);
-  if (r == 0) return make_uint2(full, 0u);
-  if (narrow && r <= uint32_t(kNarrowSlots)) return make_uint2(full, 1u);
-  return make_uint2(full + 1u, 0u);
+  return make_uint2((c + kQueriesPerTile - 1u) / kQueriesPerTile, 0u);
 }
 // Per leaf: its items and units.
 __device__ __forceinline__ uint32_t LeafUnits(uint32_t c, uint32_t n, uint32_t chunk_tiles,
@@ -2283,8 +2283,8 @@ struct LaneVal {
   __device__ __forceinline__ operator int() const { return v; }
 };
 
-// NRW: 0 = 32-slot items only (only that path is compiled in: fewer
-// registers and code), 1 = both kinds, kNarrowOnly = 16-slot items only.
+// NRW: 0 = 32-slot items only, kNarrowOnly = 16-slot items only (one path
+// compiled into each kernel: fewer registers and less code).
 template <int K, int ABL = 0, int NRW = 0>
 __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(ScanArgs a) {
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
@@ -2438,9 +2438,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         const uint32_t s0 = __builtin_amdgcn_readfirstlane(s_desc[sgi].slot0);
         const uint32_t ns = __builtin_amdgcn_readfirstlane(s_desc[sgi].nslots);
         uint32_t cs = uint32_t(c);
-        if constexpr (NRW != 0) {
-          if (__builtin_amdgcn_readfirstlane(s_desc[sgi].leaf) & kItemNarrow) cs = uint32_t(lane & 15);
-        }
+        if constexpr (NRW == int(kNarrowOnly)) cs = uint32_t(lane & 15);
         ItemLane r;
         if (cs < ns) {
           SMX_CHECK(s0 + cs, a.bd.recs, "leaf slot");
@@ -2875,13 +2873,9 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         whits = 0;
       }
       };
+      static_assert(NRW == 0 || NRW == int(kNarrowOnly), "one tile width per kernel");
       if constexpr (NRW == int(kNarrowOnly)) {
         run_seg(std::true_type{});
-      } else if constexpr (NRW != 0) {
-        if (leaf_w & kItemNarrow)
-          run_seg(std::true_type{});
-        else
-          run_seg(std::false_type{});
       } else {
         run_seg(std::false_type{});
       }
@@ -4001,9 +3995,6 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
     else if (narrow == kNarrowOnly)                                                        \
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, int(kNarrowOnly)>), dim3(grid),         \
                          dim3(64 * ScanWaves<KV>()), 0, s, a);                             \
-    else if (narrow)                                                                       \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, 1>), dim3(grid),                        \
-                         dim3(64 * ScanWaves<KV>()), 0, s, a);                             \
     else                                                                                   \
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
                          0, s, a);                                                         \
@@ -4014,9 +4005,6 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
     if (variant != 0) return hipErrorInvalidValue;                                         \
     if (narrow == kNarrowOnly)                                                             \
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, int(kNarrowOnly)>), dim3(grid),         \
-                         dim3(64 * ScanWaves<KV>()), 0, s, a);                             \
-    else if (narrow)                                                                       \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, 1>), dim3(grid),                        \
                          dim3(64 * ScanWaves<KV>()), 0, s, a);                             \
     else                                                                                   \
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()), \

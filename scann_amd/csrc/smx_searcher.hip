@@ -181,7 +181,6 @@ struct smx_index {
   // (v_smfmac_i32_16x16x128_i8); SMX_NARROW=0 keeps every query tile 32 wide
   bool narrow_tiles = true;
   bool narrow_only = false;        // SMX_NARROW=2: 16-slot tiles only whatever the density
-  bool narrow_mixed_only = false;  // SMX_NARROW=3: never the 16-slot-only mode
   // above fused_worklist_leaves: the work-list launches on this stream before
   // the seed (true; SMX_SERIAL_WORKLIST=0: on the side stream beside it --
   // same box A/B, configs[3]/[4]: 0.578 vs 0.584 and 1.478 vs 1.495 ms/step)
@@ -555,20 +554,17 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   const int seed = std::min(h->seed_leaves, L);
 
   const int variant = h->scan_variant;
-  // 16-slot tiles where leaves see few queries on average (configs 3/4: ~8
-  // per leaf); with ~100 (glove) the 32-slot-only kernel is faster (the
-  // 16-slot path costs registers and code in the kernel that carries it)
-  // (fewer than 16 per leaf: 16-slot tiles only, the narrow-only kernel;
-  // SMX_NARROW=2 forces that mode, for the tests)
+  // 16-slot tiles only (lut16_scan_kernel<K, 0, kNarrowOnly>) where leaves
+  // see fewer than 32 queries on average (configs 3/4: ~8 per leaf; glove's
+  // recall gate L = 20: 20 per leaf, scan 38.2 -> 33.6 us); 32-slot tiles at
+  // glove's L = 100 (100 per leaf) and SIFT's (50 per leaf), where the wide
+  // kernel is faster (106 vs 115 us on SIFT).  SMX_NARROW=2 forces 16-slot
+  // tiles, SMX_NARROW=0 32-slot tiles (the tests run every mode).
   const uint64_t qpl_x = uint64_t(nq) * uint64_t(L);   // queries per leaf x nl
   uint32_t narrow = 0;
-  if (h->narrow_tiles && variant == 0) {
-    if (h->narrow_only ||
-        (!h->narrow_mixed_only && qpl_x < uint64_t(smx::kNarrowSlots) * uint64_t(ix.nl)))
-      narrow = smx::kNarrowOnly;
-    else if (qpl_x < uint64_t(smx::kNarrowQueriesPerLeaf) * uint64_t(ix.nl))
-      narrow = 1;
-  }
+  if (h->narrow_tiles && variant == 0 &&
+      (h->narrow_only || qpl_x < uint64_t(smx::kNarrowQueriesPerLeaf) * uint64_t(ix.nl)))
+    narrow = smx::kNarrowOnly;
   smx::Bounds bd;
   bd.nq = uint32_t(nq);
   bd.items = w.max_items;
@@ -974,10 +970,9 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
     h->fused_worklist_leaves = std::min(std::atoi(fw), smx::kFusedWorklistLeaves);
   if (const char* nw = std::getenv("SMX_NARROW")) {
     // 0: 32-slot tiles only; 1: by density (default); 2: 16-slot tiles only
-    // whatever the density; 3: never 16-slot-only (the remainder tiles only)
+    // whatever the density
     h->narrow_tiles = nw[0] != '0';
     h->narrow_only = nw[0] == '2';
-    h->narrow_mixed_only = nw[0] == '3';
   }
   if (const char* sw = std::getenv("SMX_SERIAL_WORKLIST")) h->serial_worklist = sw[0] != '0';
   const char* ng = std::getenv("SMX_NO_GRAPH");

@@ -3,10 +3,9 @@
 These switches select kernels without changing any result (all are read
 when a handle is created):
 
-  * SMX_NARROW -- 16-slot scan tiles (v_smfmac_i32_16x16x128_i8): 0 none,
-    1 by density (a leaf's last <= 16 queries below 32 queries per leaf on
-    average, 16-slot tiles only below 16), 2 16-slot tiles only, 3 never the
-    16-slot-only mode;
+  * SMX_NARROW -- 16-slot scan tiles (v_smfmac_i32_16x16x128_i8): 0 none
+    (32-slot tiles only), 1 by density (16-slot tiles only below 32 queries
+    per leaf on average), 2 16-slot tiles only;
   * SMX_FUSED_WORKLIST=0 / SMX_SERIAL_WORKLIST=0 -- the work list from its
     three launches (as above 4096 leaves), on the seed's stream or on the
     side stream;
@@ -28,7 +27,7 @@ from tests.conftest import make_index
 
 pytestmark = pytest.mark.gpu
 
-PATHS = [({"SMX_NARROW": n}, 0) for n in "0123"] + [
+PATHS = [({"SMX_NARROW": n}, 0) for n in "012"] + [
     # the smallest work items: the item buffer's worst case, 16-slot only
     ({"SMX_NARROW": "2"}, 8), ({"SMX_NARROW": "1"}, 8), ({"SMX_NARROW": "0"}, 16),
     # the work list by its three launches: before the seed on one stream, and

@@ -9,7 +9,7 @@ import pytest
 import worklist_model as wm
 
 
-@pytest.mark.parametrize("small", [True, False, 2])
+@pytest.mark.parametrize("small", [False, 2])
 @pytest.mark.parametrize("seed", range(10))
 def test_shares_cover_items_exactly_once(seed, small):
     rng = np.random.default_rng(seed)
@@ -30,27 +30,9 @@ def test_shares_cover_items_exactly_once(seed, small):
     ([4000] * 3, [200, 1, 64]),      # leaves of many chunks, full query tiles
 ])
 def test_edge_shapes(sizes, counts):
-    for small in (True, False, 2):
+    for small in (False, 2):
         for grid in (8, 256, 3072):
             wm.check(sizes, counts, grid=grid, small=small)
-
-
-@pytest.mark.parametrize("seed", range(6))
-def test_few_queries_per_leaf_take_16_slot_tiles(seed):
-    """configs[4]'s density (a few queries per leaf): the items are 16-slot
-    tiles (weight 1), shares of 1-3 units (more workgroups than units) stay
-    exact, and a remainder of 17-31 queries keeps a 32-slot tile."""
-    rng = np.random.default_rng(300 + seed)
-    nl = int(rng.integers(50, 2000))
-    sizes = rng.integers(0, 4000, nl)
-    counts = rng.poisson(rng.uniform(1, 12), nl)
-    wl = wm.check([int(x) for x in sizes], [int(x) for x in counts],
-                  grid=int(rng.choice([256, 3072, 8192])), chunk_tiles=20)
-    for leaf, n, j0, j1, q, w in wl["work"]:
-        c = int(counts[leaf])
-        assert w == (1 if (c - 32 * q) <= 16 else 2)
-    assert wm.query_tiles(17) == (1, 0) and wm.query_tiles(16) == (0, 1)
-    assert wm.query_tiles(48) == (1, 1) and wm.query_tiles(64) == (2, 0)
 
 
 @pytest.mark.parametrize("seed", range(6))
@@ -86,7 +68,7 @@ def test_item_capacity_at_small_chunks(seed, chunk_tiles):
     nl = int(rng.integers(20, 400))
     sizes = [64 * 32] * nl if seed == 0 else [int(x) for x in rng.integers(0, 4000, nl)]
     counts = [48] * nl if seed == 0 else [int(x) for x in rng.poisson(rng.uniform(1, 60), nl)]
-    for small in (True, False, 2):
+    for small in (False, 2):
         wm.check(sizes, counts, grid=256, chunk_tiles=chunk_tiles, small=small)
     if seed == 0:
         wl = wm.build(sizes, counts, 256, 8, 2)

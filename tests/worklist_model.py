@@ -41,21 +41,16 @@ def leaf_order(sizes):
     return order
 
 
-def query_tiles(c, small=True):
+def query_tiles(c, small=False):
     """(32-slot, 16-slot) query tiles of a leaf with c queries (LeafQueryTiles):
-    a remainder of at most 16 queries takes a 16-slot tile; small == 2: every
-    query tile has 16 slots."""
+    small == 2 (kNarrowOnly): every query tile has 16 slots; otherwise every
+    query tile has 32."""
     if small == 2:
         return 0, (c + 15) // 16
-    full, r = divmod(c, 32)
-    if r == 0:
-        return full, 0
-    if small and r <= 16:
-        return full, 1
-    return full + 1, 0
+    return (c + 31) // 32, 0
 
 
-def build(sizes, counts, grid, chunk_tiles, small=True):
+def build(sizes, counts, grid, chunk_tiles, small=False):
     """Items (leaf, n, j0, jend, query tile, weight) and the workgroups'
     shares (first item, first tile, units).  A unit is a 16-slot tile: a
     32-slot item's tiles weigh 2, a 16-slot item's 1; a tile belongs to the
@@ -182,7 +177,7 @@ def max_items(sizes, pairs):
     return (pairs // 16 + len(sizes) + 1) * chunks
 
 
-def check(sizes, counts, grid=256, chunk_tiles=20, small=True):
+def check(sizes, counts, grid=256, chunk_tiles=20, small=False):
     wl = build(sizes, counts, grid, chunk_tiles, small)
     cap = max_items(sizes, int(sum(counts)))
     assert len(wl["work"]) <= cap, f"{len(wl['work'])} items > MaxItems {cap}"
