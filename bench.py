@@ -406,6 +406,10 @@ def main():
                     help="skip the oracle check of the generated-shard lines")
     ap.add_argument("--leaves-to-search", type=int, default=0,
                     help="override the configuration's leaves_to_search (0: as configured)")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the one-batch-at-a-time timing (the per-batch latency)")
+    ap.add_argument("--no-stages", action="store_true",
+                    help="skip the per-stage replay (stage_ms, the scan alone)")
     ap.add_argument("--in-flight", type=int, default=3,
                     help="query batches in flight (streams, one library workspace each)")
     args = ap.parse_args()
@@ -477,30 +481,39 @@ def main():
             el = float(tt.item())
         return el
 
-    # timed steps: eager launches of the six pipeline kernels per step
+    # timed steps: eager launches of the pipeline kernels per step, with two
+    # HIP events around every scan launch on its own stream (profiling mode
+    # 2: no synchronisation, the batches stay in flight) -- the roofline's
+    # per-launch duration comes from these very launches
     nat.set_profiling(False)
     for i in range(max(args.warmup, n_fl)):
         step(i)
+    nat.set_profiling(2)
     elapsed = timed_steps(n_fl)
+    t_fl = nat.timings()
+    nat.set_profiling(False)
     ms_per_step = elapsed * 1000.0 / args.steps
     value = world * NQ * args.steps / elapsed
+    scan_ms_fl, scan_launches = float(t_fl["scan_ms_mode2"]), int(t_fl["scan_launches"])
     # the same steps one at a time (one stream): the per-batch latency
-    elapsed_1 = timed_steps(1) if n_fl > 1 else elapsed
+    elapsed_1 = timed_steps(1) if n_fl > 1 and not args.no_latency else None
 
-    # per-kernel durations: the same steps replayed with HIP events recorded on
-    # the library's stream around every stage launch (profiled calls launch
-    # eagerly: events inside a captured graph carry no timestamps)
+    # per-stage durations, each kernel alone: the same steps replayed one at
+    # a time with HIP events recorded on the call's stream around every stage
+    # launch (profiling mode 1: synchronous calls); with --no-stages one such
+    # call only, for the launch's code bytes and tile counts
     nat.set_profiling(True)
     step()
     scan_ms, stage, scan_bytes = [], {}, []
-    for _ in range(args.steps):
+    n_rep = 1 if args.no_stages else args.steps
+    for _ in range(n_rep):
         step()
         t = nat.timings()
         scan_ms.append(t["scan_ms"])
         scan_bytes.append(t["scan_code_bytes"])
         for k in ("partition_ms", "lut_ms", "invert_ms", "seed_scan_ms", "seed_select_ms",
                   "scan_ms", "select_ms", "total_ms"):
-            stage[k] = stage.get(k, 0.0) + t[k] / args.steps
+            stage[k] = stage.get(k, 0.0) + t[k] / n_rep
     t_last = nat.timings()
     nat.set_profiling(False)
     torch.cuda.synchronize()
@@ -534,7 +547,19 @@ def main():
 
     avg_scan_ms = float(np.mean(scan_ms))
     bytes_per_launch = float(np.mean(scan_bytes))
-    roof = scan_roofline(bytes_per_launch, avg_scan_ms, t_last, ix.num_blocks)
+    # the roofline of the scan launches of the timed region (in flight, each
+    # sharing the device with the other batches' kernels), and of the scan
+    # alone (serial replay) beside it
+    roof = scan_roofline(bytes_per_launch, scan_ms_fl, t_last, ix.num_blocks)
+    roof["avg_launch_ms_source"] = (
+        f"HIP events on each call's stream around every scan launch of the timed region "
+        f"({scan_launches} launches, {n_fl} batches in flight)")
+    iso = scan_roofline(bytes_per_launch, avg_scan_ms, t_last, ix.num_blocks)
+    roof["isolated"] = {
+        "avg_launch_ms": iso["avg_launch_ms"], "achieved": iso["achieved"], "frac": iso["frac"],
+        "smfmac_pipe_frac": iso["smfmac_pipe_frac"],
+        "source": f"HIP events around the scan of {len(scan_ms)} calls replayed one at a time "
+                  f"(the kernel alone on the device)"}
     traffic = scan_traffic(args.config)
 
     if rank == 0:
@@ -547,8 +572,9 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "in_flight": n_fl,
-            "single_stream": {"qps": round(world * NQ * args.steps / elapsed_1, 1),
-                              "ms_per_step": round(elapsed_1 * 1000.0 / args.steps, 4)},
+            "single_stream": ({"qps": round(world * NQ * args.steps / elapsed_1, 1),
+                               "ms_per_step": round(elapsed_1 * 1000.0 / args.steps, 4)}
+                              if elapsed_1 else None),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -563,9 +589,10 @@ def main():
             },
             "recall_at_10": round(recall, 4),
             "roofline": dict(roof, traffic=traffic,
-                             hbm_GBps_measured=(round(traffic / (avg_scan_ms * 1e-3) / 1e9, 1)
+                             hbm_GBps_measured=(round(traffic / (scan_ms_fl * 1e-3) / 1e9, 1)
                                                 if traffic else None)),
-            "stage_ms": {k: round(v, 4) for k, v in stage.items()},
+            "stage_ms": ({k: round(v, 4) for k, v in stage.items()} if not args.no_stages
+                         else None),
             "operating_points": points,
             "qps_at_recall_0.95": next(({"leaves_to_search": p["leaves_to_search"],
                                          "qps": p["qps"], "recall_at_10": p["recall_at_10"]}

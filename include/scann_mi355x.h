@@ -117,7 +117,12 @@ typedef struct smx_search_params {
 
 /* Stage timings of the last search on a handle (ms, HIP events recorded on
  * the handle's stream around each launch; filled only when profiling was
- * enabled with smx_set_profiling). */
+ * enabled with smx_set_profiling(index, 1), which makes every call
+ * synchronous).  smx_set_profiling(index, 2) instead records two events
+ * around every scan launch of the calls that follow, without synchronising
+ * (up to 4096 launches, the latest kept): smx_get_timings then reports
+ * their count and mean duration (scan_launches, scan_ms_mode2) once the
+ * caller has synchronised the device. */
 typedef struct smx_timings {
   float partition_ms;
   float lut_ms;
@@ -141,6 +146,11 @@ typedef struct smx_timings {
   int32_t scan_workgroups;  /* persistent scan grid (one wave each)          */
   double scan_item_tiles16; /* 16-slot tiles of the main scan
                                (x 2*ceil(K/4) v_smfmac_i32_16x16x128_i8)     */
+  int32_t scan_launches;    /* profiling mode 2: scan launches averaged into
+                               scan_ms_mode2                                 */
+  float scan_ms_mode2;      /* profiling mode 2: mean duration of those scan
+                               launches (HIP events on each call's stream,
+                               no synchronisation: batches stay in flight)   */
 } smx_timings;
 
 /* Index lifecycle (ScannNumpy ctor / destructor; scann_npy.cc:57-77). */
@@ -312,6 +322,8 @@ int smx_gather_residuals(const float* d_x, int32_t d, const uint32_t* d_rows,
                          int64_t row_base, float* d_out, void* stream);
 
 /* ---- diagnostics ---------------------------------------------------------- */
+/* 0: off; 1: per-call stage timings (synchronous calls); 2: scan-launch
+ * durations of the calls in flight (see smx_timings). */
 int smx_set_profiling(smx_index* index, int32_t enabled);
 int smx_get_timings(const smx_index* index, smx_timings* out);
 /* Tuning knobs: candidate buffer capacity per query (0, the default: sized

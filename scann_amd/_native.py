@@ -37,7 +37,8 @@ class Timings(ctypes.Structure):
                 ("scan_pairs", ctypes.c_int32), ("seed_pairs", ctypes.c_int32),
                 ("overflow_retries", ctypes.c_int32), ("max_candidates", ctypes.c_int32),
                 ("scan_item_tiles", ctypes.c_double), ("mean_candidates", ctypes.c_float),
-                ("scan_workgroups", ctypes.c_int32), ("scan_item_tiles16", ctypes.c_double)]
+                ("scan_workgroups", ctypes.c_int32), ("scan_item_tiles16", ctypes.c_double),
+                ("scan_launches", ctypes.c_int32), ("scan_ms_mode2", ctypes.c_float)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -320,8 +321,11 @@ class NativeIndex:
               "smx_lut16_leaf_scores")
         return out[:n]
 
-    def set_profiling(self, on: bool):
-        check(self.lib.smx_set_profiling(self.h, int(bool(on))), "smx_set_profiling")
+    def set_profiling(self, on):
+        """False / True (mode 1: synchronous per-call stage timings) or 2
+        (scan-launch durations of the calls in flight, no synchronisation)."""
+        mode = 2 if on == 2 else int(bool(on))
+        check(self.lib.smx_set_profiling(self.h, mode), "smx_set_profiling")
 
     def timings(self):
         t = Timings()

@@ -187,7 +187,12 @@ struct smx_index {
   bool serial_worklist = true;
   int grid = 0;                    // scan grid: resident one-wave workgroups (occupancy API)
   int cus = 0;                     // compute units of the device
-  bool profiling = false;
+  bool profiling = false;          // mode 1: per-call stage timings (synchronous calls)
+  // mode 2: an event pair around every scan launch, no synchronisation
+  // (kScanLog pairs, the latest kept; read by smx_get_timings)
+  bool scan_log = false;
+  std::vector<hipEvent_t> scan_ev;
+  uint64_t scan_logged = 0;
   bool use_graph = false;          // SMX_GRAPH=1: replay the pipeline as a hipGraph
   uint64_t ws_generation = 0;
   uint32_t* host_stats = nullptr;  // pinned copy of the stats words
@@ -201,6 +206,7 @@ struct smx_index {
 namespace {
 
 constexpr int GraphKeyWords = 16;
+constexpr uint64_t kScanLog = 4096;   // profiling mode 2: scan event pairs kept
 
 int UploadIndex(const smx_index_desc* d, smx_index* h) {
   smx::DeviceIndex& ix = h->ix;
@@ -742,7 +748,13 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
       SMX_HIP(hipStreamWaitEvent(s, sl->join_ev, 0));   // join
     }
     Mark(h, 5, s);
+    const size_t le = size_t(h->scan_logged % kScanLog) * 2;
+    if (h->scan_log) SMX_HIP(hipEventRecord(h->scan_ev[le], s));
     SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s, narrow));
+    if (h->scan_log) {
+      SMX_HIP(hipEventRecord(h->scan_ev[le + 1], s));
+      ++h->scan_logged;
+    }
     Mark(h, 6, s);
     SMX_HIP(smx::LaunchFinalSelect(sel, nq, s));
     Mark(h, 7, s);
@@ -778,7 +790,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   bool ran = false;
   // (profiled calls run eagerly: HIP events recorded inside a captured graph
   // carry no timestamps)
-  if (h->use_graph && !h->profiling && s) {
+  if (h->use_graph && !h->profiling && !h->scan_log && s) {
     const uint64_t key[GraphKeyWords] = {
         uint64_t(reinterpret_cast<uintptr_t>(queries)), uint64_t(nq), uint64_t(L), uint64_t(pnn),
         uint64_t(final_nn), uint64_t(reorder) | uint64_t(pre_only) << 1 | uint64_t(h->profiling) << 2 |
@@ -997,6 +1009,8 @@ int smx_index_destroy(smx_index* h) {
   DFree(h->stamp_count);
   FreeIndex(h->ix);
   for (auto& e : h->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : h->scan_ev)
     if (e) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -1414,13 +1428,43 @@ int smx_lut16_leaf_scores(smx_index* h, int32_t leaf, const uint8_t* lut, int32_
 
 int smx_set_profiling(smx_index* h, int32_t enabled) {
   if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
-  h->profiling = enabled != 0;
+  if (enabled < 0 || enabled > 2) return Fail(SMX_INVALID_ARGUMENT, "profiling mode must be 0, 1 or 2");
+  std::lock_guard<std::mutex> lock(h->mu);
+  SMX_HIP(hipSetDevice(h->device));
+  h->profiling = enabled == 1;
+  h->scan_log = enabled == 2;
+  if (h->scan_log) {
+    if (h->scan_ev.empty()) {
+      h->scan_ev.assign(2 * kScanLog, nullptr);
+      for (auto& e : h->scan_ev) SMX_HIP(hipEventCreate(&e));
+    }
+    h->scan_logged = 0;
+  }
   return SMX_OK;
 }
 
 int smx_get_timings(const smx_index* h, smx_timings* out) {
   if (!h || !out) return Fail(SMX_INVALID_ARGUMENT, "null argument");
   *out = h->timings;
+  out->scan_launches = 0;
+  out->scan_ms_mode2 = 0.0f;
+  if (!h->scan_ev.empty() && h->scan_logged) {
+    // the latest min(logged, kScanLog) pairs; a pair not yet complete (the
+    // caller has not synchronised) is not counted
+    const uint64_t n = std::min<uint64_t>(h->scan_logged, kScanLog);
+    double sum = 0.0;
+    int32_t cnt = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      float ms = 0.0f;
+      if (hipEventElapsedTime(&ms, h->scan_ev[2 * i], h->scan_ev[2 * i + 1]) == hipSuccess) {
+        sum += ms;
+        ++cnt;
+      }
+    }
+    (void)hipGetLastError();
+    out->scan_launches = cnt;
+    out->scan_ms_mode2 = cnt ? float(sum / cnt) : 0.0f;
+  }
   return SMX_OK;
 }
 
