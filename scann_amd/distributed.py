@@ -66,11 +66,17 @@ class NativeShardEngine:
         self.stream = torch.cuda.Stream(device=self.device)
 
     def _enter(self, *tensors):
+        """The stream the native call runs on: the caller's current stream
+        when it is a stream of its own (the library keeps one workspace per
+        stream, so batches on different streams run concurrently), else the
+        engine's stream, ordered against the caller's both ways."""
         cur = torch.cuda.current_stream(self.device)
+        if cur.cuda_stream != 0:
+            return cur, cur
         self.stream.wait_stream(cur)
         for t in tensors:
             t.record_stream(self.stream)
-        return cur
+        return cur, self.stream
 
     def shard_width(self, leaves, pre_nn, final_nn, reorder) -> int:
         return self.nat.shard_width(leaves, pre_nn, final_nn, reorder)
@@ -78,21 +84,23 @@ class NativeShardEngine:
     def search_shard(self, queries: torch.Tensor, leaves, pre_nn, final_nn, reorder,
                      out_entries: torch.Tensor) -> None:
         q = queries.contiguous()
-        cur = self._enter(q, out_entries)
+        cur, run = self._enter(q, out_entries)
         self.nat.search_shard_device(q.data_ptr(), q.shape[0], leaves, pre_nn, final_nn, reorder,
-                                     out_entries.data_ptr(), self.stream.cuda_stream)
-        cur.wait_stream(self.stream)
+                                     out_entries.data_ptr(), run.cuda_stream)
+        if run is not cur:
+            cur.wait_stream(run)
 
     def merge(self, world, entries: torch.Tensor, nq, leaves, pre_nn, final_nn, reorder):
         idx = torch.empty((nq, final_nn), dtype=torch.int32, device=self.device)
         dst = torch.empty((nq, final_nn), dtype=torch.float32, device=self.device)
         cnt = torch.empty((nq,), dtype=torch.int32, device=self.device)
         ent = entries.contiguous()
-        cur = self._enter(ent, idx, dst, cnt)
+        cur, run = self._enter(ent, idx, dst, cnt)
         self.nat.merge_shards_device(world, nq, leaves, pre_nn, final_nn, reorder, ent.data_ptr(),
                                      idx.data_ptr(), dst.data_ptr(), cnt.data_ptr(),
-                                     self.stream.cuda_stream)
-        cur.wait_stream(self.stream)
+                                     run.cuda_stream)
+        if run is not cur:
+            cur.wait_stream(run)
         return idx, dst, cnt
 
 
