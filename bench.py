@@ -601,6 +601,7 @@ def main():
                                          "qps": p["qps"], "recall_at_10": p["recall_at_10"]}
                                         for p in points if p["recall_at_10"] >= 0.95), None),
             "candidates_max": t_last["max_candidates"],
+            "candidates_mean": round(float(t_last["mean_candidates"]), 1),
         }
         # full-size parity: oracle (ideal mode) on a query subset, ids must match
         from oracle import binding as oracle
