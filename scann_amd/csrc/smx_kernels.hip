@@ -2668,10 +2668,10 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
           }
           if (hb) {
             uint32_t pk[4];
-            pk[0] = (uint32_t(acc_a[0]) & 0xFFFFu) | (uint32_t(acc_a[1]) << 16);
-            pk[1] = (uint32_t(acc_a[2]) & 0xFFFFu) | (uint32_t(acc_a[3]) << 16);
-            pk[2] = (uint32_t(acc_b[0]) & 0xFFFFu) | (uint32_t(acc_b[1]) << 16);
-            pk[3] = (uint32_t(acc_b[2]) & 0xFFFFu) | (uint32_t(acc_b[3]) << 16);
+            pk[0] = __builtin_amdgcn_perm(uint32_t(acc_a[1]), uint32_t(acc_a[0]), 0x05040100u);
+            pk[1] = __builtin_amdgcn_perm(uint32_t(acc_a[3]), uint32_t(acc_a[2]), 0x05040100u);
+            pk[2] = __builtin_amdgcn_perm(uint32_t(acc_b[1]), uint32_t(acc_b[0]), 0x05040100u);
+            pk[3] = __builtin_amdgcn_perm(uint32_t(acc_b[3]), uint32_t(acc_b[2]), 0x05040100u);
             append_hit(hit, hb, pk, jt);
           }
         } else {
@@ -2702,10 +2702,13 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
             return;
           }
           if (hb) {
+            // the 16 sums as int16 pairs, one v_perm_b32 each (low halves of
+            // acc[2k] and acc[2k + 1]; a shift + or was two VALU per pair)
             uint32_t pk[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k)
-              pk[k] = (uint32_t(acc[2 * k]) & 0xFFFFu) | (uint32_t(acc[2 * k + 1]) << 16);
+              pk[k] = __builtin_amdgcn_perm(uint32_t(acc[2 * k + 1]), uint32_t(acc[2 * k]),
+                                            0x05040100u);
             append_hit(hit, hb, pk, jt);
           }
         }
