@@ -987,6 +987,15 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
     h->narrow_only = nw[0] == '2';
   }
   if (const char* sw = std::getenv("SMX_SERIAL_WORKLIST")) h->serial_worklist = sw[0] != '0';
+  // tuning knobs for A/Bs (the defaults otherwise; smx_set_tuning overrides)
+  if (const char* ct = std::getenv("SMX_CHUNK_TILES")) {
+    const int v = std::atoi(ct);
+    if (v >= 8 && v <= 65535) h->chunk_tiles = uint32_t(v);
+  }
+  if (const char* sl = std::getenv("SMX_SEED_LEAVES")) {
+    const int v = std::atoi(sl);
+    if (v >= 0 && v <= 64) h->seed_leaves = v;
+  }
   const char* ng = std::getenv("SMX_NO_GRAPH");
   // Eager launches by default: six kernels a call queue back to back on the
   // stream, while consecutive replays of a captured graph left ~13 us
