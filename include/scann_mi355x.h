@@ -23,9 +23,11 @@
  *  - Distances are returned in the reference's internal convention (smaller
  *    is better; -dot for dot product).  The x(-1) of ReshapeBatchedNNResult
  *    (scann/scann_ops/cc/scann.h:162-180) is applied by the caller.
- *  - Calls on one handle may come from several host threads; they are
- *    serialised on the handle's stream (re-entrant per the reference's
- *    const FindNeighbors*Impl, SURVEY.md §8b "Threading").
+ *  - Calls on one handle may come from several host threads; their host
+ *    side is serialised by the handle's mutex (re-entrant per the
+ *    reference's const FindNeighbors*Impl, SURVEY.md §8b "Threading"), and
+ *    each stream gets its own per-call workspace (up to 4 streams), so work
+ *    enqueued on different streams runs concurrently on the device.
  *  - Device code targets gfx950 (MI355X) only.
  */
 #ifndef SCANN_MI355X_H_
@@ -170,8 +172,9 @@ int smx_search_batched(smx_index* index, const float* queries, int32_t nq,
 /* Same with device buffers, enqueued on `stream` (hipStream_t; NULL = the
  * handle's own stream) with no host synchronisation: the results are ready
  * when the stream reaches them (candidate-list overflow is handled on the
- * device).  Calls on different streams are ordered after one another (the
- * handle's workspace is shared).  d_out_count may be NULL. */
+ * device).  Calls on different streams run concurrently (one workspace per
+ * stream, up to 4; a fifth stream reuses the oldest one after waiting for
+ * its work).  d_out_count may be NULL. */
 int smx_search_batched_device(smx_index* index, const float* d_queries, int32_t nq,
                               int32_t dim, const smx_search_params* params,
                               uint32_t* d_out_idx, float* d_out_dist,
