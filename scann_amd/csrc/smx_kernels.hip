@@ -1356,10 +1356,9 @@ __device__ void WaveStarts(const WorklistArgs& w, int p, const uint32_t* gunits,
   }
 }
 
-// Phase 2 (64 lanes per leaf position): the leaf's work items (the last
-// query tile's item marked narrow when it has 16 slots), the empty query
-// slots of its last query tile, and the start of every scan wave whose share
-// begins inside this leaf.
+// Phase 2 (64 lanes per leaf position): the leaf's work items (16-slot query
+// tiles marked narrow), each with its query tile's leaf slots, and the start
+// of every scan wave whose share begins inside this leaf.
 // (item0 = the leaf's first item, [ua, ub) = its units, gunits = the 8
 // groups' unit boundaries)
 __device__ void ItemsCore(const WorklistArgs& w, int p, int lane, const uint32_t* gunits,
