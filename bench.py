@@ -202,20 +202,31 @@ def scan_roofline(code_bytes, scan_ms, timings, num_blocks):
     }
 
 
+def kernel_source_sha():
+    """sha256 of scann_amd/csrc/smx_kernels.hip with // and /* */ comments and
+    all blank space removed: the code a traffic record was measured on."""
+    import hashlib
+    import re
+    with open(os.path.join(ROOT, "scann_amd", "csrc", "smx_kernels.hip")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    src = re.sub(r"\s+", "", src)
+    return hashlib.sha256(src.encode()).hexdigest()
+
+
 def scan_traffic(config):
     """HBM read bytes per scan launch from this config's own PMC FETCH_SIZE
     pass (tools/profile_bench.sh -> tools/pmc_traffic.py ->
     profiles/scan_traffic_<config>.json), only when it was measured on the
     same kernel source; None otherwise."""
-    import hashlib
     tpath = os.path.join(ROOT, "profiles", f"scan_traffic_{config}.json")
     if not os.path.exists(tpath):
         return None
     with open(tpath) as f:
         tr = json.load(f)
-    with open(os.path.join(ROOT, "scann_amd", "csrc", "smx_kernels.hip"), "rb") as f:
-        if hashlib.sha256(f.read()).hexdigest() != tr.get("smx_kernels_sha256"):
-            return None
+    if kernel_source_sha() != tr.get("smx_kernels_code_sha256"):
+        return None
     return tr["hbm_read_bytes_per_launch"]
 
 

@@ -6,7 +6,8 @@ profiles/scan_traffic_<config>.json (bench.py --config <config>).
 FETCH_SIZE is in KiB and, on gfx950, reads exactly half of the bytes of a
 wide coalesced streaming read (MI355X_MICROARCH.md, HBM section), so the
 per-launch HBM read traffic is 2 * FETCH_SIZE * 1024 bytes.  The file records
-the sha256 of smx_kernels.hip so bench.py only reports it for the same kernel.
+the sha256 of smx_kernels.hip's code (comments stripped) so bench.py only
+reports it for the same kernel.
 """
 import csv
 import hashlib
@@ -19,8 +20,11 @@ KERNEL = "lut16_scan_kernel"
 
 
 def kernel_sha():
-    with open(os.path.join(ROOT, "scann_amd", "csrc", "smx_kernels.hip"), "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()
+    """sha256 of smx_kernels.hip with its comments and blank space removed (a
+    comment edit does not make a traffic record stale; any code change does)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench.kernel_source_sha()
 
 
 def main(path, config="glove"):
@@ -36,7 +40,7 @@ def main(path, config="glove"):
     res = dict(kernel=KERNEL, config=config, launches=len(vals), fetch_size_kib_avg=avg_kib,
                hbm_read_bytes_per_launch=2.0 * avg_kib * 1024.0,
                correction="x2: gfx950 FETCH_SIZE counts half of wide coalesced reads",
-               source=os.path.relpath(path, ROOT), smx_kernels_sha256=kernel_sha())
+               source=os.path.relpath(path, ROOT), smx_kernels_code_sha256=kernel_sha())
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))
