@@ -2040,7 +2040,10 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
 // 16-byte lane records of rows r and r + 16 of half gA >> 1 (`ca`, `cb`),
 // shifted right by 8 (gA & 1) bits, so that step s' reads byte 2 (s' % 2) of
 // dword s' / 2.  The same operand tables as the 32-slot path.
-template <int K, int R>
+#ifndef SMX_POS16_B64
+#define SMX_POS16_B64 0
+#endif
+template <int K, int R, bool NOLDS = false>
 __device__ __forceinline__ void TileSmfmac16(const uint32_t* ca, const uint32_t* cb,
                                              const v8i (&b)[(K + 3) / 4], const v4i* grp_tab,
                                              const int* pos_tab, v4i& acc_a, v4i& acc_b) {
@@ -2051,6 +2054,12 @@ __device__ __forceinline__ void TileSmfmac16(const uint32_t* ca, const uint32_t*
   auto ld = [&](int slot, int t) {
     const int st = t >> 1;
     const uint32_t w = (t & 1) ? cb[st >> 1] : ca[st >> 1];
+    if constexpr (NOLDS) {   // (timing ablation, results invalid: as TileSmfmac's)
+      const int x = int((st & 1) ? (w >> 16) : w);
+      o[slot] = v4i{x & 0x00010001, 0, x & 0x01000100, 0};
+      ix[slot] = x;
+      return;
+    }
     uint32_t og, op;
 #define SMX_SDWA_OFFS16(B)                                                                      \
   asm("v_lshlrev_b32_sdwa %0, 4, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD "        \
@@ -2064,7 +2073,13 @@ __device__ __forceinline__ void TileSmfmac16(const uint32_t* ca, const uint32_t*
     }
 #undef SMX_SDWA_OFFS16
     o[slot] = *reinterpret_cast<const v4i*>(reinterpret_cast<const char*>(grp_tab) + og);
+#if SMX_POS16_B64
+    // (as TileSmfmac's SMX_POS_B64: conflict-free b64 banks, one v_or more)
+    const uint2 pw = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(pos_tab) + op);
+    ix[slot] = int(pw.x | pw.y);
+#else
     ix[slot] = *reinterpret_cast<const int*>(reinterpret_cast<const char*>(pos_tab) + op);
+#endif
   };
 #pragma unroll
   for (int p = 0; p < R; ++p)
@@ -2092,6 +2107,17 @@ __device__ __forceinline__ void TileSmfmac16(const uint32_t* ca, const uint32_t*
     if (t + R < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
   }
 }
+
+// f(integral_constant<I>), ..., f(integral_constant<D - 1>): the ring slots of
+// the 16-slot scan, unrolled (each slot's registers fixed at compile time)
+template <int I, int D, class F>
+__device__ __forceinline__ void EachSlot(F& f) {
+  f(std::integral_constant<int, I>{});
+  if constexpr (I + 1 < D) EachSlot<I + 1, D>(f);
+}
+#ifndef SMX_RING16
+#define SMX_RING16 0   // 0: 4 tiles in flight per wave at <= 3 code dwords per lane, else 3
+#endif
 
 // ---------------------------------------------------------------------------
 // The scan kernel: one workgroup of kScanWaves waves per CU (3 per SIMD), the
@@ -2149,6 +2175,9 @@ template <int K>
 constexpr int ScanWaves() { return K <= 26 ? SMX_SCAN_WAVES : 8; }
 #ifndef SMX_SCAN_R
 #define SMX_SCAN_R 2
+#endif
+#ifndef SMX_SCAN_R16
+#define SMX_SCAN_R16 2
 #endif
 
 // Diagnostic stamps (ABL & 8; a separate buffer that nothing else reads):
@@ -2641,7 +2670,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
             sb[i] = cd_b[i] >> sh;
           }
           v4i acc_a, acc_b;
-          TileSmfmac16<K, R>(sa, sb, b, grp_tab, pos_tab, acc_a, acc_b);
+          TileSmfmac16<K, SMX_SCAN_R16, (ABL & 64) != 0>(sa, sb, b, grp_tab, pos_tab, acc_a, acc_b);
           if (ABL & 4) {
             int x = acc_a[0] ^ acc_b[0];
 #pragma unroll
@@ -2739,7 +2768,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         // pair, then the pair claimed ahead); every refill issues its load
         // unconditionally (the last tile again at the end), so the wait for a
         // slot's codes leaves the later slots' loads in flight.
-        constexpr int D = NW <= 3 ? 4 : 3;
+        constexpr int D = SMX_RING16 > 0 ? SMX_RING16 : (NW <= 3 ? 4 : 3);
         uint32_t cur = j, pe = min(j + 2, end), na = end;
         uint32_t na_raw = claim2(sg);
         bool na_known = false;
@@ -2808,10 +2837,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
           drain_mid();
         };
         for (;;) {
-          step(std::integral_constant<int, 0>{});
-          step(std::integral_constant<int, 1>{});
-          step(std::integral_constant<int, 2>{});
-          if constexpr (D > 3) step(std::integral_constant<int, 3>{});
+          EachSlot<0, D>(step);
           if (!ok[0]) break;
         }
       } else {
@@ -3971,35 +3997,32 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
 // 16: results invalid) and the per-segment stamps (8) exist in the
 // diagnostic build (-DSMX_SCAN_DIAGNOSTICS, tools/tune.py / scan_stamps.py).
 #ifdef SMX_SCAN_DIAGNOSTICS
+#define SMX_SCAN_VARIANT(KV, V)                                                            \
+  if (narrow == kNarrowOnly)                                                               \
+    hipLaunchKernelGGL((lut16_scan_kernel<KV, V, int(kNarrowOnly)>), dim3(grid),           \
+                       dim3(64 * ScanWaves<KV>()), 0, s, a);                               \
+  else                                                                                     \
+    hipLaunchKernelGGL((lut16_scan_kernel<KV, V>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
+                       0, s, a);
 #define SMX_SCAN_CASE(KV)                                                                  \
   case KV:                                                                                 \
-    if (variant == 16)                                                                     \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 16>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
-                         0, s, a);                                                         \
-    else if (variant == 2)                                                                 \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 2>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
-                         0, s, a);                                                         \
-    else if (variant == 4)                                                                 \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 4>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
-                         0, s, a);                                                         \
-    else if (variant == 8)                                                                 \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 8>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
-                         0, s, a);                                                         \
-    else if (variant == 32)                                                                \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 32>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
-                         0, s, a);                                                         \
-    else if (variant == 64)                                                                \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 64>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
-                         0, s, a);                                                         \
-    else if (variant == 68)                                                                \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 68>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
-                         0, s, a);                                                         \
-    else if (narrow == kNarrowOnly)                                                        \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, int(kNarrowOnly)>), dim3(grid),         \
-                         dim3(64 * ScanWaves<KV>()), 0, s, a);                             \
-    else                                                                                   \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
-                         0, s, a);                                                         \
+    if (variant == 16) {                                                                   \
+      SMX_SCAN_VARIANT(KV, 16)                                                             \
+    } else if (variant == 2) {                                                             \
+      SMX_SCAN_VARIANT(KV, 2)                                                              \
+    } else if (variant == 4) {                                                             \
+      SMX_SCAN_VARIANT(KV, 4)                                                              \
+    } else if (variant == 8) {                                                             \
+      SMX_SCAN_VARIANT(KV, 8)                                                              \
+    } else if (variant == 32) {                                                            \
+      SMX_SCAN_VARIANT(KV, 32)                                                             \
+    } else if (variant == 64) {                                                            \
+      SMX_SCAN_VARIANT(KV, 64)                                                             \
+    } else if (variant == 68) {                                                            \
+      SMX_SCAN_VARIANT(KV, 68)                                                             \
+    } else {                                                                               \
+      SMX_SCAN_VARIANT(KV, 0)                                                              \
+    }                                                                                      \
     break;
 #else
 #define SMX_SCAN_CASE(KV)                                                                  \

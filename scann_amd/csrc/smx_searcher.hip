@@ -568,7 +568,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   // tiles, SMX_NARROW=0 32-slot tiles (the tests run every mode).
   const uint64_t qpl_x = uint64_t(nq) * uint64_t(L);   // queries per leaf x nl
   uint32_t narrow = 0;
-  if (h->narrow_tiles && variant == 0 &&
+  if (h->narrow_tiles &&
       (h->narrow_only || qpl_x < uint64_t(smx::kNarrowQueriesPerLeaf) * uint64_t(ix.nl)))
     narrow = smx::kNarrowOnly;
   smx::Bounds bd;
@@ -987,6 +987,14 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
     h->narrow_only = nw[0] == '2';
   }
   if (const char* sw = std::getenv("SMX_SERIAL_WORKLIST")) h->serial_worklist = sw[0] != '0';
+#ifdef SMX_SCAN_DIAGNOSTICS
+  // a timing ablation for a whole process (tools: the shard configurations'
+  // bench lines under the timing library; see smx::LaunchScan)
+  if (const char* sv = std::getenv("SMX_SCAN_VARIANT")) {
+    const int v = std::atoi(sv);
+    if (v == 2 || v == 4 || v == 16 || v == 32 || v == 64 || v == 68) h->scan_variant = v;
+  }
+#endif
   // tuning knobs for A/Bs (the defaults otherwise; smx_set_tuning overrides)
   if (const char* ct = std::getenv("SMX_CHUNK_TILES")) {
     const int v = std::atoi(ct);

@@ -31,6 +31,8 @@ constexpr int TILES = 4096;
 // MODE 2: as 1 with two accumulators (tile t+1's chain beside tile t's test)
 // MODE 3: as 1 with the operands read from the scan's two 16-entry LDS
 //         tables by random code bytes (3 reads in flight), as in the scan
+// MODE 4: v_smfmac_i32_16x16x128_i8 (the 16-slot tiles), two chains in turn
+//         as in the 16-slot scan, operands in registers (one long chain)
 template <int MODE>
 __global__ void __launch_bounds__(768) rate(const int* __restrict__ rnd, long long* cycles,
                                             int* sink) {
@@ -81,6 +83,17 @@ __global__ void __launch_bounds__(768) rate(const int* __restrict__ rnd, long lo
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) codes[q] = codes[q] * 1664525u + 1013904223u;
+    } else if (MODE == 4) {
+      v4i acc_a = {acc[0], acc[1], acc[2], acc[3]}, acc_b = {acc[4], acc[5], acc[6], acc[7]};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        acc_a = __builtin_amdgcn_smfmac_i32_16x16x128_i8(a, b[s], acc_a, ix, 0, 0);
+        // (chain B on other B fragments: identical chains would be merged)
+        acc_b = __builtin_amdgcn_smfmac_i32_16x16x128_i8(a, b[KS - 1 - s], acc_b, ix, 0, 0);
+        a[0] += 0x00010000;
+      }
+      acc[0] = acc_a[0]; acc[1] = acc_a[1]; acc[2] = acc_a[2]; acc[3] = acc_a[3];
+      acc[4] = acc_b[0]; acc[5] = acc_b[1]; acc[6] = acc_b[2]; acc[7] = acc_b[3];
     } else {
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
@@ -127,10 +140,11 @@ void run(const int* d_rnd, int waves_per_simd, const char* name) {
   CHECK(hipMemcpy(h, d, sizeof(long long) * nw, hipMemcpyDeviceToHost));
   double m = 0;
   for (int i = 0; i < nw; ++i) m += double(h[i]) / nw;
-  const double per = m / (double(TILES) * KS);
+  const int per_tile = MODE == 4 ? 2 * KS : KS;   // smfmacs per tile
+  const double per = m / (double(TILES) * per_tile);
   // wall: the smfmacs of a CU's waves over its 4 SIMDs, at the in-kernel clock
-  const double per_simd_smfmac = double(TILES) * KS * waves_per_simd;
-  const double wall_cyc = m / (double(TILES) * KS) / waves_per_simd;   // memtime basis
+  const double per_simd_smfmac = double(TILES) * per_tile * waves_per_simd;
+  const double wall_cyc = per / waves_per_simd;   // memtime basis
   printf("%-34s %d wave(s)/SIMD: %6.1f memtime cycles per smfmac per wave, %6.1f per SIMD; "
          "wall %.3f ms = %.2f ns per smfmac per SIMD (%.0f smfmac/SIMD)\n", name,
          waves_per_simd, per, wall_cyc, ms, ms * 1e6 / per_simd_smfmac, per_simd_smfmac);
@@ -150,6 +164,7 @@ int main() {
     run<0>(d_rnd, w, "chain, 13 random B");
     run<1>(d_rnd, w, "per-tile zero + min test");
     run<3>(d_rnd, w, "+ LDS operand tables (scan)");
+    run<4>(d_rnd, w, "16x16x128 chains A/B, 26 per tile");
   }
   return 0;
 }
