@@ -2040,9 +2040,6 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
 // 16-byte lane records of rows r and r + 16 of half gA >> 1 (`ca`, `cb`),
 // shifted right by 8 (gA & 1) bits, so that step s' reads byte 2 (s' % 2) of
 // dword s' / 2.  The same operand tables as the 32-slot path.
-#ifndef SMX_POS16_B64
-#define SMX_POS16_B64 0
-#endif
 template <int K, int R, bool NOLDS = false>
 __device__ __forceinline__ void TileSmfmac16(const uint32_t* ca, const uint32_t* cb,
                                              const v8i (&b)[(K + 3) / 4], const v4i* grp_tab,
@@ -2073,13 +2070,7 @@ __device__ __forceinline__ void TileSmfmac16(const uint32_t* ca, const uint32_t*
     }
 #undef SMX_SDWA_OFFS16
     o[slot] = *reinterpret_cast<const v4i*>(reinterpret_cast<const char*>(grp_tab) + og);
-#if SMX_POS16_B64
-    // (as TileSmfmac's SMX_POS_B64: conflict-free b64 banks, one v_or more)
-    const uint2 pw = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(pos_tab) + op);
-    ix[slot] = int(pw.x | pw.y);
-#else
     ix[slot] = *reinterpret_cast<const int*>(reinterpret_cast<const char*>(pos_tab) + op);
-#endif
   };
 #pragma unroll
   for (int p = 0; p < R; ++p)
