@@ -473,6 +473,8 @@ def main():
                                   o[0].data_ptr(), o[1].data_ptr(), o[2].data_ptr(),
                                   stream=ctypes.c_void_p(streams[k].cuda_stream))
 
+    enqueue_s = {}
+
     def timed_steps(fl):
         torch.cuda.synchronize()
         if dist is not None:
@@ -481,6 +483,7 @@ def main():
         t0 = time.perf_counter()
         for i in range(args.steps):
             step(i, fl=fl)
+        enqueue_s[fl] = time.perf_counter() - t0   # host time issuing the steps
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
@@ -498,6 +501,9 @@ def main():
         step(i)
     elapsed = timed_steps(n_fl)
     ms_per_step = elapsed * 1000.0 / args.steps
+    # host time spent issuing the timed steps (library calls, launches): when
+    # it nears ms_per_step the host, not the device, sets the rate
+    issue_ms = enqueue_s[n_fl] * 1000.0 / args.steps
     value = world * NQ * args.steps / elapsed
     # the same in-flight steps again with two HIP events around every scan
     # launch on its own stream (profiling mode 2: no synchronisation, the
@@ -586,6 +592,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "in_flight": n_fl,
+            "host_issue_ms_per_step": round(issue_ms, 4),
             "single_stream": ({"qps": round(world * NQ * args.steps / elapsed_1, 1),
                                "ms_per_step": round(elapsed_1 * 1000.0 / args.steps, 4)}
                               if elapsed_1 else None),
