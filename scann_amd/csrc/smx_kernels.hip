@@ -352,12 +352,16 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 // a serial norm loop over global memory (at 256 blocks, one wave per SIMD,
 // nothing else hides them).
 constexpr int kPartTile = 64, kPartChunk = 32, kPartFullDim = 128;
+#ifndef SMX_PART_BLOCKS
+#define SMX_PART_BLOCKS 1024
+#endif
+constexpr int kPartBlocks = SMX_PART_BLOCKS;   // grid size above which a block takes several center tiles
 
 template <int CHUNK>
 __global__ void __launch_bounds__(256) partition_scores_kernel(
     const float* __restrict__ queries, int nq, int dim, const float* __restrict__ centers,
     const float* __restrict__ cnorm, int nl, int metric, float* __restrict__ scores,
-    StateInit init) {
+    StateInit init, int ctiles) {
   constexpr bool kFull = CHUNK == kPartFullDim;   // dim <= CHUNK: one staging round
   {
     // the search's per-call state (no separate memset nodes); nothing in this
@@ -413,55 +417,97 @@ __global__ void __launch_bounds__(256) partition_scores_kernel(
     // returns 0, and dims past dim (the next row's) are masked below.  (Rows
     // by 128-byte runs, tid % 32 + 32 j, measured 8.7 us against 8.0 at
     // glove's 100 dims, 12.6 against 13.1 at SIFT's 128.)
+    // A block takes `ctiles` consecutive center tiles with its query tile
+    // staged once; the next center tile's loads are in flight (registers)
+    // while the MFMAs of the current one run (many leaves: 782 center tiles
+    // at configs[4]'s 50000).
     constexpr int kPer = kPartFullDim / 4;
     const int row = tid >> 2, sub = tid & 3;
-    const uint32_t qrows = uint32_t(min(kPartTile, nq - qt)), crows = uint32_t(min(kPartTile, nl - ct));
+    const uint32_t qrows = uint32_t(min(kPartTile, nq - qt));
     const auto qrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(queries + size_t(qt) * dim), 0, int(qrows * uint32_t(dim) * 4u), 0x00020000);
-    const auto crs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(centers + size_t(ct) * dim), 0, int(crows * uint32_t(dim) * 4u), 0x00020000);
     const int off = (row * dim + sub) * 4;
-    float qv[kPer], cv[kPer];
+    const int ct_first = blockIdx.y * ctiles * kPartTile;
+    const int ct_end = min(nl, ct_first + ctiles * kPartTile);
+    float cv[kPer];
+    auto load_c = [&](int ct) {
+      const uint32_t crows = uint32_t(min(kPartTile, nl - ct));
+      const auto crs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(centers + size_t(ct) * dim), 0, int(crows * uint32_t(dim) * 4u), 0x00020000);
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      qv[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(qrs, off + 16 * j, 0, 0));
-      cv[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(crs, off + 16 * j, 0, 0));
+      for (int j = 0; j < kPer; ++j)
+        cv[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(crs, off + 16 * j, 0, 0));
+    };
+    {
+      float qv[kPer];
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        qv[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(qrs, off + 16 * j, 0, 0));
+      load_c(ct_first);
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int d = sub + 4 * j;
+        qs[row][d] = d < dim ? -qv[j] : -0.0f;
+      }
     }
+    for (int cti = ct_first; cti < ct_end; cti += kPartTile) {
+      if (cti != ct_first) __syncthreads();   // the previous tile's operand reads are done
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const int d = sub + 4 * j;
-      qs[row][d] = d < dim ? -qv[j] : -0.0f;
-      cs[row][d] = d < dim ? __fmul_rn(cv[j], cscale) : 0.0f;
-    }
-    __syncthreads();
-    if (metric == 1) {
-      if (tid < kPartTile) {   // (-q)^2 = q^2; the zero padding adds +0
-        double s = 0.0;
-        for (int d0 = 0; d0 < dim; d0 += 16) {
-          float x[16];
-#pragma unroll
-          for (int u = 0; u < 16; ++u) x[u] = qs[tid][d0 + u];
-#pragma unroll
-          for (int u = 0; u < 16; ++u) s += double(x[u]) * double(x[u]);
-        }
-        qn[tid] = float(s);
+      for (int j = 0; j < kPer; ++j) {
+        const int d = sub + 4 * j;
+        cs[row][d] = d < dim ? __fmul_rn(cv[j], cscale) : 0.0f;
       }
       __syncthreads();
-    }
-    init_acc(acc);
-    // (steps by 16 dims: the zero padding up to 128 leaves acc unchanged, and
-    // the operand reads of 8 MFMAs go out together)
-    const int steps = (dim + 15) & ~15;
-    for (int s = 0; s < steps; s += 16) {
-      float av[8], bv[8];
+      if (cti + kPartTile < ct_end) load_c(cti + kPartTile);   // in flight beside the MFMAs
+      if (metric == 1 && cti == ct_first) {
+        if (tid < kPartTile) {   // (-q)^2 = q^2; the zero padding adds +0
+          double s = 0.0;
+          for (int d0 = 0; d0 < dim; d0 += 16) {
+            float x[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        av[u] = qs[qw + r][s + 2 * u + k];
-        bv[u] = cs[cw + r][s + 2 * u + k];
+            for (int u = 0; u < 16; ++u) x[u] = qs[tid][d0 + u];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) s += double(x[u]) * double(x[u]);
+          }
+          qn[tid] = float(s);
+        }
+        __syncthreads();
       }
+      const int c0t = cti + cw;
+      const int cbt = min(c0t + r, nl - 1);
+      if (metric == 1) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+        for (int i = 0; i < 16; ++i) {
+          const int rw = (i & 3) + 8 * (i >> 2) + 4 * k;
+          acc[i] = __fadd_rn(cnorm[cbt], qn[qw + rw]);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+      }
+      // (steps by 16 dims: the zero padding up to 128 leaves acc unchanged, and
+      // the operand reads of 8 MFMAs go out together)
+      const int steps = (dim + 15) & ~15;
+      for (int s = 0; s < steps; s += 16) {
+        float av[8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          av[u] = qs[qw + r][s + 2 * u + k];
+          bv[u] = cs[cw + r][s + 2 * u + k];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+      }
+      const int colt = c0t + r;
+      if (colt < nl) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int rw = q0 + (i & 3) + 8 * (i >> 2) + 4 * k;
+          if (rw < nq) scores[size_t(rw) * nl + colt] = acc[i];
+        }
+      }
     }
+    return;
   }
   for (int d0 = 0; !kFull && d0 < dim; d0 += CHUNK) {
     __syncthreads();
@@ -3875,13 +3921,19 @@ hipError_t LaunchPartitionTopL(const DeviceIndex& ix, const float* queries, int 
     hipLaunchKernelGGL(partition_scores_a8_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s,
                        queries, nq, ix.dim, ix.centers, ix.nl, ix.metric, scores, f.init);
   } else {
-    const dim3 grid((nq + kPartTile - 1) / kPartTile, (ix.nl + kPartTile - 1) / kPartTile);
-    if (ix.dim <= kPartFullDim)
+    const int qtiles = (nq + kPartTile - 1) / kPartTile, ctl = (ix.nl + kPartTile - 1) / kPartTile;
+    if (ix.dim <= kPartFullDim) {
+      // center tiles per block: one up to ~kPartBlocks blocks, then as many
+      // as keep the grid near it (two blocks per CU at a time, ~2 rounds)
+      const int per = std::max(1, (qtiles * ctl + kPartBlocks - 1) / kPartBlocks);
+      const dim3 grid(qtiles, (ctl + per - 1) / per);
       hipLaunchKernelGGL(partition_scores_kernel<kPartFullDim>, grid, dim3(256), 0, s, queries, nq,
-                         ix.dim, ix.centers, ix.cnorm, ix.nl, ix.metric, scores, f.init);
-    else
-      hipLaunchKernelGGL(partition_scores_kernel<kPartChunk>, grid, dim3(256), 0, s, queries, nq,
-                         ix.dim, ix.centers, ix.cnorm, ix.nl, ix.metric, scores, f.init);
+                         ix.dim, ix.centers, ix.cnorm, ix.nl, ix.metric, scores, f.init, per);
+    } else {
+      hipLaunchKernelGGL(partition_scores_kernel<kPartChunk>, dim3(qtiles, ctl), dim3(256), 0, s,
+                         queries, nq, ix.dim, ix.centers, ix.cnorm, ix.nl, ix.metric, scores, f.init,
+                         1);
+    }
   }
   // static LDS of the kernel besides the dynamic key buffers: the LUT build's
   // raw table and reduction (~5 KB) and the selection's words
