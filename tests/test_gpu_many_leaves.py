@@ -18,7 +18,7 @@ from scann_amd.index import TreeAHIndex
 pytestmark = pytest.mark.gpu
 
 
-def _random_index(nl, n, dim, metric, seed, dup=True):
+def _random_index(nl, n, dim, metric, seed, dup=True, nq=24):
     rng = np.random.default_rng(seed)
     centers = rng.standard_normal((nl, dim)).astype(np.float32)
     if dup:   # every center of the second half repeats one of the first half
@@ -37,7 +37,7 @@ def _random_index(nl, n, dim, metric, seed, dup=True):
                      residual=metric == 0, centers=centers, codebook=codebook,
                      leaf_offsets=offsets, leaf_members=ids, member_codes=codes,
                      num_datapoints=n, dataset=db)
-    q = rng.standard_normal((24, dim)).astype(np.float32)
+    q = rng.standard_normal((nq, dim)).astype(np.float32)
     return ix, q
 
 
@@ -45,6 +45,23 @@ def _random_index(nl, n, dim, metric, seed, dup=True):
 def native():
     from scann_amd import _native
     return _native
+
+
+@pytest.mark.parametrize("nl,metric,dim", [(20000, 0, 96), (50000, 1, 100), (5000, 1, 128)])
+def test_partition_scores_several_center_tiles_per_block(native, oracle, nl, metric, dim):
+    """Above 1024 64x64 tiles a partition block takes several consecutive
+    center tiles (its query tile staged once, the next center tile's loads in
+    flight; smx_kernels.hip partition_scores_kernel): 200 queries = 4 query
+    tiles, so 20000 / 50000 leaves give 2 / 4 center tiles per block (the last
+    block a partial run), 5000 leaves one (control).  Both metrics, dims with
+    and without 16-dim padding."""
+    ix, q = _random_index(nl, 2 * nl, dim, metric, seed=3 * nl + metric, nq=200)
+    n = native.NativeIndex(ix)
+    for L in (10, 100):
+        gl, gd = n.partition_topl(q, L)
+        ol, od = oracle.partition_topl(q, ix.centers, ix.metric, L)
+        np.testing.assert_array_equal(gl, ol)
+        np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
 
 
 @pytest.mark.parametrize("nl,metric", [(1000, 0), (2048, 1), (5000, 0), (10000, 1), (20000, 0),
