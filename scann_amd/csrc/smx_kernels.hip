@@ -2070,6 +2070,62 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
   return acc;
 }
 
+// The tile with a dense first step (K % 4 == 2 with nb <= 2 K - 2: glove's
+// 50 blocks): the last sparse step would carry two padding blocks, so
+// blocks 4 KS + h (KS = K/2 - 1; nibble x0 of code byte KS) go through one
+// v_mfma_i32_32x32x32_i8 with C = 0 -- A lane (r, h) = the one-hot row of its
+// block (a 16-entry LDS table), B lane (c, h) = that block's LUT row -- and
+// the KS sparse steps accumulate onto it: the same MFMA count, no accumulator
+// zeroing, no padded half step.
+template <int K, int R>
+__device__ __forceinline__ v16i TileSmfmacD(const uint32_t* codes, const v8i (&b)[K / 2 - 1],
+                                            const v4i& bd, const v4i* grp_tab, const int* pos_tab,
+                                            const v4i* hot_tab) {
+  constexpr int KS = K / 2 - 1;
+  v4i o[R];
+  int ix[R];
+  auto ld = [&](int slot, int t) {
+    const uint32_t w = codes[t >> 2];
+    uint32_t og, op;
+#define SMX_SDWA_OFFS(B)                                                                        \
+  asm("v_lshlrev_b32_sdwa %0, 4, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD "        \
+      "src1_sel:BYTE_" #B "\n\tv_and_b32_sdwa %1, %3, %2 dst_sel:DWORD dst_unused:UNUSED_PAD "   \
+      "src0_sel:DWORD src1_sel:BYTE_" #B                                                         \
+      : "=&v"(og), "=&v"(op) : "v"(w), "v"(0xF0u))
+    switch (t & 3) {
+      case 0: SMX_SDWA_OFFS(0); break;
+      case 1: SMX_SDWA_OFFS(1); break;
+      case 2: SMX_SDWA_OFFS(2); break;
+      default: SMX_SDWA_OFFS(3); break;
+    }
+#undef SMX_SDWA_OFFS
+    o[slot] = *reinterpret_cast<const v4i*>(reinterpret_cast<const char*>(grp_tab) + og);
+    ix[slot] = *reinterpret_cast<const int*>(reinterpret_cast<const char*>(pos_tab) + op);
+  };
+  // the dense step's one-hot row: x0 = ((by & 3) << 2) | ((by >> 4) & 3)
+  const uint32_t by = (codes[KS >> 2] >> (8 * (KS & 3))) & 0xFFu;
+  const uint32_t x0 = ((by & 3u) << 2) | ((by >> 4) & 3u);
+  const v4i hot = hot_tab[x0];
+#pragma unroll
+  for (int p = 0; p < R; ++p)
+    if (p < KS) ld(p, p);
+  v16i acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(hot, bd, v16i{}, 0, 0, 0);
+#pragma unroll
+  for (int st = 0; st < KS; ++st) {
+    acc = __builtin_amdgcn_smfmac_i32_32x32x64_i8(o[st % R], b[st], acc, ix[st % R], 0, 0);
+    if (st + R < KS) ld(st % R, st + R);
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, 2 * R + 1, 0);
+  __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // the dense step
+  __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // (the next tile's code load)
+#pragma unroll
+  for (int st = 0; st < KS; ++st) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if (st + R < KS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+  }
+  return acc;
+}
+
 // One tile of a 16-slot item: S[dp][q] for 32 datapoints x 16 queries on
 // v_smfmac_i32_16x16x128_i8, two accumulator chains (A: datapoints 0..15, B:
 // 16..31) of K16 = ceil(K / 4) steps of 8 AH blocks each.  Operand layout
@@ -2350,8 +2406,10 @@ struct LaneVal {
 
 // NRW: 0 = 32-slot items only, kNarrowOnly = 16-slot items only (one path
 // compiled into each kernel: fewer registers and less code).
-template <int K, int ABL = 0, int NRW = 0>
+template <int K, int ABL = 0, int NRW = 0, bool DN = false>
 __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(ScanArgs a) {
+  // DN: the dense-first tile (TileSmfmacD), 32-slot items only
+  static_assert(!DN || (K % 4 == 2 && NRW == 0), "dense-first tiles: K % 4 == 2, 32-slot");
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
   constexpr int W = 4 * NW;
   constexpr int Q = 32, KB = kItemKeys, NWAVES = ScanWaves<K>();
@@ -2361,9 +2419,10 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
   // the two operand tables in one 512-byte array at LDS 0 (256-aligned, the
   // largest alignment is placed first): group entries [0, 256), position
   // entries at 256 + 16 p, so both offsets fold into the ds_read's immediate
-  __shared__ __align__(256) v4i opnd_tab[32];
+  __shared__ __align__(256) v4i opnd_tab[48];
   v4i* const grp_tab = opnd_tab;
   int* const pos_tab = reinterpret_cast<int*>(opnd_tab + 16);
+  v4i* const hot_tab = opnd_tab + 32;   // one-hot rows (the dense-first step)
   __shared__ uint32_t s_item[kMaxSegs], s_end[kMaxSegs], s_next[kMaxSegs];
   __shared__ SegDesc s_desc[kMaxSegs];
   __shared__ uint32_t s_nseg, s_claim, s_sw, s_su;
@@ -2389,6 +2448,9 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
     // position nibble p0 | p1 << 2: p0 in index fields 0..7, p1 in 8..15
     pos_tab[4 * threadIdx.x] = int((threadIdx.x & 3u) * 0x5555u | ((threadIdx.x >> 2) * 0x5555u) << 16);
     pos_tab[4 * threadIdx.x + 1] = 0;   // the high half of the ds_read_b64
+    v4i hv = {0, 0, 0, 0};
+    hv[threadIdx.x >> 2] = int(1u << (8 * (threadIdx.x & 3u)));
+    hot_tab[threadIdx.x] = hv;
   }
   const uint32_t worker = blockIdx.x * NWAVES + wv;
   // this workgroup's share: `units` tiles from tile jfirst of item w on
@@ -2548,11 +2610,12 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       uint32_t tiles_done = 0;
       auto run_seg = [&](auto nr_tag) {
       constexpr bool NR = decltype(nr_tag)::value;
-      constexpr int KB_STEPS = NR ? (K + 3) / 4 : K / 2;   // B fragments (steps)
+      constexpr int KB_STEPS = NR ? (K + 3) / 4 : K / 2 - (DN ? 1 : 0);   // B fragments (steps)
       // this segment's B fragments and first tile: 32-slot, LUT rows
       // 4s + 2h, 4s + 2h + 1 of query c per sparse step; 16-slot, rows
       // 8s' + 2gB, 8s' + 2gB + 1 of query n = lane % 16 (gB = lane / 16)
       v8i b[KB_STEPS];
+      v4i bd = {};   // (DN) the dense step's B fragment
       uint32_t codes[NW] = {}, codes_b[NW] = {};
       // addresses as a wave-uniform base + a 32-bit lane offset (saddr
       // loads: no 64-bit per-lane pointers live across the tile loop); the
@@ -2572,6 +2635,9 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         const v8i* bp = reinterpret_cast<const v8i*>(lutb + size_t(boff));
 #pragma unroll
         for (int s2 = 0; s2 < KB_STEPS; ++s2) b[s2] = bp[(NR ? 4 : 2) * s2];
+        if constexpr (DN && !NR)   // the dense step's LUT row: block 4 (K/2 - 1) + h
+          bd = *reinterpret_cast<const v4i*>(lutb + size_t(lq * uint32_t(LutRows(K) * 16) +
+                                                           uint32_t(4 * (K / 2 - 1) + h) * 16u));
       };
       auto load_codes = [&](uint32_t t, uint32_t (&ca)[NW], uint32_t (&cbb)[NW]) {
         LoadCodes<K>(tile_ptr(t), ca);
@@ -2740,7 +2806,9 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
             append_hit(hit, hb, pk, jt);
           }
         } else {
-          v16i acc = TileSmfmac<K, R, (ABL & 64) != 0>(cd, b, grp_tab, pos_tab);
+          v16i acc;
+          if constexpr (DN) acc = TileSmfmacD<K, R>(cd, b, bd, grp_tab, pos_tab, hot_tab);
+          else acc = TileSmfmac<K, R, (ABL & 64) != 0>(cd, b, grp_tab, pos_tab);
           if (ABL & 4) {
             int x = acc[0];
 #pragma unroll
@@ -4039,6 +4107,25 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
 // The product library compiles the scan only; the timing ablations (2, 4,
 // 16: results invalid) and the per-segment stamps (8) exist in the
 // diagnostic build (-DSMX_SCAN_DIAGNOSTICS, tools/tune.py / scan_stamps.py).
+// The 32-slot scan of K = KV: the dense-first tile where the blocks fit it
+// (KV % 4 == 2, nb <= 2 KV - 2: glove's 50 blocks at KV = 26; SMX_DENSE_FIRST=0
+// for the all-sparse tile).
+template <int KV>
+void LaunchWide(const DeviceIndex& ix, const ScanArgs& a, int grid, hipStream_t s) {
+  if constexpr (KV % 4 == 2) {
+    static const bool on = [] {
+      const char* e = std::getenv("SMX_DENSE_FIRST");
+      return !(e && e[0] == '0');
+    }();
+    if (on && ix.nb <= 2 * KV - 2) {
+      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, 0, true>), dim3(grid), dim3(64 * ScanWaves<KV>()),
+                         0, s, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()), 0, s, a);
+}
+
 #ifdef SMX_SCAN_DIAGNOSTICS
 #define SMX_SCAN_VARIANT(KV, V)                                                            \
   if (narrow == kNarrowOnly)                                                               \
@@ -4063,8 +4150,10 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
       SMX_SCAN_VARIANT(KV, 64)                                                             \
     } else if (variant == 68) {                                                            \
       SMX_SCAN_VARIANT(KV, 68)                                                             \
-    } else {                                                                               \
+    } else if (narrow == kNarrowOnly) {                                                    \
       SMX_SCAN_VARIANT(KV, 0)                                                              \
+    } else {                                                                               \
+      LaunchWide<KV>(ix, a, grid, s);                                                      \
     }                                                                                      \
     break;
 #else
@@ -4075,8 +4164,7 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, int(kNarrowOnly)>), dim3(grid),         \
                          dim3(64 * ScanWaves<KV>()), 0, s, a);                             \
     else                                                                                   \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
-                         0, s, a);                                                         \
+      LaunchWide<KV>(ix, a, grid, s);                                                      \
     break;
 #endif
 
