@@ -104,7 +104,7 @@ CONFIGS = {
                                "50000 leaves, 8-way shard), batch=1000"),
 }
 CFG = CONFIGS["glove"]
-SWEEP_LEAVES = (10, 20, 30, 40, 50, 60, 70, 80, 100, 150)
+SWEEP_LEAVES = (10, 12, 15, 20, 30, 40, 50, 60, 70, 80, 100, 150)
 
 
 def scan_k(num_blocks):
@@ -404,7 +404,7 @@ def main():
         sys.exit(subprocess.call(plan[1], env=env))
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=1_183_514)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -423,6 +423,10 @@ def main():
                     help="skip the per-stage replay (stage_ms, the scan alone)")
     ap.add_argument("--in-flight", type=int, default=3,
                     help="query batches in flight (streams, one library workspace each)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak: every GPU searches its own 1000-query batches (value); strong: "
+                         "one 1000-query batch split over the GPUs, results all-gathered "
+                         "(value); the other mode is reported beside it when N > 1")
     args = ap.parse_args()
     global CFG, LEAVES, LEAVES_TO_SEARCH
     CFG = CONFIGS[args.config]
@@ -473,26 +477,42 @@ def main():
                                   o[0].data_ptr(), o[1].data_ptr(), o[2].data_ptr(),
                                   stream=ctypes.c_void_p(streams[k].cuda_stream))
 
-    enqueue_s = {}
+    enqueue_s, wall_s = {}, {}
 
-    def timed_steps(fl):
+    def timed_steps(fl, fn=None):
+        """K steps bracketed by barrier + synchronize; the elapsed time is
+        taken from HIP events (recorded on streams[0] after the bracket's
+        synchronize, every stream waiting on it, and after joining every
+        stream), so host jitter outside the device's work does not enter it;
+        the wall clock of the same bracket is kept beside it.  Max over
+        ranks."""
+        fn = fn or (lambda i: step(i, fl=fl))
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        e0.record(streams[0])
+        for st in streams[1:]:
+            st.wait_event(e0)
         for i in range(args.steps):
-            step(i, fl=fl)
+            fn(i)
+        for st in streams[1:]:
+            streams[0].wait_stream(st)
+        e1.record(streams[0])
         enqueue_s[fl] = time.perf_counter() - t0   # host time issuing the steps
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
-        el = time.perf_counter() - t0
+        wall = time.perf_counter() - t0
+        el = e0.elapsed_time(e1) * 1e-3
         if dist is not None:
-            tt = torch.tensor([el], dtype=torch.float64, device=dev)
+            tt = torch.tensor([el, wall], dtype=torch.float64, device=dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            el = float(tt.item())
+            el, wall = float(tt[0].item()), float(tt[1].item())
+        wall_s[fl] = wall
         return el
 
     # timed steps: eager launches of the pipeline kernels per step
@@ -500,6 +520,7 @@ def main():
     for i in range(max(args.warmup, n_fl)):
         step(i)
     elapsed = timed_steps(n_fl)
+    wall_ms_per_step = wall_s[n_fl] * 1000.0 / args.steps
     ms_per_step = elapsed * 1000.0 / args.steps
     # host time spent issuing the timed steps (library calls, launches): when
     # it nears ms_per_step the host, not the device, sets the rate
@@ -516,6 +537,53 @@ def main():
     scan_ms_fl, scan_launches = float(t_fl["scan_ms_mode2"]), int(t_fl["scan_launches"])
     # the same steps one at a time (one stream): the per-batch latency
     elapsed_1 = timed_steps(1) if n_fl > 1 and not args.no_latency else None
+
+    # strong scaling: rank 0's 1000-query batch split over
+    # the ranks by query_slice (SearchBatchedParallel's chunking,
+    # scann.cc:478-501, across GPUs), each slice searched on the step's
+    # stream and the slices' results all-gathered (RCCL), so every rank holds
+    # the whole batch's results; QPS = 1000 x K / max-rank time
+    strong = None
+    if world > 1 or args.scaling == "strong":
+        from scann_amd.distributed import SplitBatchSearcher, query_slice
+        q0d = qd if rank == 0 else torch.from_numpy(queries_for_rank(db.shape[1], 0)).to(dev)
+        b0, e0_ = query_slice(NQ, rank, world)
+        souts = [(torch.zeros((e0_ - b0, FINAL_NN), dtype=torch.int32, device=dev),
+                  torch.zeros((e0_ - b0, FINAL_NN), dtype=torch.float32, device=dev),
+                  torch.zeros(e0_ - b0, dtype=torch.int32, device=dev)) for _ in range(n_fl)]
+        gathered = [None] * n_fl
+
+        def strong_step(i):
+            k = i % n_fl
+            o = souts[k]
+
+            def search(qs):
+                nat.search_batched_device(qs.data_ptr(), int(qs.shape[0]), LEAVES_TO_SEARCH,
+                                          PRE_NN, FINAL_NN, True, o[0].data_ptr(),
+                                          o[1].data_ptr(), o[2].data_ptr(),
+                                          stream=ctypes.c_void_p(streams[k].cuda_stream))
+                return o
+
+            with torch.cuda.stream(streams[k]):
+                gathered[k] = SplitBatchSearcher(search, rank, world, None).search_batched(q0d)
+
+        for i in range(max(args.warmup, n_fl)):
+            strong_step(i)
+        el_s = timed_steps(n_fl, strong_step)
+        torch.cuda.synchronize()
+        strong = {"qps": round(NQ * args.steps / el_s, 1),
+                  "ms_per_step": round(el_s * 1000.0 / args.steps, 4),
+                  "queries_per_gpu": e0_ - b0,
+                  "parallelism": f"one {NQ}-query batch split over {world} GPU(s) by query_slice, "
+                                 f"results all-gathered"
+                                 + (" (RCCL all_gather_into_tensor)" if world > 1 else "")
+                                 + f", {n_fl} batches in flight"}
+        if rank == 0:
+            # the split result == the whole batch searched on one GPU (rank 0's
+            # weak-scaling batch is the same queries)
+            g = gathered[(args.steps - 1) % n_fl]
+            whole = outs[(args.steps - 1) % n_fl] if args.steps else outs[0]
+            strong["ids_equal_whole_batch"] = bool(torch.equal(g[0], whole[0]))
 
     # per-stage durations, each kernel alone: the same steps replayed one at
     # a time with HIP events recorded on the call's stream around every stage
@@ -566,20 +634,25 @@ def main():
 
     avg_scan_ms = float(np.mean(scan_ms))
     bytes_per_launch = float(np.mean(scan_bytes))
-    # the roofline of the scan launches of the timed region (in flight, each
-    # sharing the device with the other batches' kernels), and of the scan
-    # alone (serial replay) beside it
-    roof = scan_roofline(bytes_per_launch, scan_ms_fl, t_last, ix.num_blocks)
+    # the roofline of the scan kernel alone on the device (serial replay, HIP
+    # events around each scan launch: the duration rocprofv3 reports for one
+    # batch at a time, profiles/r06/prof_*_alone/), and beside it the launches
+    # of the timed region, which share the device with the other batches in
+    # flight (their duration is residency, not the kernel's own time)
+    roof = scan_roofline(bytes_per_launch, avg_scan_ms, t_last, ix.num_blocks)
     roof["avg_launch_ms_source"] = (
-        f"HIP events on each call's stream around every scan launch of a second timed pass "
-        f"of the same in-flight steps ({scan_launches} launches, {n_fl} batches in flight; "
-        f"{world * NQ * args.steps / elapsed_ev:.0f} QPS with the events)")
-    iso = scan_roofline(bytes_per_launch, avg_scan_ms, t_last, ix.num_blocks)
-    roof["isolated"] = {
-        "avg_launch_ms": iso["avg_launch_ms"], "achieved": iso["achieved"], "frac": iso["frac"],
-        "smfmac_pipe_frac": iso["smfmac_pipe_frac"],
-        "source": f"HIP events around the scan of {len(scan_ms)} calls replayed one at a time "
-                  f"(the kernel alone on the device)"}
+        f"HIP events on the call's stream around the scan of {len(scan_ms)} calls replayed one "
+        f"at a time (the kernel alone on the device)")
+    fl = scan_roofline(bytes_per_launch, scan_ms_fl, t_last, ix.num_blocks)
+    roof["in_flight"] = {
+        "avg_launch_ms": fl["avg_launch_ms"], "achieved": fl["achieved"], "frac": fl["frac"],
+        "smfmac_pipe_frac": fl["smfmac_pipe_frac"],
+        # scans resident at once on average: launch time x launches / elapsed
+        "scan_concurrency": round(scan_ms_fl * 1e-3 * args.steps / elapsed_ev, 3),
+        "source": f"HIP events on each call's stream around every scan launch of a second timed "
+                  f"pass of the same in-flight steps ({scan_launches} launches, {n_fl} batches "
+                  f"in flight, {world * NQ * args.steps / elapsed_ev:.0f} QPS with the events): "
+                  f"each launch shares the device with the other batches' kernels"}
     traffic = scan_traffic(args.config)
 
     if rank == 0:
@@ -596,6 +669,9 @@ def main():
             "single_stream": ({"qps": round(world * NQ * args.steps / elapsed_1, 1),
                                "ms_per_step": round(elapsed_1 * 1000.0 / args.steps, 4)}
                               if elapsed_1 else None),
+            "timing": "HIP events between the timed region's barrier + synchronize brackets "
+                      "(max over ranks); wall clock of the same brackets: "
+                      f"{wall_ms_per_step:.4f} ms/step",
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -610,7 +686,7 @@ def main():
             },
             "recall_at_10": round(recall, 4),
             "roofline": dict(roof, traffic=traffic,
-                             hbm_GBps_measured=(round(traffic / (scan_ms_fl * 1e-3) / 1e9, 1)
+                             hbm_GBps_measured=(round(traffic / (avg_scan_ms * 1e-3) / 1e9, 1)
                                                 if traffic else None)),
             "stage_ms": ({k: round(v, 4) for k, v in stage.items()} if not args.no_stages
                          else None),
@@ -621,6 +697,21 @@ def main():
             "candidates_max": t_last["max_candidates"],
             "candidates_mean": round(float(t_last["mean_candidates"]), 1),
         }
+        if strong is not None:
+            if args.scaling == "strong":
+                # the split batch is the line's value; the weak figures beside it
+                result["weak_scaling"] = {"qps": result["value"],
+                                          "ms_per_step": result["ms_per_step"],
+                                          "parallelism": result["config"]["parallelism"]}
+                result["value"] = strong["qps"]
+                result["ms_per_step"] = strong["ms_per_step"]
+                result["scaling"] = "strong"
+                result["config"]["batch"] = NQ
+                result["config"]["parallelism"] = strong["parallelism"]
+                result["strong_scaling"] = {k: v for k, v in strong.items()
+                                            if k not in ("qps", "ms_per_step", "parallelism")}
+            else:
+                result["strong_scaling"] = strong
         # full-size parity: oracle (ideal mode) on a query subset, ids must match
         from oracle import binding as oracle
         oracle.build()

@@ -174,11 +174,21 @@ int smx_search_batched(smx_index* index, const float* queries, int32_t nq,
  * when the stream reaches them (candidate-list overflow is handled on the
  * device).  Calls on different streams run concurrently (one workspace per
  * stream, up to 4; a fifth stream reuses the oldest one after waiting for
- * its work).  d_out_count may be NULL. */
+ * its work).  d_out_count may be NULL.  A batch of any size is accepted: it
+ * runs as sub-batches of at most 2^26 / num_leaves queries (the leaf-slot
+ * table's budget, 256 MB per stream), one after another on the stream.
+ * A stream passed here (or to the other *_device search calls) must stay
+ * valid until smx_release_stream(index, stream) or smx_index_destroy: the
+ * handle orders a later call on another stream after it. */
 int smx_search_batched_device(smx_index* index, const float* d_queries, int32_t nq,
                               int32_t dim, const smx_search_params* params,
                               uint32_t* d_out_idx, float* d_out_dist,
                               int32_t* d_out_count, void* stream);
+
+/* Waits for the work the handle enqueued on `stream` and frees that stream's
+ * workspace (no-op for a stream the handle has not searched on), after which
+ * the caller may destroy the stream.  NULL = the handle's own stream. */
+int smx_release_stream(smx_index* index, void* stream);
 
 /* Single-query search (ScannNumpy::Search / ScannInterface::Search,
  * scann_npy.cc, scann.cc; TreeAHHybridResidual::FindNeighborsImpl,

@@ -61,6 +61,7 @@ SIGNATURES = {
     "smx_lut16_leaf_scores": (ctypes.c_int, [_vp, _i32, _vp, _vp]),
     "smx_kth_threshold_keys": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp]),
     "smx_set_profiling": (ctypes.c_int, [_vp, _i32]),
+    "smx_release_stream": (ctypes.c_int, [_vp, _vp]),
     "smx_get_timings": (ctypes.c_int, [_vp, ctypes.POINTER(Timings)]),
     "smx_set_tuning": (ctypes.c_int, [_vp, _i32, _i32, _i32, _i32]),
     "smx_shard_width": (ctypes.c_int, [_vp, ctypes.POINTER(SearchParams), ctypes.POINTER(_i32)]),
@@ -252,6 +253,11 @@ class NativeIndex:
                                                  out_idx_ptr, out_dist_ptr, out_count_ptr,
                                                  _current_stream(stream)),
               "Error during search")
+
+    def release_stream(self, stream=None):
+        """Waits for this handle's work on `stream` and frees its workspace
+        (smx_release_stream): the stream may then be destroyed."""
+        check(self.lib.smx_release_stream(self.h, _current_stream(stream)), "smx_release_stream")
 
     # -- range-split shards (SURVEY §8e(ii)); device pointers ----------------
     SHARD_ENTRY_BYTES = 16   # smx_shard_entry {u64 key; u32 id; f32 exact}

@@ -71,6 +71,9 @@ struct DeviceIndex {
   int ksteps = 0;        // ceil(nb / 2)
   int lane_bytes = 0;    // LaneBytes(ksteps)
   int shift = 0;         // global top-N shift, 0 = tie by global id
+  // the dense-first 32-slot scan tile where the blocks fit it (LaunchWide);
+  // set per handle at creation (SMX_DENSE_FIRST=0: the all-sparse tile)
+  bool dense_first = true;
   uint32_t num_datapoints = 0;
   uint64_t num_members = 0;
   uint64_t num_tiles = 0;
@@ -185,6 +188,7 @@ struct SeedArgs {
   uint64_t* tau_key;
   int L;
   int seed;
+  int seed_rows;              // rows scored per query (<= kSeedKeys)
   int kk;
   int residual;
   int nb;
@@ -289,6 +293,8 @@ struct MergeArgs {
   float* out_dist;
   int32_t* out_count;
   int out_width;
+  ShardEntry* out_entries;    // partial rounds of the wide merge (set by the launcher)
+  ShardEntry* scratch[2];     // the wide merge's round buffers (MergeScratchEntries each)
 };
 
 // ---- launchers (smx_kernels.hip) ------------------------------------------
@@ -389,6 +395,8 @@ hipError_t LaunchGatherResiduals(const float* x, int d, const uint32_t* rows, co
                                  const float* centers, int64_t m, int64_t row_base, float* out,
                                  hipStream_t s);
 hipError_t LaunchMergeShards(const MergeArgs& a, hipStream_t s);
+// Entries of each of the wide merge's two round buffers (0: none needed).
+size_t MergeScratchEntries(int world, int nq, int kk);
 hipError_t LaunchExactDistances(const DeviceIndex& ix, const float* queries, int nq,
                                 const uint32_t* ids, int k, float* out, hipStream_t s);
 hipError_t LaunchLeafScores(const DeviceIndex& ix, int leaf, const int8_t* lut,

@@ -1657,7 +1657,7 @@ __device__ __forceinline__ void LoadCodes(const uint8_t* p, uint32_t* codes) {
 // exact k'-th value.
 // ---------------------------------------------------------------------------
 #ifndef SMX_SEED_U
-#define SMX_SEED_U 4
+#define SMX_SEED_U 2
 #endif
 constexpr int kSeedPerThread = kSeedKeys / 256;
 constexpr uint32_t kSeedCap = 256u * kSeedPerThread;
@@ -1728,130 +1728,149 @@ __device__ uint32_t BlockRank256(uint64_t key, uint64_t* sbuf) {
   return r + b;
 }
 
-// The ranks below: counting ranks by default; SMX_SEED_BLOCKRANK=1 ranks the
-// minima and the compacted values with BlockRank256 (phase stamps: select p50
-// 7.4 -> 6.3 us, but no gain in the seed launch, whose end is set by its
-// slowest blocks: same-box A/B).
-#ifndef SMX_SEED_BLOCKRANK
-#define SMX_SEED_BLOCKRANK 0
-#endif
+// The k-th smallest (1-based, k <= 64) of the 64 lanes' values of one wave:
+// the answer's bits from the top, each by one ballot count (bit b is 1 when
+// fewer than k values lie at or below the prefix with bit b clear and every
+// lower bit set).  No LDS, no barrier; the loop is wave-uniform.
+__device__ __forceinline__ uint32_t WaveKth(uint32_t v, uint32_t k) {
+  uint32_t x = 0;
+  for (int b = 31; b >= 0; --b) {
+    const uint32_t t = x | ((1u << b) - 1u);
+    if (uint32_t(__popcll(__ballot(v <= t))) < k) x |= 1u << b;
+  }
+  return x;
+}
+
 // The threshold key of a query from its seed distances (ordered bits, 16
-// per thread of a 256-thread block, 0xFFFFFFFF = none): the exact kk-th
-// smallest value v as (v << 32 | 0xFFFFFFFF), which admits every candidate
-// at that distance.  Block-wide (every thread calls; the key is returned to
-// all).  kk <= 256: the kk-th of the 256 per-thread minima bounds the kk-th
-// value from above (a subset's kk-th is never smaller); the few values under
-// it (~1.3 kk) are ranked exactly.  Otherwise (or when those overflow),
-// rounds of a linear 256-bin histogram narrow the value range down.
+// per thread of a 256-thread block, 0xFFFFFFFF = none; the caller has
+// checked that at least kk values are real): (v << 32 | 0xFFFFFFFF) for v
+// the exact kk-th smallest value, which admits every candidate at that
+// distance.  Block-wide (every thread calls; the key is returned to all).
+// kk <= 256: each wave's ceil(kk/4)-th smallest per-thread minimum (WaveKth)
+// -- every wave then holds at least ceil(kk/4) values at or below it, so the
+// largest of the four bounds the kk-th value from above -- then the values
+// at or below that bound (~1.3-1.6 kk) compacted into LDS by ballot slots and
+// the exact kk-th of them found by wave 0 alone (WaveKthN).  Otherwise, or
+// when more than kSeedSel values pass the bound, the bits of the kk-th value
+// by block-wide ballot counts (one barrier per bit).  (Round 5: counting
+// ranks of the 256 minima and of the compacted keys, 7.2 us p50 per block.)
 __device__ uint64_t ThresholdOfVals(const uint32_t (&vals)[kSeedPerThread], uint32_t kk) {
-  __shared__ uint64_t skey[kSeedSel];
-  __shared__ uint32_t hist[256];
-  __shared__ uint32_t wsum[4], s_lo[4], s_hi[4], s_bin, s_below, s_thi, s_cnt;
-  __shared__ uint64_t s_T;
+  __shared__ uint32_t sval[kSeedSel];
+  __shared__ uint32_t s_wb[4], s_wc[2][4], s_cnt, s_x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if (tid == 0) s_cnt = 0;
-  __syncthreads();
   if (kk <= 256u) {
-    // The kk-th smallest of the 256 per-thread minima bounds the kk-th value
-    // from above (a subset's kk-th is never smaller); the few values under it
-    // (~1.3 kk) are compacted and the exact kk-th found by a counting rank
-    // over (value, number) keys.  Histogram rounds only when they overflow.
     uint32_t vmin = 0xFFFFFFFFu;
 #pragma unroll
     for (int i = 0; i < kSeedPerThread; ++i) vmin = min(vmin, vals[i]);
-    const uint64_t mk = (uint64_t(vmin) << 32) | uint32_t(tid);
-#if SMX_SEED_BLOCKRANK
-    if (BlockRank256(mk, skey) == kk - 1u) s_thi = vmin;
-#else
-    skey[tid] = mk;
+    const uint32_t wk = WaveKth(vmin, (kk + 3u) >> 2);
+    if (lane == 0) s_wb[wid] = wk;
+    if (tid == 0) s_cnt = 0;
     __syncthreads();
-    if (CountLess(skey, 256u, mk) == kk - 1u) s_thi = vmin;
-#endif
-    __syncthreads();
-    const uint32_t thi = s_thi;
+    const uint32_t thi = max(max(s_wb[0], s_wb[1]), max(s_wb[2], s_wb[3]));
+    // compaction: the wave's count by ballots, one LDS atomic per wave for
+    // its base, then the slots again by ballots (no per-value registers)
+    uint32_t n = 0;
 #pragma unroll
-    for (int i = 0; i < kSeedPerThread; ++i)
-      if (vals[i] <= thi) {
-        const uint32_t pos = atomicAdd(&s_cnt, 1u);
-        if (pos < uint32_t(kSeedSel)) skey[pos] = (uint64_t(vals[i]) << 32) | (uint32_t(tid) + 256u * i);
-      }
-    __syncthreads();
-    const uint32_t c = s_cnt;
-    if (SMX_SEED_BLOCKRANK && c <= 256u) {   // block rank of the compacted keys (the rest padded above them)
-      const uint64_t key = uint32_t(tid) < c ? skey[tid] : (~0ull << 16) | uint32_t(tid);
-      __syncthreads();   // skey is the rank's buffer
-      if (BlockRank256(key, skey) == kk - 1u) s_T = (key & 0xFFFFFFFF00000000ull) | 0xFFFFFFFFull;
-      __syncthreads();
-      return s_T;
-    }
-    if (c <= uint32_t(kSeedSel)) {
-      for (uint32_t i = tid; i < c; i += 256) {
-        const uint64_t key = skey[i];
-        if (CountLess(skey, c, key) == kk - 1u) s_T = (key & 0xFFFFFFFF00000000ull) | 0xFFFFFFFFull;
-      }
-      __syncthreads();
-      return s_T;
-    }
-  }
-  // range of the values, then histogram rounds down to the kk-th value
-  uint32_t lo = 0xFFFFFFFFu, hi = 0;
-#pragma unroll
-  for (int i = 0; i < kSeedPerThread; ++i)
-    if (vals[i] != 0xFFFFFFFFu) {
-      lo = min(lo, vals[i]);
-      hi = max(hi, vals[i]);
-    }
-  for (int off = 32; off > 0; off >>= 1) {
-    lo = min(lo, uint32_t(__shfl_xor(int(lo), off)));
-    hi = max(hi, uint32_t(__shfl_xor(int(hi), off)));
-  }
-  if (lane == 0) { s_lo[wid] = lo; s_hi[wid] = hi; }
-  __syncthreads();
-  lo = min(min(s_lo[0], s_lo[1]), min(s_lo[2], s_lo[3]));
-  hi = max(max(s_hi[0], s_hi[1]), max(s_hi[2], s_hi[3]));
-  uint32_t below = 0;   // values smaller than lo
-  while (lo < hi) {     // block-uniform; each round shrinks [lo, hi] ~256-fold
-    // bin = floor((v - lo) * scale / 2^32), scale = floor(255.99 * 2^32 / span):
-    // monotone, 0 at lo, <= 255 at hi, no division per value
-    const uint64_t scale = ((uint64_t(255) << 32) + 0xFFFFFFFFull) / uint64_t(hi - lo);
-    hist[tid] = 0;
-    __syncthreads();
+    for (int i = 0; i < kSeedPerThread; ++i) n += uint32_t(__popcll(__ballot(vals[i] <= thi)));
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&s_cnt, n);
+    base = uint32_t(__builtin_amdgcn_readfirstlane(int(base)));
 #pragma unroll
     for (int i = 0; i < kSeedPerThread; ++i) {
-      const uint32_t v = vals[i];
-      if (v >= lo && v <= hi) atomicAdd(&hist[uint32_t((uint64_t(v - lo) * scale) >> 32)], 1u);
+      const bool in = vals[i] <= thi;
+      const uint64_t m = __ballot(in);
+      const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi(
+                                      uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+      if (in && pos < uint32_t(kSeedSel)) sval[pos] = vals[i];
+      base += uint32_t(__popcll(m));
     }
     __syncthreads();
-    const uint32_t hv = hist[tid];
-    const uint32_t inc = BlockInclusiveScan256(hv, wsum);
-    if (below + inc - hv < kk && below + inc >= kk) {
-      s_bin = uint32_t(tid);
-      s_below = below + inc - hv;
+    const uint32_t c = s_cnt;
+    if (c <= uint32_t(kSeedSel)) {
+      // wave 0: the exact kk-th of the c compacted values, 4 or 16 per lane
+      if (wid == 0) {
+        uint32_t x = 0;
+        const int per = c <= 256u ? 4 : kSeedSel / 64;
+        for (int b = 31; b >= 0; --b) {
+          const uint32_t t = x | ((1u << b) - 1u);
+          uint32_t cnt = 0;
+          for (int i = 0; i < per; ++i) {
+            const uint32_t j = uint32_t(lane) + 64u * uint32_t(i);
+            cnt += uint32_t(__popcll(__ballot(j < c && sval[j] <= t)));
+          }
+          if (cnt < kk) x |= 1u << b;
+        }
+        if (lane == 0) s_x = x;
+      }
+      __syncthreads();
+      return (uint64_t(s_x) << 32) | 0xFFFFFFFFull;
     }
-    __syncthreads();
-    const uint32_t b = s_bin;
-    below = s_below;
-    BinRange(b, scale, lo, hi);
-    __syncthreads();   // hist, wsum and s_bin are rewritten by the next round
   }
-  if (tid == 0) s_T = (uint64_t(hi) << 32) | 0xFFFFFFFFull;
-  __syncthreads();
-  return s_T;
+  // the bits of the kk-th value by block-wide counts (s_wc double-buffered by
+  // the bit's parity: a wave rewrites one only after the next barrier, which
+  // every wave reaches after reading it)
+  uint32_t x = 0;
+  for (int b = 31; b >= 0; --b) {
+    const uint32_t t = x | ((1u << b) - 1u);
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int i = 0; i < kSeedPerThread; ++i) cnt += uint32_t(__popcll(__ballot(vals[i] <= t)));
+    if (lane == 0) s_wc[b & 1][wid] = cnt;
+    __syncthreads();
+    const uint32_t tot = s_wc[b & 1][0] + s_wc[b & 1][1] + s_wc[b & 1][2] + s_wc[b & 1][3];
+    if (tot < kk) x |= 1u << b;
+  }
+  return (uint64_t(x) << 32) | 0xFFFFFFFFull;
+}
+
+// Seed scoring tables: per code byte j of half h two 64-entry byte tables,
+// each indexed by six bits of the byte and holding one block's LUT entry
+// biased by +128 (EncodeCodePair: bits 0-1 = g0, 2-3 = g1, 4-5 = p0, 6-7 =
+// p1 for the blocks x0 = 4j + h = 4 g0 + p0 and x1 = 4j + 2 + h = 4 g1 + p1):
+//   lo table, index byte & 0x3F = g0 | g1 << 2 | p0 << 4 -> LUT[x0];
+//   hi table, index byte >> 2   = g1 | p0 << 2 | p1 << 4 -> LUT[x1];
+// in both, entry i = LUT[4 (i & 3) + ((i >> 4) & 3)].  A table is 16 dwords
+// in 16 distinct banks and every lane of one read uses the same table, so
+// the reads are conflict-free: 2 LDS cycles per lookup, two lookups per code
+// byte.  (Round 5's 256-entry int16 byte-pair tables: one lookup per byte
+// but ~2.8-way bank conflicts of the random 16-bit reads -- 5.6 cycles per
+// byte; 40% of the seed's LDS-active cycles were conflicts.)
+template <int K>
+__device__ __forceinline__ uint32_t SeedRowSum(const uint8_t* ntab, const uint32_t* c0,
+                                               const uint32_t* c1) {
+  constexpr int NB = (K + 1) / 2;
+  uint32_t acc = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t* c = h ? c1 : c0;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const uint32_t w = c[j >> 2];
+      const uint32_t lo = (w >> (8 * (j & 3))) & 0x3Fu;
+      const uint32_t hi = (w >> (8 * (j & 3) + 2)) & 0x3Fu;
+      const uint8_t* t = ntab + ((h * NB + j) * 2) * 64;
+      acc += uint32_t(t[lo]) + uint32_t(t[64 + hi]);
+    }
+  }
+  return acc;
 }
 
 // The threshold key of query qi from its seed leaves, or kNoThreshold (no
 // bound); block-wide (256 threads, all call; the value is returned to all).
+// Rows: the seed leaves' rows numbered across the leaves (a prefix sum of
+// their sizes), at most a.seed_rows (<= kSeedCap) of them; thread t scores
+// numbers t, t + 256, ...: groups of U rows whose code loads are issued one
+// group ahead of the scoring.
 template <int K>
 __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
   constexpr int NW = ((((K + 1) / 2) + 3) / 4);
   constexpr int W = 4 * NW;
-  constexpr int U = SMX_SEED_U;   // datapoints whose code loads are in flight together
+  constexpr int U = SMX_SEED_U;   // rows per group
+  constexpr int G = kSeedPerThread / U;
   constexpr int NB = (K + 1) / 2;   // code bytes per half holding steps < K
+  static_assert(kSeedPerThread % U == 0, "whole groups");
   __shared__ __align__(16) int8_t lut[2 * K * 16];
-  // pair tables: ptab[h][j][byte] = the LUT sum of the two nibbles of code
-  // byte j of half h (blocks 4j + h and 4j + 2 + h): one LDS lookup per code
-  // byte instead of one per nibble
-  __shared__ int16_t ptab[2 * NB * 256];
+  __shared__ __align__(16) uint8_t ntab[2 * NB * 2 * 64];
   __shared__ uint32_t s_start[kSeedMaxLeaves + 1];
   __shared__ uint64_t s_tile0[kSeedMaxLeaves];
   __shared__ float s_bias[kSeedMaxLeaves];
@@ -1880,51 +1899,71 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
   }
   __syncthreads();
   SMX_PHASE(1, qi, 1);
-  const uint32_t total = min(s_start[kSeedMaxLeaves], kSeedCap);
+  const uint32_t total = min(s_start[kSeedMaxLeaves], min(uint32_t(a.seed_rows), kSeedCap));
   const uint32_t kk = uint32_t(a.kk);
   if (kk == 0 || total < kk) return kNoThreshold;   // no bound: the threshold stays open
-#pragma unroll
-  for (int i = 0; i < 2 * NB; ++i) {
-    const int h = i / NB, j = i % NB, s0 = 2 * j, s1 = 2 * j + 1;
-    int v = lut[(2 * s0 + h) * 16 + CodePairLo(uint32_t(tid))];
-    if (s1 < K) v += lut[(2 * s1 + h) * 16 + CodePairHi(uint32_t(tid))];
-    ptab[i * 256 + tid] = int16_t(v);
+  // the tables, one dword (four entries) per store: table tb = (h, j, part),
+  // entries i0..i0+3 share (i >> 4) & 3 = p and take LUT[4 k + p], k = 0..3
+  for (int d = tid; d < 2 * NB * 2 * 16; d += 256) {
+    const int tb = d >> 4, i0 = (d & 15) * 4, p = (i0 >> 4) & 3;
+    const int hj = tb >> 1, part = tb & 1, h = hj / NB, j = hj % NB;
+    const int s = 2 * j + part;   // MFMA step: LUT row 2 s + h = block 4 j + 2 part + h
+    uint32_t word = 0x80808080u;  // zero rows (steps >= K) biased
+    if (s < K) {
+      const int8_t* row = lut + (2 * s + h) * 16 + p;
+      word = (uint32_t(uint8_t(row[0] ^ 0x80))) | (uint32_t(uint8_t(row[4] ^ 0x80)) << 8) |
+             (uint32_t(uint8_t(row[8] ^ 0x80)) << 16) | (uint32_t(uint8_t(row[12] ^ 0x80)) << 24);
+    }
+    reinterpret_cast<uint32_t*>(ntab)[d] = word;
   }
+  // the leaf boundaries as uniform values (the common seed of <= 4 leaves;
+  // more leaves take the LDS walk)
+  const uint32_t st1 = s_start[1], st2 = s_start[2], st3 = s_start[3];
   __syncthreads();
 
+  // row -> its code bytes (both halves) and its leaf
+  auto row_ptr = [&](uint32_t g, int& r) -> const uint8_t* {
+    if (nseed <= 4) {
+      r = (g >= st1 ? 1 : 0) + (g >= st2 ? 1 : 0) + (g >= st3 ? 1 : 0);
+      r = min(r, nseed - 1);
+    } else {
+      while (g >= s_start[r + 1]) ++r;
+    }
+    const uint32_t dp = g - s_start[r];
+    SMX_CHECK(s_tile0[r] + (dp >> 5), a.bd.tiles, "seed tile");
+    return a.tiles + ((s_tile0[r] + (dp >> 5)) * 64 + (dp & 31)) * W;
+  };
+  constexpr uint32_t kBias = 2u * NB * 2u * 128u;   // the tables' +128 per lookup
   uint32_t vals[kSeedPerThread];
+  uint32_t cb[2][U][2 * NW];   // code words of two groups (double buffer)
+  int rb[2][U];
   int r = 0;   // seed leaf of this thread's current number (numbers only grow)
+  auto load = [&](int g0, int buf) {
 #pragma unroll
-  for (int i0 = 0; i0 < kSeedPerThread; i0 += U) {
-    if (uint32_t(i0) * 256u < total) {   // block-uniform
-      uint32_t c0[U][NW], c1[U][NW];
-      int ru[U];
+    for (int u = 0; u < U; ++u) {
+      const uint32_t g = min(uint32_t(tid) + 256u * uint32_t(g0 * U + u), total - 1);
+      const uint8_t* t0 = row_ptr(g, r);
+      rb[buf][u] = r;
+      LoadCodes<K>(t0, cb[buf][u]);
+      LoadCodes<K>(t0 + 32 * W, cb[buf][u] + NW);
+    }
+  };
+  load(0, 0);
+#pragma unroll
+  for (int g0 = 0; g0 < G; ++g0) {
+    const int buf = g0 & 1;
+    if (uint32_t(g0) * U * 256u < total) {   // block-uniform
+      if (g0 + 1 < G && uint32_t(g0 + 1) * U * 256u < total) load(g0 + 1, buf ^ 1);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t g = min(uint32_t(tid) + 256u * uint32_t(i0 + u), total - 1);
-        while (g >= s_start[r + 1]) ++r;
-        ru[u] = r;
-        const uint32_t dp = g - s_start[r];
-        SMX_CHECK(s_tile0[r] + (dp >> 5), a.bd.tiles, "seed tile");
-        const uint8_t* t0 = a.tiles + ((s_tile0[r] + (dp >> 5)) * 64 + (dp & 31)) * W;
-        LoadCodes<K>(t0, c0[u]);
-        LoadCodes<K>(t0 + 32 * W, c1[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        int acc = 0;
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          const uint32_t b0 = (c0[u][j >> 2] >> (8 * (j & 3))) & 0xFFu;
-          const uint32_t b1 = (c1[u][j >> 2] >> (8 * (j & 3))) & 0xFFu;
-          acc += int(ptab[j * 256 + b0]) + int(ptab[(NB + j) * 256 + b1]);
-        }
-        const uint32_t g = uint32_t(tid) + 256u * uint32_t(i0 + u);
-        vals[i0 + u] = g < total ? OrderedBits(DistOf(acc, inv, s_bias[ru[u]])) : 0xFFFFFFFFu;
+        const int acc = int(SeedRowSum<K>(ntab, cb[buf][u], cb[buf][u] + NW)) - int(kBias);
+        const uint32_t g = uint32_t(tid) + 256u * uint32_t(g0 * U + u);
+        vals[g0 * U + u] =
+            g < total ? OrderedBits(DistOf(acc, inv, s_bias[rb[buf][u]])) : 0xFFFFFFFFu;
       }
     } else {
 #pragma unroll
-      for (int u = 0; u < U; ++u) vals[i0 + u] = 0xFFFFFFFFu;   // no datapoint
+      for (int u = 0; u < U; ++u) vals[g0 * U + u] = 0xFFFFFFFFu;   // no datapoint
     }
   }
   SMX_PHASE(1, qi, 2);
@@ -1946,7 +1985,7 @@ __device__ uint64_t SeedTau(const SeedArgs& a, int qi) {
 // measured slower: block 0 published its prefixes only 48.7 us after its
 // start beside the seed blocks -- tools/phase_stamps.py)
 template <int K>
-__global__ void __launch_bounds__(256) seed_tau_kernel(SeedArgs a, WorklistArgs w, int nq) {
+__global__ void __launch_bounds__(256, 4) seed_tau_kernel(SeedArgs a, WorklistArgs w, int nq) {
   const int qi = blockIdx.x;
   if (qi >= nq) {   // the fused work-list blocks
     WorklistFusedBlock(w, qi - nq);
@@ -3904,6 +3943,166 @@ __global__ void __launch_bounds__(256) merge_shards_kernel(MergeArgs a) {
   if (tid == 0 && a.out_count) a.out_count[qi] = int32_t(keep);
 }
 
+// ---------------------------------------------------------------------------
+// The merge for wide shard lists (k' up to 2048 per shard, world x k' up to
+// kMergeWideEntries per launch; a SOAR shard keeps k' = 2 x pre_reorder_nn,
+// tree_ah_hybrid_residual.h:263-267).  The same global rank as
+// merge_shards_kernel (position in its list + smaller keys of every other
+// list, equal keys by list), with dynamic LDS sized by the call.  kPartial:
+// block (query, group) merges the group's lists into one list of the k'
+// smallest entries (sorted by (key, list); padded with UINT64_MAX), so that
+// more lists than one launch holds merge in rounds -- the k' smallest of a
+// union are the k' smallest of its parts' k' smallest.  Otherwise the SOAR
+// de-duplication (tree_ah_hybrid_residual.cc:779-783: a datapoint's two copies
+// averaged 0.5a + 0.5b), the pre_reorder_nn cut by (distance, id) and the
+// final (distance, id) order, on bitonic sorts of up to 2048 keys.
+// ---------------------------------------------------------------------------
+constexpr int kMergeWideEntries = 8192;
+
+size_t MergeWideLds(int lists, int kk) {
+  uint32_t kkp2 = 1;
+  while (kkp2 < uint32_t(kk)) kkp2 <<= 1;
+  return size_t(lists) * size_t(kk) * 8 + size_t(kkp2) * (8 + 8 + 4 * 5);
+}
+
+template <bool kPartial>
+__global__ void __launch_bounds__(256) merge_shards_wide_kernel(MergeArgs a, int group_lists) {
+  extern __shared__ uint64_t mlds[];
+  __shared__ uint32_t cnt[64], s_c;
+  const int tid = threadIdx.x;
+  const int qi = blockIdx.x;
+  const int kk = a.kk;
+  const int w0 = int(blockIdx.y) * group_lists;
+  const int W = min(group_lists, a.world - w0);
+  const uint32_t kkp2 = NextPow2(uint32_t(kk));
+  uint64_t* lk = mlds;                          // [W * kk] the lists' keys
+  uint64_t* sel = lk + size_t(W) * kk;          // [kkp2] the kk smallest, by rank
+  uint64_t* aux = sel + kkp2;                   // [kkp2] sort keys
+  uint32_t* sid = reinterpret_cast<uint32_t*>(aux + kkp2);
+  float* sex = reinterpret_cast<float*>(sid + kkp2);
+  uint32_t* gid = reinterpret_cast<uint32_t*>(sex + kkp2);
+  float* dist = reinterpret_cast<float*>(gid + kkp2);
+  float* ex = dist + kkp2;
+  auto entry = [&](int w, int j) -> const ShardEntry& {
+    return a.entries[(size_t(w0 + w) * a.nq + qi) * kk + j];
+  };
+  for (int e = tid; e < W * kk; e += 256) lk[e] = entry(e / kk, e % kk).key;
+  if (tid == 0) s_c = 0;
+  __syncthreads();
+  for (int w = tid; w < W; w += 256) {   // valid entries: the padding sorts last
+    int lo = 0, hi = kk;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (lk[w * kk + mid] != ~0ull) lo = mid + 1; else hi = mid;
+    }
+    cnt[w] = uint32_t(lo);
+  }
+  __syncthreads();
+  for (int e = tid; e < W * kk; e += 256) {
+    const int w = e / kk, j = e % kk;
+    if (uint32_t(j) >= cnt[w]) continue;
+    const uint64_t key = lk[e];
+    uint32_t r = uint32_t(j);
+    for (int v = 0; v < W && r < uint32_t(kk); ++v) {
+      if (v == w) continue;
+      int lo = 0, hi = int(cnt[v]);
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const uint64_t x = lk[v * kk + mid];
+        if (x < key || (v < w && x == key)) lo = mid + 1; else hi = mid;
+      }
+      r += uint32_t(lo);
+    }
+    if (r < uint32_t(kk)) {
+      const ShardEntry& se = entry(w, j);
+      sel[r] = key;
+      sid[r] = se.id;
+      sex[r] = se.exact;
+    }
+  }
+  uint32_t total = 0;
+  for (int w = 0; w < W; ++w) total += cnt[w];
+  uint32_t m = min(total, uint32_t(kk));
+  __syncthreads();
+  if constexpr (kPartial) {
+    ShardEntry* out = a.out_entries + (size_t(blockIdx.y) * a.nq + qi) * kk;
+    for (uint32_t i = tid; i < uint32_t(kk); i += 256) {
+      ShardEntry e;
+      e.key = i < m ? sel[i] : ~0ull;
+      e.id = i < m ? sid[i] : 0u;
+      e.exact = i < m ? sex[i] : 0.0f;
+      out[i] = e;
+    }
+  } else {
+    for (uint32_t i = tid; i < m; i += 256) {
+      gid[i] = sid[i];
+      dist[i] = FromOrdered(uint32_t(sel[i] >> 32));
+      ex[i] = sex[i];
+    }
+    __syncthreads();
+    if (!a.disjoint) {
+      // copies of one datapoint next to each other: sort (gid << 32 | slot)
+      const uint32_t mp2 = NextPow2(max(m, 1u));
+      for (uint32_t i = tid; i < mp2; i += 256)
+        aux[i] = i < m ? ((uint64_t(gid[i]) << 32) | i) : ~0ull;
+      __syncthreads();
+      BitonicSort(aux, mp2);
+      // run starts: (ordered(averaged distance) << 32 | gid), the rest MAX;
+      // sex[i] = the exact distance of the run starting at sorted position i
+      for (uint32_t i = tid; i < mp2; i += 256) {
+        uint64_t o = ~0ull;
+        if (i < m) {
+          const uint32_t g = uint32_t(aux[i] >> 32);
+          if (i == 0 || uint32_t(aux[i - 1] >> 32) != g) {
+            const uint32_t s0 = uint32_t(aux[i] & 0xFFFFFFFFu);
+            float d = dist[s0];
+            if (i + 1 < m && uint32_t(aux[i + 1] >> 32) == g) {
+              const float d2 = dist[uint32_t(aux[i + 1] & 0xFFFFFFFFu)];
+              d = __fadd_rn(__fmul_rn(0.5f, d), __fmul_rn(0.5f, d2));
+            }
+            o = (uint64_t(OrderedBits(d)) << 32) | g;
+            sex[i] = ex[s0];
+            atomicAdd(&s_c, 1u);
+          }
+        }
+        sel[i] = o;
+      }
+      __syncthreads();
+      BitonicSort(sel, mp2);
+      const uint32_t mu = min(s_c, uint32_t(a.pre_nn));
+      // the kept datapoints by (averaged distance, id); each one's exact
+      // distance from its run start (binary search of the gid-sorted runs)
+      for (uint32_t r = tid; r < mu; r += 256) {
+        const uint32_t g = uint32_t(sel[r] & 0xFFFFFFFFu);
+        uint32_t lo = 0, hi = m;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (uint32_t(aux[mid] >> 32) < g) lo = mid + 1; else hi = mid;
+        }
+        gid[r] = g;
+        dist[r] = FromOrdered(uint32_t(sel[r] >> 32));
+        ex[r] = sex[lo];
+      }
+      __syncthreads();
+      m = mu;
+    }
+    // the final (distance, id) order of the kept m
+    const uint32_t mp2 = NextPow2(max(m, 1u));
+    for (uint32_t i = tid; i < mp2; i += 256)
+      aux[i] = i < m ? ((uint64_t(OrderedBits(a.reorder ? ex[i] : dist[i])) << 32) | gid[i]) : ~0ull;
+    __syncthreads();
+    BitonicSort(aux, mp2);
+    const uint32_t keep = min(m, uint32_t(a.out_width));
+    for (int i = tid; i < a.out_width; i += 256) {
+      const bool has = uint32_t(i) < keep;
+      a.out_idx[size_t(qi) * a.out_width + i] = has ? uint32_t(aux[i] & 0xFFFFFFFFu) : 0u;
+      a.out_dist[size_t(qi) * a.out_width + i] =
+          has ? FromOrdered(uint32_t(aux[i] >> 32)) : __int_as_float(0x7fc00000);
+    }
+    if (tid == 0 && a.out_count) a.out_count[qi] = int32_t(keep);
+  }
+}
+
 // Candidate-list statistics for the host loop (one block; no same-address
 // atomics from every query's block): [0] any list over capacity, [1] the
 // largest such count, [2] the largest count, [8] the sum of counts.
@@ -4113,11 +4312,7 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
 template <int KV>
 void LaunchWide(const DeviceIndex& ix, const ScanArgs& a, int grid, hipStream_t s) {
   if constexpr (KV % 4 == 2) {
-    static const bool on = [] {
-      const char* e = std::getenv("SMX_DENSE_FIRST");
-      return !(e && e[0] == '0');
-    }();
-    if (on && ix.nb <= 2 * KV - 2) {
+    if (ix.dense_first && ix.nb <= 2 * KV - 2) {
       hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, 0, true>), dim3(grid), dim3(64 * ScanWaves<KV>()),
                          0, s, a);
       return;
@@ -4274,12 +4469,42 @@ hipError_t LaunchKthKeys(const uint32_t* vals, int sets, int kk, uint64_t* out, 
   return hipGetLastError();
 }
 
+int MergeGroupLists(int kk) { return std::max(1, kMergeWideEntries / std::max(kk, 1)); }
+
 hipError_t LaunchMergeShards(const MergeArgs& a, hipStream_t s) {
   if (a.nq == 0) return hipSuccess;
-  if (a.world < 1 || a.world > 64 || a.kk > kSelMax || a.world * a.kk > kMergeMaxEntries)
-    return hipErrorInvalidValue;
-  hipLaunchKernelGGL(merge_shards_kernel, dim3(a.nq), dim3(256), 0, s, a);
+  if (a.world < 1 || a.world > 64 || a.kk < 1 || a.kk > 2048) return hipErrorInvalidValue;
+  if (a.kk <= kSelMax && a.world * a.kk <= kMergeMaxEntries) {
+    hipLaunchKernelGGL(merge_shards_kernel, dim3(a.nq), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
+  // wide lists: rounds of partial merges (groups of MergeGroupLists lists,
+  // ping-ponging through a.scratch[0/1]) down to one launch's worth
+  MergeArgs m = a;
+  const int gl = MergeGroupLists(a.kk);
+  int round = 0;
+  while (m.world > gl) {
+    const int groups = (m.world + gl - 1) / gl;
+    MergeArgs p = m;
+    p.out_entries = a.scratch[round & 1];
+    if (!p.out_entries) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(merge_shards_wide_kernel<true>, dim3(a.nq, groups), dim3(256),
+                       MergeWideLds(gl, a.kk), s, p, gl);
+    m.entries = p.out_entries;
+    m.world = groups;
+    ++round;
+  }
+  hipLaunchKernelGGL(merge_shards_wide_kernel<false>, dim3(a.nq, 1), dim3(256),
+                     MergeWideLds(m.world, a.kk), s, m, m.world);
   return hipGetLastError();
+}
+
+size_t MergeScratchEntries(int world, int nq, int kk) {
+  if (kk <= kSelMax && world * kk <= kMergeMaxEntries) return 0;
+  const int gl = MergeGroupLists(kk);
+  if (world <= gl) return 0;
+  const int groups = (world + gl - 1) / gl;   // the first round's output is the largest
+  return size_t(groups) * size_t(nq) * size_t(kk);
 }
 
 bool FinalSelectFits(const SelectArgs& a) {

@@ -89,7 +89,8 @@ struct Workspace {
   // allocated sizes, each the largest of its own quantity over past calls
   // (never a product of per-dimension maxima: nq = 10^4 at L = 20 followed
   // by nq = 10 at L = 2000 keeps 2 * 10^5 pairs, not 2 * 10^7)
-  int nq = 0, dim = 0;
+  int nq = 0, dim = 0;              // nq: queries of one sub-batch (RunSearch)
+  int sq = 0;                       // staged queries / outputs (whole host batch)
   size_t pairs = 0, cand_words = 0, out_words = 0;
   uint64_t gen = 0;                 // bumped on every (re)allocation
   uint32_t max_items = 0;
@@ -116,6 +117,8 @@ struct Workspace {
   uint32_t* out_idx = nullptr;
   float* out_dist = nullptr;
   int32_t* out_count = nullptr;
+  smx::ShardEntry* merge_scratch[2] = {nullptr, nullptr};   // the wide merge's rounds
+  size_t merge_entries = 0;
 
   void Release() {
     DFree(queries); DFree(topl_leaf); DFree(topl_dist); DFree(scores); DFree(lut); DFree(mult);
@@ -125,7 +128,10 @@ struct Workspace {
     DFree(work); DFree(tau); DFree(cand); DFree(cand_count); DFree(out_idx);
     DFree(out_dist);
     DFree(out_count);
-    nq = dim = 0;
+    DFree(merge_scratch[0]);
+    DFree(merge_scratch[1]);
+    merge_entries = 0;
+    nq = sq = dim = 0;
     pairs = cand_words = out_words = 0;
     cap = max_items = 0;
   }
@@ -150,17 +156,16 @@ struct StreamSlot {
 };
 constexpr int kMaxStreamSlots = 4;
 
+// The slot's work must have finished (the callers synchronise the device or
+// the slot's last stream first): no caller stream is touched here, since the
+// caller may already have destroyed it.
 void DestroySlot(StreamSlot* sl) {
-  if (sl->last_stream) (void)hipStreamSynchronize(sl->last_stream);
   if (sl->graph_exec) (void)hipGraphExecDestroy(sl->graph_exec);
   sl->ws.Release();
   if (sl->done_ev) (void)hipEventDestroy(sl->done_ev);
   if (sl->fork_ev) (void)hipEventDestroy(sl->fork_ev);
   if (sl->join_ev) (void)hipEventDestroy(sl->join_ev);
-  if (sl->side) {
-    (void)hipStreamSynchronize(sl->side);
-    (void)hipStreamDestroy(sl->side);
-  }
+  if (sl->side) (void)hipStreamDestroy(sl->side);
   delete sl;
 }
 
@@ -170,10 +175,12 @@ struct smx_index {
   smx::DeviceIndex ix;
   int device = 0;
   hipStream_t stream = nullptr;
-  std::mutex mu;
+  mutable std::mutex mu;            // one call at a time per handle (smx_get_timings too)
   std::vector<StreamSlot*> slots;   // one per stream the handle has searched on
   uint32_t cap_per_query = 0;      // candidate list capacity; 0 = sized per call (AutoCap)
   int seed_leaves = 4;
+  uint32_t seed_rows = smx::kSeedKeys;   // rows the seed scores per query (SMX_SEED_ROWS)
+  uint64_t leaf_slot_budget = 1ull << 26;   // see kLeafSlotBudget
   int scan_variant = 0;            // see smx::LaunchScan
   int fused_worklist_leaves = smx::kFusedWorklistLeaves;   // 0: always the side stream
   uint32_t chunk_tiles = 20;       // tiles per work item (tools/tune.py: 16-20 best at glove)
@@ -456,6 +463,18 @@ int SlotFor(smx_index* h, hipStream_t s, StreamSlot** out) {
   return SMX_OK;
 }
 
+// Leaf-slot words (`leaf_pair`, nl x queries) one sub-batch may use: 2^26
+// words = 256 MB per stream slot, and nl x queries < 2^32 (32-bit slot
+// indices).  At the Deep1B shape (50000 leaves) that is 1342 queries per
+// sub-batch; every BASELINE batch of 1000 runs whole.
+// (SMX_LEAF_SLOT_BUDGET at creation lowers it: the tests' sub-batch split)
+constexpr uint64_t kLeafSlotBudget = 1ull << 26;
+
+int SubBatchQueries(const smx_index* h) {
+  const uint64_t q = h->leaf_slot_budget / uint64_t(std::max(h->ix.nl, 1));
+  return int(std::max<uint64_t>(1, std::min<uint64_t>(q, 1u << 30)));
+}
+
 int EnsureWorkspace(smx_index* h, StreamSlot* sl, int nq, int L, int kk, int width) {
   Workspace& w = sl->ws;
   const smx::DeviceIndex& ix = h->ix;
@@ -467,17 +486,21 @@ int EnsureWorkspace(smx_index* h, StreamSlot* sl, int nq, int L, int kk, int wid
   const uint32_t base = h->cap_per_query ? h->cap_per_query
                                          : AutoCap(L, kk, std::min(h->seed_leaves, L));
   const uint32_t cap = std::max<uint32_t>(base, 2u * uint32_t(kk));
+  // per-sub-batch buffers for at most SubBatchQueries queries; the staged
+  // queries and outputs (host-buffer entry points) for the whole batch
+  const int sq = nq;
+  nq = std::min(nq, SubBatchQueries(h));
   const size_t pairs = size_t(nq) * L;
-  const size_t cand_words = size_t(nq) * cap, out_words = size_t(nq) * width;
-  if (nq <= w.nq && pairs <= w.pairs && cand_words <= w.cand_words && out_words <= w.out_words &&
-      ix.dim == w.dim) {
+  const size_t cand_words = size_t(nq) * cap, out_words = size_t(sq) * width;
+  if (nq <= w.nq && sq <= w.sq && pairs <= w.pairs && cand_words <= w.cand_words &&
+      out_words <= w.out_words && ix.dim == w.dim) {
     w.cap = cap;
     return SMX_OK;
   }
   // grow each quantity to cover this call and the earlier ones, so that
   // alternating shapes (leaves_to_search sweeps) settle after one growth
   // (hipFree synchronises the device)
-  const int anq = std::max(nq, w.nq);
+  const int anq = std::max(nq, w.nq), asq = std::max(sq, w.sq);
   const size_t apairs = std::max(pairs, w.pairs);
   const size_t acand = std::max(cand_words, w.cand_words);
   const size_t aout = std::max(out_words, w.out_words);
@@ -485,7 +508,7 @@ int EnsureWorkspace(smx_index* h, StreamSlot* sl, int nq, int L, int kk, int wid
   const int nl = ix.nl;
   const uint32_t max_items = MaxItems(ix, apairs);
   int rc;
-  if ((rc = DAlloc(&w.queries, size_t(anq) * ix.dim)) || (rc = DAlloc(&w.topl_leaf, apairs)) ||
+  if ((rc = DAlloc(&w.queries, size_t(asq) * ix.dim)) || (rc = DAlloc(&w.topl_leaf, apairs)) ||
       (rc = DAlloc(&w.topl_dist, apairs)) || (rc = DAlloc(&w.scores, size_t(anq) * nl)) ||
       (rc = DAlloc(&w.lut, size_t(anq) * smx::LutRows(ix.ksteps) * 16)) || (rc = DAlloc(&w.mult, anq)) ||
       (rc = DAlloc(&w.inv, anq)) || (rc = DAlloc(&w.counters, CounterLayout(nl).words)) ||
@@ -498,11 +521,12 @@ int EnsureWorkspace(smx_index* h, StreamSlot* sl, int nq, int L, int kk, int wid
       (rc = DAlloc(&w.cand, acand)) ||
       (rc = DAlloc(&w.cand_count, size_t(anq) * smx::kCounterStride)) ||
       (rc = DAlloc(&w.out_idx, aout)) || (rc = DAlloc(&w.out_dist, aout)) ||
-      (rc = DAlloc(&w.out_count, anq))) {
+      (rc = DAlloc(&w.out_count, asq))) {
     w.Release();
     return rc;
   }
   w.nq = anq;
+  w.sq = asq;
   w.pairs = apairs;
   w.cand_words = acand;
   w.out_words = aout;
@@ -529,12 +553,12 @@ float Elapsed(smx_index* h, int a, int b) {
   return ms;
 }
 
-// The search pipeline.  queries: device [nq][dim].  pre_only: stop before
-// reorder and output the pre-reorder set (width pre_nn).
-int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int final_nn,
-              bool reorder, bool pre_only, uint32_t* out_idx, float* out_dist,
-              int32_t* out_count, hipStream_t s, smx::ShardEntry* shard_out = nullptr,
-              bool single = false) {
+// The search pipeline for one sub-batch (RunSearch below splits a batch).
+// queries: device [nq][dim].  pre_only: stop before reorder and output the
+// pre-reorder set (width pre_nn).
+int RunSearchChunk(smx_index* h, const float* queries, int nq, int L, int pre_nn, int final_nn,
+                   bool reorder, bool pre_only, uint32_t* out_idx, float* out_dist,
+                   int32_t* out_count, hipStream_t s, smx::ShardEntry* shard_out, bool single) {
   smx::DeviceIndex& ix = h->ix;
   if (nq == 0) return SMX_OK;
   L = std::min(L, ix.nl);
@@ -542,7 +566,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   const int kk = std::max(1, SpillK(ix, pnn));
   const int width = shard_out ? 1 : pre_only ? pnn : final_nn;
   if (uint64_t(ix.nl) * uint64_t(nq) > 0xFFFFFFFFull)
-    return Fail(SMX_INVALID_ARGUMENT, "num_leaves x batch size must be below 2^32 (leaf slots)");
+    return Fail(SMX_INTERNAL, "sub-batch above the leaf-slot bound (RunSearch splits batches)");
   StreamSlot* sl = nullptr;
   int rc = SlotFor(h, s, &sl);
   if (rc) return rc;
@@ -595,6 +619,7 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   sa.tau_key = w.tau;
   sa.L = L;
   sa.seed = seed;
+  sa.seed_rows = int(std::min<uint32_t>(h->seed_rows, uint32_t(smx::kSeedKeys)));
   sa.kk = kk;
   sa.nl = nl;
   sa.residual = ix.residual;
@@ -903,6 +928,33 @@ int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int
   return SMX_OK;
 }
 
+// The search pipeline over a whole batch: sub-batches of SubBatchQueries
+// queries run one after another on the stream (the reference's
+// search_batched takes any batch size: scann_npy.cc:233-270), each query's
+// results at its own offset of the outputs.
+int RunSearch(smx_index* h, const float* queries, int nq, int L, int pre_nn, int final_nn,
+              bool reorder, bool pre_only, uint32_t* out_idx, float* out_dist,
+              int32_t* out_count, hipStream_t s, smx::ShardEntry* shard_out = nullptr,
+              bool single = false) {
+  const int chunk = SubBatchQueries(h);
+  if (nq <= chunk)
+    return RunSearchChunk(h, queries, nq, L, pre_nn, final_nn, reorder, pre_only, out_idx,
+                          out_dist, out_count, s, shard_out, single);
+  const int pnn = reorder ? pre_nn : final_nn;
+  const size_t kk = size_t(std::max(1, SpillK(h->ix, pnn)));
+  const size_t width = size_t(shard_out ? 1 : pre_only ? pnn : final_nn);
+  for (int q0 = 0; q0 < nq; q0 += chunk) {
+    const int n = std::min(chunk, nq - q0);
+    const int rc = RunSearchChunk(
+        h, queries + size_t(q0) * h->ix.dim, n, L, pre_nn, final_nn, reorder, pre_only,
+        out_idx ? out_idx + size_t(q0) * width : nullptr,
+        out_dist ? out_dist + size_t(q0) * width : nullptr, out_count ? out_count + q0 : nullptr,
+        s, shard_out ? shard_out + size_t(q0) * kk : nullptr, single);
+    if (rc) return rc;
+  }
+  return SMX_OK;
+}
+
 // Largest k' (kept candidates per query before SOAR dedupe) the final
 // select supports: its block kernel holds the candidate list (cap <=
 // 8192 keys) plus 2 k' select buffers in LDS (LaunchFinalSelect).
@@ -987,6 +1039,13 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
     h->narrow_only = nw[0] == '2';
   }
   if (const char* sw = std::getenv("SMX_SERIAL_WORKLIST")) h->serial_worklist = sw[0] != '0';
+  // 0: the all-sparse 32-slot tile at K % 4 == 2 (read per handle, so that the
+  // tests run both tiles in one process)
+  if (const char* df = std::getenv("SMX_DENSE_FIRST")) h->ix.dense_first = df[0] != '0';
+  if (const char* lb = std::getenv("SMX_LEAF_SLOT_BUDGET")) {
+    const long long v = std::atoll(lb);
+    if (v > 0 && uint64_t(v) < kLeafSlotBudget) h->leaf_slot_budget = uint64_t(v);
+  }
 #ifdef SMX_SCAN_DIAGNOSTICS
   // a timing ablation for a whole process (tools: the shard configurations'
   // bench lines under the timing library; see smx::LaunchScan)
@@ -999,6 +1058,10 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
   if (const char* ct = std::getenv("SMX_CHUNK_TILES")) {
     const int v = std::atoi(ct);
     if (v >= 8 && v <= 65535) h->chunk_tiles = uint32_t(v);
+  }
+  if (const char* sr = std::getenv("SMX_SEED_ROWS")) {
+    const int v = std::atoi(sr);
+    if (v >= 1 && v <= smx::kSeedKeys) h->seed_rows = uint32_t(v);
   }
   if (const char* sl = std::getenv("SMX_SEED_LEAVES")) {
     const int v = std::atoi(sl);
@@ -1018,7 +1081,9 @@ int smx_index_create(const smx_index_desc* desc, int32_t device, smx_index** out
 int smx_index_destroy(smx_index* h) {
   if (!h) return SMX_OK;
   (void)hipSetDevice(h->device);
-  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  // every slot's work, whatever stream it ran on, without naming the callers'
+  // streams (they may be gone; smx_release_stream documents the lifetime)
+  (void)hipDeviceSynchronize();
   for (StreamSlot* sl : h->slots) DestroySlot(sl);
   h->slots.clear();
   if (h->host_stats) (void)hipHostFree(h->host_stats);
@@ -1031,6 +1096,24 @@ int smx_index_destroy(smx_index* h) {
     if (e) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
+  return SMX_OK;
+}
+
+int smx_release_stream(smx_index* h, void* stream) {
+  if (!h) return Fail(SMX_INVALID_ARGUMENT, "null index");
+  std::lock_guard<std::mutex> lock(h->mu);
+  SMX_HIP(hipSetDevice(h->device));
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+  for (size_t i = 0; i < h->slots.size(); ++i) {
+    StreamSlot* sl = h->slots[i];
+    if (sl->last_stream != s && sl->key != s) continue;
+    // the slot's work ran on its last stream (and its side stream)
+    if (sl->last_stream) SMX_HIP(hipStreamSynchronize(sl->last_stream));
+    if (sl->side) SMX_HIP(hipStreamSynchronize(sl->side));
+    DestroySlot(sl);
+    h->slots.erase(h->slots.begin() + long(i));
+    --i;
+  }
   return SMX_OK;
 }
 
@@ -1240,9 +1323,6 @@ int smx_search_shard_device(smx_index* h, const float* d_queries, int32_t nq, in
                             void* stream) {
   int rc = CheckSearchArgs(h, nq, dim, p);
   if (rc) return rc;
-  const int pnn = p->reorder ? p->pre_reorder_nn : p->final_nn;
-  if (std::max(1, SpillK(h->ix, pnn)) > 256)
-    return Fail(SMX_INVALID_ARGUMENT, "shard lists above 256 entries per query are not supported");
   if (nq > 0 && !d_entries) return Fail(SMX_INVALID_ARGUMENT, "null entries buffer");
   static_assert(sizeof(smx_shard_entry) == sizeof(smx::ShardEntry), "entry layout");
   std::lock_guard<std::mutex> lock(h->mu);
@@ -1264,13 +1344,37 @@ int smx_merge_shards_device(smx_index* h, int32_t world, int32_t nq,
   const int pnn = p->reorder ? p->pre_reorder_nn : p->final_nn;
   if (pnn <= 0) return Fail(SMX_INVALID_ARGUMENT, "neighbor counts must be > 0");
   const int kk = std::max(1, SpillK(h->ix, pnn));
-  if (kk > 256 || world * kk > 2048)
-    return Fail(SMX_INVALID_ARGUMENT, "world x shard list width above 2048 is not supported");
+  if (kk > kMaxKPrime)
+    return Fail(SMX_INVALID_ARGUMENT, "shard lists above 2048 entries per query are not supported");
   if (nq == 0) return SMX_OK;
   std::lock_guard<std::mutex> lock(h->mu);
   SMX_HIP(hipSetDevice(h->device));
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
   smx::MergeArgs m{};
+  // more lists than one launch of the wide merge holds: its round buffers,
+  // in this stream's slot (another stream's merge runs concurrently)
+  const size_t scratch = smx::MergeScratchEntries(world, nq, kk);
+  if (scratch) {
+    StreamSlot* sl = nullptr;
+    int rc = SlotFor(h, s, &sl);
+    if (rc) return rc;
+    if (sl->last_stream != s) {   // the slot's earlier work on its other stream
+      SMX_HIP(hipEventRecord(sl->done_ev, sl->last_stream));
+      SMX_HIP(hipStreamWaitEvent(s, sl->done_ev, 0));
+      sl->last_stream = s;
+    }
+    Workspace& w = sl->ws;
+    if (w.merge_entries < scratch) {
+      DFree(w.merge_scratch[0]);
+      DFree(w.merge_scratch[1]);
+      w.merge_entries = 0;
+      if ((rc = DAlloc(&w.merge_scratch[0], scratch)) || (rc = DAlloc(&w.merge_scratch[1], scratch)))
+        return rc;
+      w.merge_entries = scratch;
+    }
+    m.scratch[0] = w.merge_scratch[0];
+    m.scratch[1] = w.merge_scratch[1];
+  }
   m.entries = reinterpret_cast<const smx::ShardEntry*>(d_entries);
   m.world = world;
   m.nq = nq;
@@ -1462,6 +1566,7 @@ int smx_set_profiling(smx_index* h, int32_t enabled) {
 
 int smx_get_timings(const smx_index* h, smx_timings* out) {
   if (!h || !out) return Fail(SMX_INVALID_ARGUMENT, "null argument");
+  std::lock_guard<std::mutex> lock(h->mu);   // RunSearch re-records the ring events
   *out = h->timings;
   out->scan_launches = 0;
   out->scan_ms_mode2 = 0.0f;

@@ -1,8 +1,13 @@
 """Multi-GPU search: one process per GPU over ``torch.distributed``.
 
 Replicas (configs whose index fits one GPU, e.g. glove): every rank holds the
-whole index and searches its slice of the query batch (``query_slice``); there
-is no collective (``bench.py --gpus N``).
+whole index.  Weak scaling (``bench.py --gpus N``, the default): each rank
+serves its own query batches, no collective.  Strong scaling
+(``SplitBatchSearcher``, ``bench.py --scaling strong``): ONE batch is split
+over the ranks by ``query_slice`` -- the chunking of the reference's
+SearchBatchedParallel (scann/scann_ops/cc/scann.cc:478-501), across GPUs
+instead of threads -- and the slices' results are all-gathered, so every rank
+holds the whole batch's results in query order.
 
 Range split (configs whose floats or codes do not fit one GPU): rank r holds
 rows [n*r/W, n*(r+1)/W) of *every* leaf (``TreeAHIndex.shard``), which stays
@@ -33,7 +38,8 @@ def query_slice(nq: int, rank: int, world: int) -> Tuple[int, int]:
 
 def all_gather_entries(local: torch.Tensor, world: int, group=None) -> torch.Tensor:
     """The one collective of a range-split batch: [nq, k, 2] int64 per rank ->
-    [world, nq, k, 2] on every rank."""
+    [world, nq, k, 2] on every rank (any equal-shaped tensor per rank ->
+    [world, ...])."""
     out = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
     if world == 1:
         out[0].copy_(local)
@@ -121,3 +127,37 @@ class RangeSplitSearcher:
         self.engine.search_shard(queries, leaves, pre_nn, final_nn, reorder, local)
         gathered = all_gather_entries(local, self.world, self.group)
         return self.engine.merge(self.world, gathered, nq, leaves, pre_nn, final_nn, reorder)
+
+
+class SplitBatchSearcher:
+    """Strong scaling over replicas: every rank calls ``search_batched`` with
+    the same whole batch; rank r searches rows ``query_slice(nq, r, world)``
+    with ``search(q_slice) -> (idx, dist, count)`` (device or CPU tensors), the
+    slices -- padded to ceil(nq / world) rows, the all-gather's equal shape --
+    are gathered in one collective per output, and every rank returns the
+    whole batch's (idx [nq, k], dist [nq, k], count [nq]) in query order: the
+    1-rank result bit for bit, since each query's search does not depend on
+    the others of its batch."""
+
+    def __init__(self, search, rank: int, world: int, group=None):
+        self.search = search
+        self.rank = rank
+        self.world = world
+        self.group = group
+
+    def search_batched(self, queries: torch.Tensor):
+        nq = int(queries.shape[0])
+        b, e = query_slice(nq, self.rank, self.world)
+        idx, dst, cnt = self.search(queries[b:e])
+        if self.world == 1:
+            return idx, dst, cnt
+        rows = (nq + self.world - 1) // self.world
+        bounds = [query_slice(nq, r, self.world) for r in range(self.world)]
+
+        def gather(t):
+            pad = torch.zeros((rows,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            pad[: t.shape[0]].copy_(t)
+            g = all_gather_entries(pad, self.world, self.group)
+            return torch.cat([g[r, : hi - lo] for r, (lo, hi) in enumerate(bounds)], 0)
+
+        return gather(idx), gather(dst), gather(cnt)

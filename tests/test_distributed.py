@@ -163,3 +163,43 @@ def test_query_slices_cover_batch():
             spans = [sd.query_slice(nq, r, world) for r in range(world)]
             assert spans[0][0] == 0 and spans[-1][1] == nq
             assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+
+
+def _split_rank_main(rank, world, port, outdir):
+    """Strong scaling on CPU: one 61-query batch split over `world` gloo
+    ranks (uneven slices), each slice searched by the oracle, the slices
+    all-gathered by SplitBatchSearcher."""
+    import torch.distributed as dist
+    from scann_amd import distributed as sd
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        from oracle import binding as oracle
+        ix, db, q = make_index()
+
+        def search(qs):
+            i, d, c = oracle.search(ix, qs.numpy(), 12, 60, 10, True, oracle.MODE_IDEAL)
+            return (torch.from_numpy(i.astype(np.int64)), torch.from_numpy(d),
+                    torch.from_numpy(c.astype(np.int32)))
+
+        s = sd.SplitBatchSearcher(search, rank, world)
+        idx, dst, cnt = s.search_batched(torch.from_numpy(q[:61]))
+        np.savez(os.path.join(outdir, f"split{rank}.npz"), idx=idx.numpy(), dst=dst.numpy(),
+                 cnt=cnt.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_split_batch_gloo_concatenates_to_the_one_rank_result(oracle, tmp_path, world):
+    """bench.py --scaling strong's split (scann.cc:478-501 chunking across
+    ranks): every rank ends with the 1-rank result of the whole batch, bit for
+    bit."""
+    mp.spawn(_split_rank_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    ix, db, q = make_index()
+    oi, od, oc = oracle.search(ix, q[:61], 12, 60, 10, True, oracle.MODE_IDEAL)
+    for rank in range(world):
+        r = np.load(tmp_path / f"split{rank}.npz")
+        np.testing.assert_array_equal(r["idx"], oi.astype(np.int64))
+        np.testing.assert_array_equal(r["dst"].view(np.uint32), od.view(np.uint32))
+        np.testing.assert_array_equal(r["cnt"], oc)

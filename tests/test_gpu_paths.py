@@ -9,6 +9,8 @@ when a handle is created):
   * SMX_FUSED_WORKLIST=0 / SMX_SERIAL_WORKLIST=0 -- the work list from its
     three launches (as above 4096 leaves), on the seed's stream or on the
     side stream;
+  * SMX_DENSE_FIRST=0 -- the all-sparse 32-slot tile at K % 4 == 2 instead
+    of the dense-first one;
   * chunk_tiles (smx_set_tuning) -- tiles per work item, down to the
     smallest accepted (8): the most work items per call, the case the item
     buffer (MaxItems) is sized for, in every tile mode.
@@ -34,6 +36,8 @@ PATHS = [({"SMX_NARROW": n}, 0) for n in "012"] + [
     # on the side stream beside it (the paths above 4096 leaves)
     ({"SMX_NARROW": "1", "SMX_FUSED_WORKLIST": "0"}, 0),
     ({"SMX_NARROW": "2", "SMX_FUSED_WORKLIST": "0", "SMX_SERIAL_WORKLIST": "0"}, 8),
+    # the all-sparse 32-slot tile where the dense-first one would run
+    ({"SMX_NARROW": "0", "SMX_DENSE_FIRST": "0"}, 0),
 ]
 
 
@@ -110,3 +114,66 @@ def test_paths_with_crowded_leaves(oracle, small_dot):
 
 def test_paths_without_seed(oracle, small_l2):
     _check(oracle, ix=small_l2[0], q=small_l2[2], L=12, pre=100, seed=0, reorder=False)
+
+
+# K = 26 scan tiles: 49, 50 and 51 AH blocks of 2 dims.  At 49 and
+# 50 blocks the 32-slot tile opens with one dense i8 MFMA over its last blocks
+# (at 49 with a padding block); SMX_DENSE_FIRST=0 runs the all-sparse tile;
+# 51 blocks take the next K.  Each against the oracle, in both tile widths.
+DENSE_FIRST_PATHS = [({"SMX_NARROW": "0", "SMX_DENSE_FIRST": df}, 0) for df in "01"] + [
+    ({"SMX_NARROW": "2", "SMX_DENSE_FIRST": "1"}, 0)]
+
+
+@pytest.mark.parametrize("dim", [98, 100, 102])
+def test_dense_first_tiles_at_block_counts(oracle, dim):
+    ix, db, q = make_index(n=5000, d=dim, leaves=24, seed=31 + dim, components=48)
+    assert ix.num_blocks == dim // 2
+    L, pre = 8, 100
+    oi, od, oc = oracle.search(ix, q, L, pre, 10, True, oracle.MODE_IDEAL)
+    for env, chunk in DENSE_FIRST_PATHS:
+        gi, gd, gc, _ = _search(ix, q, env, L, pre, 4, True, chunk)
+        tag = f"dim={dim} {env}"
+        np.testing.assert_array_equal(gc, oc, err_msg=tag)
+        np.testing.assert_array_equal(gi, oi, err_msg=tag)
+        np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32), err_msg=tag)
+
+
+def test_sub_batches_match_whole_batch(oracle, small_dot):
+    """A batch above the leaf-slot budget runs as sub-batches (no
+    batch-size limit, as the reference's search_batched has none).  With the
+    budget lowered to 48 leaves x 20 queries, 64 queries run as 20+20+20+4
+    through the host, device and shard entry points; every query's results
+    equal the oracle's."""
+    import torch
+    ix, db, q = small_dot
+    L, pre = 6, 100
+    oi, od, oc = oracle.search(ix, q, L, pre, 10, True, oracle.MODE_IDEAL)
+    nat = _handle(ix, {"SMX_LEAF_SLOT_BUDGET": str(ix.num_leaves * 20)})
+    try:
+        gi, gd, gc = nat.search_batched(q, L, pre, 10, True)
+        np.testing.assert_array_equal(gc, oc)
+        np.testing.assert_array_equal(gi, oi)
+        np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+        dev = torch.device("cuda", 0)
+        qd = torch.from_numpy(q).to(dev)
+        di = torch.zeros((q.shape[0], 10), dtype=torch.int32, device=dev)
+        dd = torch.zeros((q.shape[0], 10), dtype=torch.float32, device=dev)
+        dc = torch.zeros(q.shape[0], dtype=torch.int32, device=dev)
+        s = torch.cuda.Stream(dev)
+        nat.search_batched_device(qd.data_ptr(), q.shape[0], L, pre, 10, True, di.data_ptr(),
+                                  dd.data_ptr(), dc.data_ptr(), stream=s.cuda_stream)
+        nat.release_stream(s.cuda_stream)   # waits for the stream's work
+        np.testing.assert_array_equal(di.cpu().numpy().astype(np.uint32), oi)
+        np.testing.assert_array_equal(dd.cpu().numpy().view(np.uint32), od.view(np.uint32))
+        np.testing.assert_array_equal(dc.cpu().numpy(), oc)
+        # one shard = the whole index: its entries then merge to the same result
+        k = nat.shard_width(L, pre, 10, True)
+        ent = torch.zeros((q.shape[0], k, 2), dtype=torch.int64, device=dev)
+        nat.search_shard_device(qd.data_ptr(), q.shape[0], L, pre, 10, True, ent.data_ptr())
+        nat.merge_shards_device(1, q.shape[0], L, pre, 10, True, ent.data_ptr(), di.data_ptr(),
+                                dd.data_ptr(), dc.data_ptr())
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(di.cpu().numpy().astype(np.uint32), oi)
+        np.testing.assert_array_equal(dd.cpu().numpy().view(np.uint32), od.view(np.uint32))
+    finally:
+        nat.close()

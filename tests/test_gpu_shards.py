@@ -61,10 +61,36 @@ def test_shard_errors(oracle):
     nat = _native.NativeIndex(s)
     with pytest.raises(_native.SmxError):
         nat.shard_width(12, 0, 10, True)   # pre_nn must be > 0 with reorder
-    big = torch.empty((1, 1, 300, 2), dtype=torch.int64, device="cuda")
-    with pytest.raises(_native.SmxError):
-        nat.search_shard_device(torch.from_numpy(q[:1]).cuda().data_ptr(), 1, 12, 300, 10, True,
+    big = torch.empty((1, 1, 2100, 2), dtype=torch.int64, device="cuda")
+    with pytest.raises(_native.SmxError):   # k' above 2048
+        nat.search_shard_device(torch.from_numpy(q[:1]).cuda().data_ptr(), 1, 12, 2100, 10, True,
                                 big.data_ptr())
+
+
+@pytest.mark.parametrize("world,pre", [(2, 300), (16, 300), (5, 1000)])
+def test_wide_shard_lists_merge_to_the_oracle(oracle, world, pre):
+    """Shard lists above 256 entries (SOAR: k' = 2 pre, tree_ah_hybrid_residual.h:
+    263-267): the wide merge, in one launch (2 x 600 entries), after a partial
+    round (16 x 600 > 8192 entries: groups of 13 lists) and at k' = 2000."""
+    from scann_amd.distributed import NativeShardEngine
+    ix, db, q = _soar_index()
+    engines = [NativeShardEngine(ix.shard(r, world), device=0) for r in range(world)]
+    qd = torch.from_numpy(q).cuda()
+    nq = q.shape[0]
+    for leaves, final, reorder in ((40, 10, True), (20, 30, False)):
+        k = engines[0].shard_width(leaves, pre, final, reorder)
+        assert k == 2 * pre
+        entries = torch.empty((world, nq, k, 2), dtype=torch.int64, device="cuda")
+        for r, e in enumerate(engines):
+            e.search_shard(qd, leaves, pre, final, reorder, entries[r])
+        idx, dst, cnt = engines[0].merge(world, entries, nq, leaves, pre, final, reorder)
+        torch.cuda.synchronize()
+        oi, od, oc = oracle.search(ix, q, leaves, pre, final, reorder, oracle.MODE_IDEAL)
+        tag = f"world={world} pre={pre} L={leaves}"
+        np.testing.assert_array_equal(cnt.cpu().numpy(), oc, err_msg=tag)
+        np.testing.assert_array_equal(idx.cpu().numpy().astype(np.uint32), oi, err_msg=tag)
+        np.testing.assert_array_equal(dst.cpu().numpy().view(np.uint32), od.view(np.uint32),
+                                      err_msg=tag)
 
 
 def _free_port():

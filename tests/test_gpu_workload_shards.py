@@ -69,8 +69,6 @@ def _check_points(oracle, ix, q, points, min_rows_per_leaf, multi_chunk_leaves):
                 np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
                 if cap:
                     assert t["overflow_retries"] > 0, t
-            if (pre if ix.disjoint else 2 * pre) > 256:
-                continue   # shard lists hold at most 256 entries (k' = 2 pre with SOAR)
             si_o, sd_o, sc_o = oracle.search(ix, q, lv, pre, 10, True, oracle.MODE_IDEAL, 16)
             if ix.disjoint:   # the view's top-k is the shard's, renumbered
                 np.testing.assert_array_equal(si_o, ix.leaf_members[oi])
@@ -102,8 +100,7 @@ def test_soar_shard_at_workload_density(oracle):
     """configs[3]: rank 0 of 8 of a 10000-leaf SOAR index (shift 18, k' =
     2 x pre), >= 1000 members per rank-leaf, at the bench's L = 100 /
     pre = 100, the recall gate's L = 200 / pre = 128 and L = 1000 / pre =
-    256 (the standalone view only: a SOAR shard's list holds k' = 2 pre <=
-    256 entries)."""
+    256 (k' = 512 entries per shard list: the wide merge)."""
     ix, q = _shard(8 * 10000 * 520, 10000, 4096, 1.5, 4, 250_000)
     assert ix.global_topn_shift == 18 and not ix.disjoint
     _check_points(oracle, ix, q, [(100, 100), (200, 128), (1000, 256)], 1000, 100)
