@@ -1787,18 +1787,39 @@ __device__ uint64_t ThresholdOfVals(const uint32_t (&vals)[kSeedPerThread], uint
     __syncthreads();
     const uint32_t c = s_cnt;
     if (c <= uint32_t(kSeedSel)) {
-      // wave 0: the exact kk-th of the c compacted values, 4 or 16 per lane
+      // wave 0: the exact kk-th of the c compacted values, held in registers
+      // (4 per lane; above 256 values, 16 per lane), the bits by ballots
       if (wid == 0) {
         uint32_t x = 0;
-        const int per = c <= 256u ? 4 : kSeedSel / 64;
-        for (int b = 31; b >= 0; --b) {
-          const uint32_t t = x | ((1u << b) - 1u);
-          uint32_t cnt = 0;
-          for (int i = 0; i < per; ++i) {
+        if (c <= 256u) {
+          uint32_t v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
             const uint32_t j = uint32_t(lane) + 64u * uint32_t(i);
-            cnt += uint32_t(__popcll(__ballot(j < c && sval[j] <= t)));
+            v[i] = j < c ? sval[j] : 0xFFFFFFFFu;
           }
-          if (cnt < kk) x |= 1u << b;
+          for (int b = 31; b >= 0; --b) {
+            const uint32_t t = x | ((1u << b) - 1u);
+            const uint32_t cnt = uint32_t(__popcll(__ballot(v[0] <= t))) +
+                                 uint32_t(__popcll(__ballot(v[1] <= t))) +
+                                 uint32_t(__popcll(__ballot(v[2] <= t))) +
+                                 uint32_t(__popcll(__ballot(v[3] <= t)));
+            if (cnt < kk) x |= 1u << b;
+          }
+        } else {
+          uint32_t v[kSeedSel / 64];
+#pragma unroll
+          for (int i = 0; i < kSeedSel / 64; ++i) {
+            const uint32_t j = uint32_t(lane) + 64u * uint32_t(i);
+            v[i] = j < c ? sval[j] : 0xFFFFFFFFu;
+          }
+          for (int b = 31; b >= 0; --b) {
+            const uint32_t t = x | ((1u << b) - 1u);
+            uint32_t cnt = 0;
+#pragma unroll
+            for (int i = 0; i < kSeedSel / 64; ++i) cnt += uint32_t(__popcll(__ballot(v[i] <= t)));
+            if (cnt < kk) x |= 1u << b;
+          }
         }
         if (lane == 0) s_x = x;
       }

@@ -179,7 +179,15 @@ struct smx_index {
   std::vector<StreamSlot*> slots;   // one per stream the handle has searched on
   uint32_t cap_per_query = 0;      // candidate list capacity; 0 = sized per call (AutoCap)
   int seed_leaves = 4;
-  uint32_t seed_rows = smx::kSeedKeys;   // rows the seed scores per query (SMX_SEED_ROWS)
+  // rows the seed scores per query (SMX_SEED_ROWS): 2048 of at most 4096.
+  // The seed's score loop streams its rows' codes from the fabric (98 MB per
+  // glove batch at 4096 rows, 6.3 TB/s: PMC, profiles/r06/pmc_seed.txt), so
+  // with batches in flight it competes with the other batches' scans; same
+  // box (profiles/r06/ab/seed_rows.txt), glove in flight at L = 20 / 100:
+  // 14.89 / 9.31 M QPS at 2048 rows against 13.73 / 8.98 M at 4096 (one batch
+  // alone: 10.22 / 6.97 against 10.69 / 7.27 M -- the tighter thresholds of
+  // 4096 rows shorten the scan: 40.2 -> 33.1 us at L = 20).
+  uint32_t seed_rows = 2048;
   uint64_t leaf_slot_budget = 1ull << 26;   // see kLeafSlotBudget
   int scan_variant = 0;            // see smx::LaunchScan
   int fused_worklist_leaves = smx::kFusedWorklistLeaves;   // 0: always the side stream

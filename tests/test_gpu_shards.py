@@ -77,9 +77,9 @@ def test_wide_shard_lists_merge_to_the_oracle(oracle, world, pre):
     engines = [NativeShardEngine(ix.shard(r, world), device=0) for r in range(world)]
     qd = torch.from_numpy(q).cuda()
     nq = q.shape[0]
-    for leaves, final, reorder in ((40, 10, True), (20, 30, False)):
+    for leaves, final, reorder in ((40, 10, True), (20, min(pre, 300), False)):
         k = engines[0].shard_width(leaves, pre, final, reorder)
-        assert k == 2 * pre
+        assert k == 2 * (pre if reorder else final)
         entries = torch.empty((world, nq, k, 2), dtype=torch.int64, device="cuda")
         for r, e in enumerate(engines):
             e.search_shard(qd, leaves, pre, final, reorder, entries[r])
