@@ -74,10 +74,11 @@ CONFIGS = {
     "soar100m": dict(n=100_000_000, leaves=10000, leaves_to_search=100, metric=0, seed=4,
                      generated=True, split=8, soar=1.5, dim=96, components=512, spread=1.6,
                      train_sample=250_000,
-                     # (pre_reorder_nn <= 128: SOAR shard lists hold 2 x pre <= 256)
-                     sweep=[20, 40, 60, 100, 150, 200, [100, 128], [200, 128], [400, 128]],
-                     # (a SOAR shard's list holds k' = 2 x pre <= 256 entries)
-                     parity_points=[(100, 100), (200, 128)],
+                     # (k' = 2 x pre_reorder_nn per SOAR shard list: the 512-entry lists
+                     # of pre 256 take the wide merge)
+                     sweep=[20, 40, 60, 100, 150, 200, [100, 128], [200, 128], [400, 128],
+                            [1000, 256]],
+                     parity_points=[(100, 100), (200, 128), (1000, 256)],
                      workload="configs[3]: synthetic 100M x 96 dot product + SOAR (lambda 1.5, "
                               "overretrieve 2), tree-AH 10000 leaves, LUT16 AH 48 blocks x 2 "
                               "dims, leaves_to_search=100, reorder 100, k=10, batch=1000, "
@@ -146,6 +147,7 @@ def build_index(n, seed):
 # the one-hot LUT16 GEMM needs (a one-hot row is 2:4 sparse, so the sparse
 # instruction computes the whole dense product).
 SMFMAC_PEAK_TOPS = 2 * 32 * 32 * 64 / 32 * 1024 * 2.4e9 / 1e12
+HBM_PEAK_BPS = 8.0e12   # MI355X HBM3E (MI355X_MICROARCH.md)
 DENSE_I8_PEAK_TOPS = 5000.0
 
 
@@ -687,7 +689,11 @@ def main():
             "recall_at_10": round(recall, 4),
             "roofline": dict(roof, traffic=traffic,
                              hbm_GBps_measured=(round(traffic / (avg_scan_ms * 1e-3) / 1e9, 1)
-                                                if traffic else None)),
+                                                if traffic else None),
+                             # the scan's HBM basis: PMC bytes per launch / the kernel alone /
+                             # 8 TB/s (MI355X_MICROARCH.md)
+                             hbm_frac=(round(traffic / (avg_scan_ms * 1e-3) / HBM_PEAK_BPS, 4)
+                                       if traffic else None)),
             "stage_ms": ({k: round(v, 4) for k, v in stage.items()} if not args.no_stages
                          else None),
             "operating_points": points,
@@ -927,16 +933,22 @@ def main_generated(args, rank, world, local, dist, dev):
                             f"{split} copies of this rank's [nq][{k}] list"),
             "roofline": dict(roof, traffic=traffic,
                              hbm_GBps_measured=(round(traffic / (avg_scan_ms * 1e-3) / 1e9, 1)
-                                                if traffic else None)),
+                                                if traffic else None),
+                             # the scan's HBM basis: PMC bytes per launch / the kernel alone /
+                             # 8 TB/s (MI355X_MICROARCH.md)
+                             hbm_frac=(round(traffic / (avg_scan_ms * 1e-3) / HBM_PEAK_BPS, 4)
+                                       if traffic else None)),
             "stage_ms": {k2: round(stages[k2], 4) for k2 in
                          ("partition_ms", "invert_ms", "seed_scan_ms", "scan_ms", "select_ms",
                           "total_ms")},
         }
+        view_ids = None
         if not args.no_parity:
-            result["parity_vs_oracle"] = shard_parity(
+            result["parity_vs_oracle"], view_ids = shard_parity(
                 ix, eng, q, CFG["parity_points"], args.cpu_threads or host_threads()[0], local)
         if not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline_shard(ix, q, args.cpu_threads or host_threads()[0])
+            result["cpu_baseline"] = cpu_baseline_shard(ix, q, args.cpu_threads or host_threads()[0],
+                                                        view_ids)
         print(json.dumps(result), flush=True)
     nat.close()
     if dist is not None:
@@ -981,6 +993,7 @@ def shard_parity(ix, eng, q, points, threads, device):
     sub = q[:PARITY_QUERIES]
     nv = _native.NativeIndex(view, device=device)
     out = []
+    view_ids = {}
     try:
         for lv, pre in points:
             t = time.perf_counter()
@@ -1003,6 +1016,7 @@ def shard_parity(ix, eng, q, points, threads, device):
             vi, vd, vc = oracle.search(view, sub, lv, pre, FINAL_NN, True, oracle.MODE_IDEAL,
                                        threads)
             gi, gd, gc = nv.search_batched(sub, lv, pre, FINAL_NN, True)
+            view_ids[(lv, pre)] = gi
             ent["standalone_view"] = {
                 "id_mismatch": float((gi != vi).mean()),
                 "dist_bits_mismatch": float((gd.view(np.uint32) != vd.view(np.uint32)).mean()),
@@ -1017,13 +1031,16 @@ def shard_parity(ix, eng, q, points, threads, device):
                     "standalone_view: the shard renumbered as an index of its own through "
                     "search_batched vs the oracle on that view",
             "mode": "oracle ideal mode (oracle/scann_oracle.cc) vs the GPU, bit-exact ids and "
-                    "distances", "points": out}
+                    "distances", "points": out}, view_ids
 
 
-def cpu_baseline_shard(ix, q, threads):
+def cpu_baseline_shard(ix, q, threads, view_ids=None):
     """The AVX2 port over this rank's shard viewed as a standalone index
     (members renumbered 0..M-1, their float rows as the dataset): the
-    reference's per-rank work, timed on a bounded sample of the batch."""
+    reference's per-rank work, timed on a bounded sample of the batch.  Its
+    emulate-mode ids (FastTopNeighbors GC + the int16 truncated threshold,
+    lut16_avx2.inc:432-438, 515-521) against the GPU's on the same view for
+    the parity subset (SURVEY A.7's emulate-vs-ideal mismatch)."""
     from oracle import binding as oracle
     oracle.build()
     m = ix.num_members
@@ -1031,7 +1048,11 @@ def cpu_baseline_shard(ix, q, threads):
     port = oracle.Avx2Port(view)
     model, isa = cpu_info()
     sub = q[:max(threads, 250)]
-    port.search(sub, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True, threads)
+    pi, _, _ = port.search(sub, LEAVES_TO_SEARCH, PRE_NN, FINAL_NN, True, threads)
+    mismatch = None
+    gv = (view_ids or {}).get((LEAVES_TO_SEARCH, PRE_NN))
+    if gv is not None:
+        mismatch = float((pi[:gv.shape[0]] != gv).mean())
     runs = []
     for _ in range(3):
         t = time.perf_counter()
@@ -1042,7 +1063,12 @@ def cpu_baseline_shard(ix, q, threads):
                 kind="port", cpu_model=model, isa=isa, runs_qps=[round(x, 1) for x in runs],
                 sample=f"median of 3 runs of {sub.shape[0]} queries through the AVX2 port over "
                        f"this rank's shard as a standalone index ({m} members renumbered, "
-                       f"emulate-mode pipeline A), {threads} threads; no merge")
+                       f"emulate-mode pipeline A), {threads} threads; no merge",
+                id_mismatch_vs_gpu=mismatch,
+                id_mismatch_basis=(f"the port's ids vs the GPU's search_batched on the same "
+                                   f"standalone view, first {gv.shape[0]} queries (the parity "
+                                   f"subset) at leaves_to_search {LEAVES_TO_SEARCH}, "
+                                   f"pre_reorder_nn {PRE_NN}" if gv is not None else None))
 
 
 def _peek_gpus(argv):

@@ -31,9 +31,9 @@ pytestmark = pytest.mark.gpu
 NQ = 64
 
 
-def _shard(n, leaves, components, soar, seed, train):
+def _shard(n, leaves, components, soar, seed, train, spread=0.9):
     from scann_amd import generate
-    ds = generate.GeneratedDataset(n, 96, seed, components=components,
+    ds = generate.GeneratedDataset(n, 96, seed, components=components, spread=spread,
                                    device=torch.device("cuda"))
     ix = generate.build_generated_shard(
         ds, leaves, 0, 8, soar_lambda=soar, seed=seed, training_sample_size=train,
@@ -88,19 +88,21 @@ def _check_points(oracle, ix, q, points, min_rows_per_leaf, multi_chunk_leaves):
 
 
 def test_deep1b_shard_at_workload_density(oracle):
-    """configs[4]: rank 0 of 8 of a 50000-leaf dot-product index (shift 16),
-    >= 500 rows per rank-leaf, at the bench's headline L = 400 / pre = 100
-    and the recall-gate point L = 2000 / pre = 256."""
-    ix, q = _shard(8 * 50000 * 520, 50000, 1 << 17, None, 5, 1_000_000)
+    """configs[4] at the bench's own density: rank 0 of 8 of the 10^9-row,
+    50000-leaf dot-product index (shift 16; 125M rows, ~2,500 per
+    rank-leaf), at the bench's headline L = 400 / pre = 100 and the
+    recall-gate point L = 2000 / pre = 256."""
+    ix, q = _shard(1_000_000_000, 50000, 1 << 17, None, 5, 1_000_000)
     assert ix.global_topn_shift == 16 and ix.disjoint
-    _check_points(oracle, ix, q, [(400, 100), (2000, 256)], 500, 100)
+    _check_points(oracle, ix, q, [(400, 100), (2000, 256)], 2400, 1000)
 
 
 def test_soar_shard_at_workload_density(oracle):
-    """configs[3]: rank 0 of 8 of a 10000-leaf SOAR index (shift 18, k' =
-    2 x pre), >= 1000 members per rank-leaf, at the bench's L = 100 /
-    pre = 100, the recall gate's L = 200 / pre = 128 and L = 1000 / pre =
-    256 (k' = 512 entries per shard list: the wide merge)."""
-    ix, q = _shard(8 * 10000 * 520, 10000, 4096, 1.5, 4, 250_000)
+    """configs[3] at the bench's own density: rank 0 of 8 of the 10^8-row,
+    10000-leaf SOAR index (shift 18, k' = 2 x pre; 12.5M rows, ~2,500
+    members per rank-leaf), at the bench's L = 100 / pre = 100, the recall
+    gate's L = 200 / pre = 128 and L = 1000 / pre = 256 (k' = 512 entries per
+    shard list: the wide merge)."""
+    ix, q = _shard(100_000_000, 10000, 512, 1.5, 4, 250_000, spread=1.6)   # bench.py's data
     assert ix.global_topn_shift == 18 and not ix.disjoint
-    _check_points(oracle, ix, q, [(100, 100), (200, 128), (1000, 256)], 1000, 100)
+    _check_points(oracle, ix, q, [(100, 100), (200, 128), (1000, 256)], 2400, 1000)
