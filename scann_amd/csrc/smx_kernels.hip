@@ -1732,13 +1732,27 @@ __device__ uint32_t BlockRank256(uint64_t key, uint64_t* sbuf) {
 // the answer's bits from the top, each by one ballot count (bit b is 1 when
 // fewer than k values lie at or below the prefix with bit b clear and every
 // lower bit set).  No LDS, no barrier; the loop is wave-uniform.
-__device__ __forceinline__ uint32_t WaveKth(uint32_t v, uint32_t k) {
-  uint32_t x = 0;
-  for (int b = 31; b >= 0; --b) {
+// The bits are searched from the highest one in which the values' range
+// [lo, hi] (wave-uniform, the k-th inside it) differs: the ones above are
+// the prefix every value shares.
+__device__ __forceinline__ uint32_t WaveKth(uint32_t v, uint32_t k, uint32_t lo, uint32_t hi) {
+  if (lo == hi) return lo;
+  const int top = 31 - __clz(lo ^ hi);
+  uint32_t x = lo & ~((top == 31) ? 0xFFFFFFFFu : ((2u << top) - 1u));
+  for (int b = top; b >= 0; --b) {
     const uint32_t t = x | ((1u << b) - 1u);
     if (uint32_t(__popcll(__ballot(v <= t))) < k) x |= 1u << b;
   }
   return x;
+}
+
+__device__ __forceinline__ uint32_t WaveMin(uint32_t v) {
+  for (int off = 32; off > 0; off >>= 1) v = min(v, uint32_t(__shfl_xor(int(v), off)));
+  return v;
+}
+__device__ __forceinline__ uint32_t WaveMax(uint32_t v) {
+  for (int off = 32; off > 0; off >>= 1) v = max(v, uint32_t(__shfl_xor(int(v), off)));
+  return v;
 }
 
 // The threshold key of a query from its seed distances (ordered bits, 16
@@ -1756,17 +1770,26 @@ __device__ __forceinline__ uint32_t WaveKth(uint32_t v, uint32_t k) {
 // ranks of the 256 minima and of the compacted keys, 7.2 us p50 per block.)
 __device__ uint64_t ThresholdOfVals(const uint32_t (&vals)[kSeedPerThread], uint32_t kk) {
   __shared__ uint32_t sval[kSeedSel];
-  __shared__ uint32_t s_wb[4], s_wc[2][4], s_cnt, s_x;
+  __shared__ uint32_t s_wb[4], s_wlo[4], s_wc[2][4], s_cnt, s_x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (kk <= 256u) {
     uint32_t vmin = 0xFFFFFFFFu;
 #pragma unroll
     for (int i = 0; i < kSeedPerThread; ++i) vmin = min(vmin, vals[i]);
-    const uint32_t wk = WaveKth(vmin, (kk + 3u) >> 2);
-    if (lane == 0) s_wb[wid] = wk;
+    // the wave's bound: none (MAX) when fewer than k of its minima are real
+    const uint32_t k4 = (kk + 3u) >> 2;
+    const uint32_t wlo = WaveMin(vmin);
+    uint32_t wk = 0xFFFFFFFFu;
+    if (uint32_t(__popcll(__ballot(vmin != 0xFFFFFFFFu))) >= k4)
+      wk = WaveKth(vmin, k4, wlo, WaveMax(vmin != 0xFFFFFFFFu ? vmin : 0u));
+    if (lane == 0) {
+      s_wb[wid] = wk;
+      s_wlo[wid] = wlo;
+    }
     if (tid == 0) s_cnt = 0;
     __syncthreads();
     const uint32_t thi = max(max(s_wb[0], s_wb[1]), max(s_wb[2], s_wb[3]));
+    const uint32_t blo = min(min(s_wlo[0], s_wlo[1]), min(s_wlo[2], s_wlo[3]));
     // compaction: the wave's count by ballots, one LDS atomic per wave for
     // its base, then the slots again by ballots (no per-value registers)
     uint32_t n = 0;
@@ -1790,7 +1813,11 @@ __device__ uint64_t ThresholdOfVals(const uint32_t (&vals)[kSeedPerThread], uint
       // wave 0: the exact kk-th of the c compacted values, held in registers
       // (4 per lane; above 256 values, 16 per lane), the bits by ballots
       if (wid == 0) {
-        uint32_t x = 0;
+        // the kk-th lies in [blo, thi] (blo = the smallest value; at least kk
+        // values are at or below thi): the bits below their highest
+        // differing one
+        const int top = blo == thi ? -1 : 31 - __clz(blo ^ thi);
+        uint32_t x = top < 0 ? blo : blo & ~((top == 31) ? 0xFFFFFFFFu : ((2u << top) - 1u));
         if (c <= 256u) {
           uint32_t v[4];
 #pragma unroll
@@ -1798,7 +1825,7 @@ __device__ uint64_t ThresholdOfVals(const uint32_t (&vals)[kSeedPerThread], uint
             const uint32_t j = uint32_t(lane) + 64u * uint32_t(i);
             v[i] = j < c ? sval[j] : 0xFFFFFFFFu;
           }
-          for (int b = 31; b >= 0; --b) {
+          for (int b = top; b >= 0; --b) {
             const uint32_t t = x | ((1u << b) - 1u);
             const uint32_t cnt = uint32_t(__popcll(__ballot(v[0] <= t))) +
                                  uint32_t(__popcll(__ballot(v[1] <= t))) +
@@ -1813,7 +1840,7 @@ __device__ uint64_t ThresholdOfVals(const uint32_t (&vals)[kSeedPerThread], uint
             const uint32_t j = uint32_t(lane) + 64u * uint32_t(i);
             v[i] = j < c ? sval[j] : 0xFFFFFFFFu;
           }
-          for (int b = 31; b >= 0; --b) {
+          for (int b = top; b >= 0; --b) {
             const uint32_t t = x | ((1u << b) - 1u);
             uint32_t cnt = 0;
 #pragma unroll
