@@ -4,6 +4,7 @@
 #define SMX_INTERNAL_H_
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 namespace smx {
@@ -345,8 +346,10 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count,
 // variant 0: the LUT16 scan (lut16_scan_kernel; `narrow`: the work list
 // holds 16-slot items); 4: the same without its threshold epilogue (timing
 // ablation, results invalid; the diagnostic variants take 32-slot items only).
+// e0 / e1 (or NULL): timing events recorded by the scan's own dispatch.
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,
-                      hipStream_t s, uint32_t narrow);
+                      hipStream_t s, uint32_t narrow, hipEvent_t e0 = nullptr,
+                      hipEvent_t e1 = nullptr);
 // Resident scan workgroups per CU (occupancy of the index's instantiation).
 hipError_t ScanBlocksPerCU(const DeviceIndex& ix, int* blocks);
 // The per-query thresholds (tau_key) from the seed leaves.

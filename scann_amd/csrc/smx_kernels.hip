@@ -4357,16 +4357,30 @@ hipError_t LaunchWorklist(const DeviceIndex& ix, const uint32_t* leaf_count, Wor
 // The 32-slot scan of K = KV: the dense-first tile where the blocks fit it
 // (KV % 4 == 2, nb <= 2 KV - 2: glove's 50 blocks at KV = 26; SMX_DENSE_FIRST=0
 // for the all-sparse tile).
+// A scan launch, timed by the dispatch itself when events are given
+// (hipExtLaunchKernelGGL records them in the kernel's own dispatch packet:
+// the kernel's execution, as rocprofv3's kernel trace measures it, without
+// the command processor's time between separate event packets and the
+// dispatch -- 3-5 us on the profiled stage timings of round 5).
+template <class F>
+void ScanDispatch(F kernel, int grid, int threads, hipStream_t s, const ScanArgs& a,
+                  hipEvent_t e0, hipEvent_t e1) {
+  if (e0 && e1)
+    hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, e0, e1, 0, a);
+  else
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, a);
+}
+
 template <int KV>
-void LaunchWide(const DeviceIndex& ix, const ScanArgs& a, int grid, hipStream_t s) {
+void LaunchWide(const DeviceIndex& ix, const ScanArgs& a, int grid, hipStream_t s, hipEvent_t e0,
+                hipEvent_t e1) {
   if constexpr (KV % 4 == 2) {
     if (ix.dense_first && ix.nb <= 2 * KV - 2) {
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, 0, true>), dim3(grid), dim3(64 * ScanWaves<KV>()),
-                         0, s, a);
+      ScanDispatch(lut16_scan_kernel<KV, 0, 0, true>, grid, 64 * ScanWaves<KV>(), s, a, e0, e1);
       return;
     }
   }
-  hipLaunchKernelGGL((lut16_scan_kernel<KV, 0>), dim3(grid), dim3(64 * ScanWaves<KV>()), 0, s, a);
+  ScanDispatch(lut16_scan_kernel<KV, 0>, grid, 64 * ScanWaves<KV>(), s, a, e0, e1);
 }
 
 #ifdef SMX_SCAN_DIAGNOSTICS
@@ -4396,7 +4410,7 @@ void LaunchWide(const DeviceIndex& ix, const ScanArgs& a, int grid, hipStream_t 
     } else if (narrow == kNarrowOnly) {                                                    \
       SMX_SCAN_VARIANT(KV, 0)                                                              \
     } else {                                                                               \
-      LaunchWide<KV>(ix, a, grid, s);                                                      \
+      LaunchWide<KV>(ix, a, grid, s, e0, e1);                                              \
     }                                                                                      \
     break;
 #else
@@ -4404,15 +4418,15 @@ void LaunchWide(const DeviceIndex& ix, const ScanArgs& a, int grid, hipStream_t 
   case KV:                                                                                 \
     if (variant != 0) return hipErrorInvalidValue;                                         \
     if (narrow == kNarrowOnly)                                                             \
-      hipLaunchKernelGGL((lut16_scan_kernel<KV, 0, int(kNarrowOnly)>), dim3(grid),         \
-                         dim3(64 * ScanWaves<KV>()), 0, s, a);                             \
+      ScanDispatch(lut16_scan_kernel<KV, 0, int(kNarrowOnly)>, grid, 64 * ScanWaves<KV>(), s, \
+                   a, e0, e1);                                                             \
     else                                                                                   \
-      LaunchWide<KV>(ix, a, grid, s);                                                      \
+      LaunchWide<KV>(ix, a, grid, s, e0, e1);                                              \
     break;
 #endif
 
 hipError_t LaunchScan(const DeviceIndex& ix, const ScanArgs& a, int grid, int variant,
-                      hipStream_t s, uint32_t narrow) {
+                      hipStream_t s, uint32_t narrow, hipEvent_t e0, hipEvent_t e1) {
   switch (ix.ksteps) {
     SMX_SCAN_CASE(4)
     SMX_SCAN_CASE(8)

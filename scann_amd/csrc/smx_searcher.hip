@@ -780,15 +780,19 @@ int RunSearchChunk(smx_index* h, const float* queries, int nq, int L, int pre_nn
       SMX_HIP(hipEventRecord(sl->join_ev, sl->side));
       SMX_HIP(hipStreamWaitEvent(s, sl->join_ev, 0));   // join
     }
-    Mark(h, 5, s);
+    // the scan's timing events go into its own dispatch (hipExtLaunchKernel):
+    // its execution alone, as rocprofv3 measures it
     const size_t le = size_t(h->scan_logged % kScanLog) * 2;
-    if (h->scan_log) SMX_HIP(hipEventRecord(h->scan_ev[le], s));
-    SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s, narrow));
-    if (h->scan_log) {
-      SMX_HIP(hipEventRecord(h->scan_ev[le + 1], s));
-      ++h->scan_logged;
+    hipEvent_t se0 = nullptr, se1 = nullptr;
+    if (h->profiling) {
+      se0 = h->ev[5];
+      se1 = h->ev[6];
+    } else if (h->scan_log) {
+      se0 = h->scan_ev[le];
+      se1 = h->scan_ev[le + 1];
     }
-    Mark(h, 6, s);
+    SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s, narrow, se0, se1));
+    if (h->scan_log && !h->profiling) ++h->scan_logged;
     SMX_HIP(smx::LaunchFinalSelect(sel, nq, s));
     Mark(h, 7, s);
     return SMX_OK;
