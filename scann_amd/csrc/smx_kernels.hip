@@ -2079,6 +2079,26 @@ __global__ void __launch_bounds__(256, 4) seed_tau_kernel(SeedArgs a, WorklistAr
 #ifndef SMX_POS_B64
 #define SMX_POS_B64 0
 #endif
+// SMX_POS_VALU: the index word built by VALU from the code byte instead of
+// read from the position table.  Only the index fields of the compressed
+// values that are 1 matter (value 2 g0 -> bits [4 g0, 4 g0 + 2) must hold
+// p0, value 8 + 2 g1 -> bits [16 + 4 g1, ...) must hold p1; the odd values
+// are 0, their fields free): u = (byte >> 4) | (byte >> 6) << 16, times
+// 0x1111 (v_mul_u32_u24), puts p0 in the low two bits of nibbles 0-3 and p1
+// in those of nibbles 4-7 -- 4 VALU instead of one SDWA op and a ds_read_b32
+// (the 2-way bank-conflicting read of the position table).
+#ifndef SMX_POS_VALU
+#define SMX_POS_VALU 0
+#endif
+#define SMX_POS_WORD(W, B, OUT)                                                                 \
+  do {                                                                                          \
+    uint32_t b4_, b6_;                                                                          \
+    asm("v_lshrrev_b32_sdwa %0, 4, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "      \
+        "src1_sel:BYTE_" #B "\n\tv_lshrrev_b32_sdwa %1, 6, %2 dst_sel:DWORD "                   \
+        "dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_" #B                                \
+        : "=&v"(b4_), "=&v"(b6_) : "v"(W));                                                     \
+    OUT = int(__umul24((b6_ << 16) | b4_, 0x1111u));                                            \
+  } while (0)
 template <int K, int R, bool NOLDS = false>
 __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)[K / 2],
                                            const v4i* grp_tab, const int* pos_tab) {
@@ -2112,7 +2132,15 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
       }
 #undef SMX_SDWA_OFFS
       o[slot] = *reinterpret_cast<const v4i*>(reinterpret_cast<const char*>(grp_tab) + og);
-#if SMX_POS_B64
+#if SMX_POS_VALU
+      switch (t & 3) {
+        case 0: SMX_POS_WORD(w, 0, ix[slot]); break;
+        case 1: SMX_POS_WORD(w, 1, ix[slot]); break;
+        case 2: SMX_POS_WORD(w, 2, ix[slot]); break;
+        default: SMX_POS_WORD(w, 3, ix[slot]); break;
+      }
+      (void)op;
+#elif SMX_POS_B64
       // the index word read as the low half of a ds_read_b64: its bank is
       // (a/4) mod 64, so the 16 entries 16 bytes apart sit on 16 distinct
       // bank pairs (a ds_read_b32 banks (a/4) mod 32: entries p and p + 8
@@ -2144,7 +2172,8 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
     acc = __builtin_amdgcn_smfmac_i32_32x32x64_i8(o[s % R], b[s], acc, ix[s % R], 0, 0);
     if (s + R < KS) ld(s % R, s + R);
   }
-  __builtin_amdgcn_sched_group_barrier(0x100, 2 * R, 0);
+  constexpr int kDs = SMX_POS_VALU ? 1 : 2;   // LDS reads per operand step
+  __builtin_amdgcn_sched_group_barrier(0x100, kDs * R, 0);
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     // the index word's v_or right before its MFMA (placed early, it waits for
@@ -2152,7 +2181,7 @@ __device__ __forceinline__ v16i TileSmfmac(const uint32_t* codes, const v8i (&b)
     if (!NOLDS && SMX_POS_B64) __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
     if (s == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-    if (s + R < KS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    if (s + R < KS) __builtin_amdgcn_sched_group_barrier(0x100, kDs, 0);
   }
   return acc;
 }
@@ -2187,7 +2216,17 @@ __device__ __forceinline__ v16i TileSmfmacD(const uint32_t* codes, const v8i (&b
     }
 #undef SMX_SDWA_OFFS
     o[slot] = *reinterpret_cast<const v4i*>(reinterpret_cast<const char*>(grp_tab) + og);
+#if SMX_POS_VALU
+    switch (t & 3) {
+      case 0: SMX_POS_WORD(w, 0, ix[slot]); break;
+      case 1: SMX_POS_WORD(w, 1, ix[slot]); break;
+      case 2: SMX_POS_WORD(w, 2, ix[slot]); break;
+      default: SMX_POS_WORD(w, 3, ix[slot]); break;
+    }
+    (void)op;
+#else
     ix[slot] = *reinterpret_cast<const int*>(reinterpret_cast<const char*>(pos_tab) + op);
+#endif
   };
   // the dense step's one-hot row: x0 = ((by & 3) << 2) | ((by >> 4) & 3)
   const uint32_t by = (codes[KS >> 2] >> (8 * (KS & 3))) & 0xFFu;
@@ -2202,13 +2241,14 @@ __device__ __forceinline__ v16i TileSmfmacD(const uint32_t* codes, const v8i (&b
     acc = __builtin_amdgcn_smfmac_i32_32x32x64_i8(o[st % R], b[st], acc, ix[st % R], 0, 0);
     if (st + R < KS) ld(st % R, st + R);
   }
-  __builtin_amdgcn_sched_group_barrier(0x100, 2 * R + 1, 0);
+  constexpr int kDs = SMX_POS_VALU ? 1 : 2;
+  __builtin_amdgcn_sched_group_barrier(0x100, kDs * R + 1, 0);
   __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // the dense step
   __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // (the next tile's code load)
 #pragma unroll
   for (int st = 0; st < KS; ++st) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    if (st + R < KS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    if (st + R < KS) __builtin_amdgcn_sched_group_barrier(0x100, kDs, 0);
   }
   return acc;
 }
@@ -2259,7 +2299,15 @@ __device__ __forceinline__ void TileSmfmac16(const uint32_t* ca, const uint32_t*
     }
 #undef SMX_SDWA_OFFS16
     o[slot] = *reinterpret_cast<const v4i*>(reinterpret_cast<const char*>(grp_tab) + og);
+#if SMX_POS_VALU
+    if (st & 1)
+      SMX_POS_WORD(w, 2, ix[slot]);
+    else
+      SMX_POS_WORD(w, 0, ix[slot]);
+    (void)op;
+#else
     ix[slot] = *reinterpret_cast<const int*>(reinterpret_cast<const char*>(pos_tab) + op);
+#endif
   };
 #pragma unroll
   for (int p = 0; p < R; ++p)
@@ -2280,11 +2328,12 @@ __device__ __forceinline__ void TileSmfmac16(const uint32_t* ca, const uint32_t*
       acc_a = __builtin_amdgcn_smfmac_i32_16x16x128_i8(o[t % R], b[t >> 1], acc_a, ix[t % R], 0, 0);
     if (t + R < NS) ld(t % R, t + R);
   }
-  __builtin_amdgcn_sched_group_barrier(0x100, 2 * R, 0);
+  constexpr int kDs = SMX_POS_VALU ? 1 : 2;
+  __builtin_amdgcn_sched_group_barrier(0x100, kDs * R, 0);
 #pragma unroll
   for (int t = 0; t < NS; ++t) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    if (t + R < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    if (t + R < NS) __builtin_amdgcn_sched_group_barrier(0x100, kDs, 0);
   }
 }
 
