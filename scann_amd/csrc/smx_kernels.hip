@@ -702,6 +702,11 @@ __device__ void TopLFinish(int qi, int L, uint32_t m, const uint64_t* sel, int32
 constexpr int kWaveTopL = 512;         // L limit of the register top-L kernel
 constexpr int kBlockTopCand = 1024;    // compacted keys one block orders
 constexpr uint32_t kTopNarrow = 256;   // histogram rounds until this many keys
+// above this many compacted keys (<= 256) the block rank instead of the
+// counting rank (as final_select_rank_kernel's kBlockRankMin)
+constexpr uint32_t kBlockRankMinTopL = 128;
+
+__device__ uint32_t BlockRank256(uint64_t key, uint64_t* sbuf);
 
 template <int VPT, int NT>
 __device__ __forceinline__ void TopLBlock(const float* __restrict__ scores, int nl, int L,
@@ -810,7 +815,14 @@ __device__ __forceinline__ void TopLBlock(const float* __restrict__ scores, int 
   }
   __syncthreads();
   const uint32_t cnt = s_cnt;
-  if (cnt <= uint32_t(kBlockTopCand)) {
+  if (NT == 256 && cnt <= 256u && cnt > kBlockRankMinTopL) {
+    // one key per thread, ranked by BlockRank256 (wave bitonic sorts and
+    // binary searches of the other waves' runs; padding keys sort last)
+    const uint64_t key = uint32_t(tid) < cnt ? sel[tid] : ((~0ull << 16) | uint32_t(tid));
+    __syncthreads();   // sel is the rank's scratch
+    const uint32_t r = BlockRank256(key, sel);
+    if (uint32_t(tid) < cnt && r < m) srt[r] = key;
+  } else if (cnt <= uint32_t(kBlockTopCand)) {
     // counting rank over (score, leaf), keys unique; keep the first m
     for (uint32_t i = tid; i < cnt; i += NT) {
       const uint64_t key = sel[i];
