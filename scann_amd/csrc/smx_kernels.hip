@@ -4447,11 +4447,10 @@ void LaunchWide(const DeviceIndex& ix, const ScanArgs& a, int grid, hipStream_t 
 #ifdef SMX_SCAN_DIAGNOSTICS
 #define SMX_SCAN_VARIANT(KV, V)                                                            \
   if (narrow == kNarrowOnly)                                                               \
-    hipLaunchKernelGGL((lut16_scan_kernel<KV, V, int(kNarrowOnly)>), dim3(grid),           \
-                       dim3(64 * ScanWaves<KV>()), 0, s, a);                               \
+    ScanDispatch(lut16_scan_kernel<KV, V, int(kNarrowOnly)>, grid, 64 * ScanWaves<KV>(), s, \
+                 a, e0, e1);                                                               \
   else                                                                                     \
-    hipLaunchKernelGGL((lut16_scan_kernel<KV, V>), dim3(grid), dim3(64 * ScanWaves<KV>()), \
-                       0, s, a);
+    ScanDispatch(lut16_scan_kernel<KV, V>, grid, 64 * ScanWaves<KV>(), s, a, e0, e1);
 #define SMX_SCAN_CASE(KV)                                                                  \
   case KV:                                                                                 \
     if (variant == 16) {                                                                   \

@@ -557,7 +557,10 @@ void Mark(smx_index* h, int i, hipStream_t s) {
 
 float Elapsed(smx_index* h, int a, int b) {
   float ms = 0.0f;
-  if (hipEventElapsedTime(&ms, h->ev[a], h->ev[b]) != hipSuccess) return 0.0f;
+  if (hipEventElapsedTime(&ms, h->ev[a], h->ev[b]) != hipSuccess) {
+    (void)hipGetLastError();   // an unrecorded pair: not sticky for the next launch check
+    return 0.0f;
+  }
   return ms;
 }
 
