@@ -2452,15 +2452,18 @@ struct QParam {
   float inv;
 };
 
-// A wave's own LDS: hit list, survivor stage (double buffered: a segment's
-// survivors are copied to the lists during the next segment), per-slot counts.
+// A wave's own LDS: hit list, the survivor stage of up to kStageSegs of its
+// segments (written to the candidate lists together: list_flush), their
+// query ids and per-slot counts.
+constexpr int kStageSegs = 4;                // segments one stage holds
+constexpr int kStageKeys = 2 * kItemKeys;    // survivors one stage holds
 struct ScanWaveLds {
-  uint4 hsum[2 * kHitsPerWave][2];   // 16 sums as int16 pairs
+  uint4 hsum[2 * kHitsPerWave][2];   // 16 sums as int16 pairs (the flush's scratch too)
   uint32_t hmeta[2 * kHitsPerWave];  // tile << 6 | lane
-  uint64_t kbuf[2][kItemKeys];
-  uint8_t kslot[2][kItemKeys];
-  uint32_t s_kn[2];
-  uint32_t qcnt[32], q_slot[32], qrun[32], prev_qid[32];
+  uint64_t kbuf[kStageKeys];
+  uint8_t kslot[kStageKeys];         // stage segment << 5 | query slot
+  uint32_t s_kn;
+  uint32_t qcnt[kStageSegs * 32], qtab[kStageSegs * 32];
   QParam qp[32];
 };
 
@@ -2609,49 +2612,47 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
     s_su = ws.z;
   }
   uint32_t sj = ws.y;   // the share's first tile inside its first item
-  bool pending = false;   // the previous segment's survivors await their copy
-  bool flush = false;     // ... and, before that, their list-slot atomics
-  uint32_t fqid = 0;      // that segment's query ids (lanes < 32)
-  uint32_t slot = 0;      // that copy's first list slot (lanes < 32)
-  uint32_t par = 0;       // this segment's survivor buffer
-  // the previous segment's survivors to their queries' lists: each key's
-  // place = its query's reserved first slot (the returned value of the
-  // segment-end atomic, waited for only here) + a running count
-  auto copy_prev = [&]() {
-    if (ABL & 16) {
-      pending = false;
-      return;
+  // The survivors of up to kStageSegs segments stay in the wave's stage and
+  // go to the candidate lists together, when the stage is full and once at
+  // the end: one list-slot atomic per (segment, query slot) with survivors,
+  // then each key at its query's reserved slot + a running count.  (Round 5
+  // flushed every segment -- its slot atomics issued behind the next
+  // segment's first code loads, the keys stored after that tile -- so with
+  // vmcnt in order every later code-load wait also waited for those atomics
+  // and stores: the ablations put 7-10 us of the scan there, more at looser
+  // seed thresholds, profiles/r06/ab/scan_ablations_rows.txt.)
+  uint32_t nst = 0;   // segments in the stage (wave-uniform)
+  auto list_flush = [&]() {
+    const uint32_t kn = min(__builtin_amdgcn_readfirstlane(wl.s_kn), uint32_t(kStageKeys));
+    if ((ABL & 16) == 0 && nst > 0) {   // (16: timing ablation without the lists)
+      uint32_t* qbase = reinterpret_cast<uint32_t*>(&wl.hsum[0][0]);   // [kStageSegs * 32]
+      uint32_t* qrun = qbase + kStageSegs * 32;
+      for (uint32_t e = uint32_t(lane); e < nst * 32u; e += 64) {
+        const uint32_t m = wl.qcnt[e];
+        uint32_t base = 0;
+        if (m) {
+          SMX_CHECK(wl.qtab[e], a.bd.nq, "slot query");
+          base = atomicAdd(&a.cand_count[size_t(wl.qtab[e]) * kCounterStride], m);
+        }
+        qbase[e] = base;
+        qrun[e] = 0;
+      }
+      WaveLdsSync();
+      for (uint32_t e = uint32_t(lane); e < kn; e += 64) {
+        const uint32_t qs = wl.kslot[e];
+        const uint32_t sl = qbase[qs] + atomicAdd(&qrun[qs], 1u);
+        SMX_GUARD(wl.qtab[qs], a.bd.nq, "list query")
+        if (sl < a.cap) a.cand[size_t(wl.qtab[qs]) * a.cap + sl] = wl.kbuf[e];
+      }
+      WaveLdsSync();
     }
-    const uint32_t pp = par ^ 1u;
-    if (lane < Q) {
-      wl.q_slot[lane] = slot;
-      wl.qrun[lane] = 0;
-    }
+    for (uint32_t e = uint32_t(lane); e < uint32_t(kStageSegs * 32); e += 64) wl.qcnt[e] = 0;
+    if (lane == 0) wl.s_kn = 0;
     WaveLdsSync();
-    const uint32_t kn = min(wl.s_kn[pp], uint32_t(KB));
-    for (uint32_t e = uint32_t(lane); e < kn; e += 64) {
-      const uint32_t qs = wl.kslot[pp][e];
-      const uint32_t sl = wl.q_slot[qs] + atomicAdd(&wl.qrun[qs], 1u);
-      SMX_GUARD(wl.prev_qid[qs], a.bd.nq, "list query")
-      if (sl < a.cap) a.cand[size_t(wl.prev_qid[qs]) * a.cap + sl] = wl.kbuf[pp][e];
-    }
-    WaveLdsSync();
-    pending = false;
+    nst = 0;
   };
-  // one list-slot atomic per query slot with survivors of the last segment;
-  // issued behind the next segment's loads (vmcnt is in order: a wait for
-  // those loads would otherwise wait for these atomics too), consumed by
-  // copy_prev after that segment's first tile
-  auto flush_prev = [&]() {
-    if ((ABL & 16) == 0 && lane < Q) {   // (16: timing ablation without the lists)
-      const uint32_t m = wl.qcnt[lane];
-      if (m) SMX_CHECK(fqid, a.bd.nq, "slot query");
-      slot = m ? atomicAdd(&a.cand_count[size_t(fqid) * kCounterStride], m) : 0u;
-      wl.prev_qid[lane] = fqid;
-    }
-    flush = false;
-    pending = true;
-  };
+  for (uint32_t e = uint32_t(lane); e < uint32_t(kStageSegs * 32); e += 64) wl.qcnt[e] = 0;
+  if (lane == 0) wl.s_kn = 0;
   // one LDS claim of two tiles of segment `sg` (lane 0; broadcast at use)
   auto claim2 = [&](uint32_t sg) -> uint32_t {
     uint32_t v = 0;
@@ -2756,6 +2757,12 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       // the segment's tiles, on the 32-slot or the 16-slot path (the item's
       // kItemNarrow flag; wave-uniform)
       uint32_t tiles_done = 0;
+      // a full stage (kStageSegs segments, or less than one segment's worth
+      // of key room) goes to the lists before this segment stages its own
+      if (nst == uint32_t(kStageSegs) ||
+          __builtin_amdgcn_readfirstlane(wl.s_kn) > uint32_t(kStageKeys - KB))
+        list_flush();
+      const uint32_t kn_seg = __builtin_amdgcn_readfirstlane(wl.s_kn);
       auto run_seg = [&](auto nr_tag) {
       constexpr bool NR = decltype(nr_tag)::value;
       constexpr int KB_STEPS = NR ? (K + 3) / 4 : K / 2 - (DN ? 1 : 0);   // B fragments (steps)
@@ -2811,7 +2818,6 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       // the slot's sum limit (written with the record by the pair scatter:
       // the largest LUT16 sum whose distance can pass the query's threshold)
       const int amax = cl.amax;
-      if (flush) flush_prev();
       if (lane < Q) {   // (16-slot: lanes 16..31 repeat slots 0..15; never counted)
         QParam v;
         v.qid = qid;
@@ -2819,9 +2825,8 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
         v.bias = cl.bias;
         v.inv = cl.inv;
         wl.qp[lane] = v;
-        wl.qcnt[lane] = 0;
+        wl.qtab[nst * 32u + lane] = qid;
       }
-      if (lane == 0) wl.s_kn[par] = 0;
       WaveLdsSync();
       uint32_t whits = 0;   // wave-uniform
 
@@ -2835,7 +2840,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       constexpr uint32_t EPH = NR ? 8u : 16u;
       auto drain = [&]() {
         const uint32_t total = whits * EPH;
-        uint32_t kn = __builtin_amdgcn_readfirstlane(wl.s_kn[par]);
+        uint32_t kn = __builtin_amdgcn_readfirstlane(wl.s_kn);
         for (uint32_t e0 = 0; e0 < total; e0 += 64) {
           const uint32_t e = e0 + uint32_t(lane);
           bool pass = false;
@@ -2871,10 +2876,10 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
             if (pass) {
               const uint32_t p = kn + __builtin_amdgcn_mbcnt_hi(
                                           uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u));
-              if (p < uint32_t(KB)) {
-                wl.kbuf[par][p] = key;
-                wl.kslot[par][p] = uint8_t(cc);
-                atomicAdd(&wl.qcnt[cc], 1u);
+              if (p < uint32_t(kStageKeys)) {
+                wl.kbuf[p] = key;
+                wl.kslot[p] = uint8_t((nst << 5) | uint32_t(cc));
+                atomicAdd(&wl.qcnt[nst * 32u + uint32_t(cc)], 1u);
               } else {  // stage full (rare): straight to the global list
                 const uint32_t qq = wl.qp[cc].qid;
                 const uint32_t gs = atomicAdd(&a.cand_count[size_t(qq) * kCounterStride], 1u);
@@ -2884,7 +2889,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
             kn += uint32_t(__popcll(bm));
           }
         }
-        if (lane == 0) wl.s_kn[par] = kn;
+        if (lane == 0) wl.s_kn = kn;
         WaveLdsSync();   // the hit list is rewritten next
       };
 
@@ -3077,10 +3082,6 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
             }
             tile(xa, xb, tq[d]);
             ++tiles_done;
-            if (pending) {   // after the segment's first tile (its stores: as the drain's)
-              copy_prev();
-              __builtin_amdgcn_s_waitcnt(0);
-            }
           }
           const uint32_t prev = tq[(d + D - 1) % D];
           ok[d] = live && produce(tq[d]);
@@ -3133,7 +3134,6 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
             load_codes(more ? tn : t, cb, cb_b);
             tile(codes, codes_b, t);
             ++tiles_done;
-            if (pending) copy_prev();   // after the segment's first tile: the atomic has returned
             if (!more) break;
             drain_mid();
             advance(t, tn);
@@ -3162,20 +3162,18 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       }
       if (ABL & 8) st_t2 = __builtin_amdgcn_s_memtime();
       if (ABL & 8) {
-        uint32_t sv = lane < Q ? wl.qcnt[lane] : 0u;
+        uint32_t sv = lane < Q ? wl.qcnt[nst * 32u + uint32_t(lane)] : 0u;
         for (int off = 32; off > 0; off >>= 1) sv += uint32_t(__shfl_xor(int(sv), off));
         st_surv = sv;
       }
-      flush = true;   // (its slot atomics: at the next segment's start)
-      fqid = qid;
-      par ^= 1u;
+      // the segment keeps its stage entry when it staged survivors
+      if (__builtin_amdgcn_readfirstlane(wl.s_kn) > kn_seg) ++nst;
       if ((ABL & 8) && lane == 0)
         StampItem(a, worker, item, st_rt, st_t0, st_t1, st_t2, __builtin_amdgcn_s_memtime(),
                   uint64_t(tiles_done) | (uint64_t(st_hits) << 16) | (uint64_t(st_surv) << 40));
     }
-    if (flush) flush_prev();
-    if (pending) copy_prev();
   }
+  list_flush();
 }
 
 // Stage entry point of the threshold select: per set of kSeedKeys ordered
