@@ -2830,49 +2830,67 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
       WaveLdsSync();
       uint32_t whits = 0;   // wave-uniform
 
-      // the hit list's elements (EPH sums per hit) spread over the lanes,
-      // element e = EPH * hit + i on lane e % 64: per-element test, key, and
-      // a ballot-ranked append to the LDS stage (no returning atomic; the
-      // lanes of one hit read its meta and parameters as broadcasts).
+      // the hit list, one hit per lane: its EPH sums (packed int16, in
+      // registers) against the slot's sum limit give a mask, and each round
+      // takes one set bit per lane -- the element's distance, key and a
+      // ballot-ranked append to the LDS stage (no returning atomic).  A hit
+      // lane has ~1-2 passing elements of its EPH, so a round of 64 hits
+      // costs ~2-3 element rounds instead of EPH (round 5 spread the EPH x
+      // hits elements over the lanes, every one tested and ranked).
       // sum <= amax implies key <= the threshold key: the scan's thresholds
       // are the seed's (ordered(d_k') << 32 | 0xFFFFFFFF) or none, and d is
       // monotone in the sum
       constexpr uint32_t EPH = NR ? 8u : 16u;
       auto drain = [&]() {
-        const uint32_t total = whits * EPH;
+        const uint32_t nh = whits;
         uint32_t kn = __builtin_amdgcn_readfirstlane(wl.s_kn);
-        for (uint32_t e0 = 0; e0 < total; e0 += 64) {
-          const uint32_t e = e0 + uint32_t(lane);
-          bool pass = false;
-          uint64_t key = 0;
-          int cc = 0;
-          if (e < total) {
-            const uint32_t hidx = NR ? e >> 3 : e >> 4, i = e & (EPH - 1u);
-            const uint32_t meta = wl.hmeta[hidx];
-            const uint32_t jj = meta >> 6;
-            uint32_t dp;
-            if constexpr (NR) {
-              // lane (n, g): column n, rows 4 g + (i & 3) of chain i >> 2
-              cc = int(meta & 15u);
-              dp = jj * kDpPerTile + 16u * (i >> 2) + 4u * ((meta >> 4) & 3u) + (i & 3u);
-            } else {
-              cc = int(meta & 31u);
-              const uint32_t hh = (meta >> 5) & 1u;
-              dp = jj * kDpPerTile + (i & 3u) + 8u * (i >> 2) + 4u * hh;
+        for (uint32_t h0 = 0; h0 < nh; h0 += 64) {
+          const uint32_t hidx = h0 + uint32_t(lane);
+          uint32_t mask = 0, meta = 0;
+          uint32_t sw[EPH / 2];
+          QParam pq = {};
+          if (hidx < nh) {
+            meta = wl.hmeta[hidx];
+            const uint4 w0 = wl.hsum[hidx][0];
+            sw[0] = w0.x; sw[1] = w0.y; sw[2] = w0.z; sw[3] = w0.w;
+            if constexpr (!NR) {
+              const uint4 w1 = wl.hsum[hidx][1];
+              sw[4] = w1.x; sw[5] = w1.y; sw[6] = w1.z; sw[7] = w1.w;
             }
-            const uint32_t word = reinterpret_cast<const uint32_t*>(&wl.hsum[hidx][0])[i >> 1];
-            const int sum = int(int16_t(uint16_t(word >> (16u * (i & 1u)))));
-            const QParam pq = wl.qp[cc];
-            if (sum <= pq.amax) {
-              pass = true;
+            pq = wl.qp[NR ? (meta & 15u) : (meta & 31u)];
+#pragma unroll
+            for (uint32_t i = 0; i < EPH; ++i) {
+              const int sum = int(int16_t(uint16_t(sw[i >> 1] >> (16u * (i & 1u)))));
+              mask |= (sum <= pq.amax ? 1u : 0u) << i;
+            }
+          } else {
+#pragma unroll
+            for (uint32_t i = 0; i < EPH / 2; ++i) sw[i] = 0;
+          }
+          const int cc = int(NR ? (meta & 15u) : (meta & 31u));
+          const uint32_t jj = meta >> 6;
+          while (__builtin_amdgcn_ballot_w64(mask != 0u)) {   // wave-uniform rounds
+            const bool pass = mask != 0u;
+            uint64_t key = 0;
+            if (pass) {
+              const uint32_t i = uint32_t(__builtin_ctz(mask));
+              mask &= mask - 1u;
+              uint32_t dp;
+              if constexpr (NR)   // lane (n, g): column n, rows 4 g + (i & 3) of chain i >> 2
+                dp = jj * kDpPerTile + 16u * (i >> 2) + 4u * ((meta >> 4) & 3u) + (i & 3u);
+              else
+                dp = jj * kDpPerTile + (i & 3u) + 8u * (i >> 2) + 4u * ((meta >> 5) & 1u);
+              uint32_t word = sw[0];
+#pragma unroll
+              for (uint32_t k = 1; k < EPH / 2; ++k)
+                if ((i >> 1) == k) word = sw[k];
+              const int sum = int(int16_t(uint16_t(word >> (16u * (i & 1u)))));
               const float d = DistOf(sum, pq.inv, pq.bias);
               const uint32_t tie = a.shift > 0 ? ((uint32_t(leaf) << a.shift) | dp)
                                                : a.members[moff + dp];
               key = (uint64_t(OrderedBits(d)) << 32) | tie;
             }
-          }
-          const uint64_t bm = __builtin_amdgcn_ballot_w64(pass);
-          if (bm) {
+            const uint64_t bm = __builtin_amdgcn_ballot_w64(pass);
             if (pass) {
               const uint32_t p = kn + __builtin_amdgcn_mbcnt_hi(
                                           uint32_t(bm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bm), 0u));
@@ -2881,7 +2899,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
                 wl.kslot[p] = uint8_t((nst << 5) | uint32_t(cc));
                 atomicAdd(&wl.qcnt[nst * 32u + uint32_t(cc)], 1u);
               } else {  // stage full (rare): straight to the global list
-                const uint32_t qq = wl.qp[cc].qid;
+                const uint32_t qq = pq.qid;
                 const uint32_t gs = atomicAdd(&a.cand_count[size_t(qq) * kCounterStride], 1u);
                 if (gs < a.cap) a.cand[size_t(qq) * a.cap + gs] = key;
               }
