@@ -117,10 +117,12 @@ typedef struct smx_search_params {
   int32_t reorder;          /* 1: exact reorder with the float dataset        */
 } smx_search_params;
 
-/* Stage timings of the last search on a handle (ms, HIP events recorded on
- * the handle's stream around each launch; filled only when profiling was
- * enabled with smx_set_profiling(index, 1), which makes every call
- * synchronous).  smx_set_profiling(index, 2) instead records two events
+/* Stage timings of the last search on a handle (ms; filled only when
+ * profiling was enabled with smx_set_profiling(index, 1), which makes every
+ * call synchronous).  The seed, scan and select stages are timed by events in
+ * the kernels' own dispatch packets (their execution, as rocprofv3 reports
+ * it); partition + top-L by HIP events recorded on the stream around the
+ * launches.  smx_set_profiling(index, 2) instead records two events
  * around every scan launch of the calls that follow, without synchronising
  * (up to 4096 launches, the latest kept): smx_get_timings then reports
  * their count and mean duration (scan_launches, scan_ms_mode2) once the

@@ -360,12 +360,15 @@ WorklistArgs MakeWorklistArgs(const DeviceIndex& ix, const uint32_t* leaf_count,
                               uint32_t narrow, const Bounds& bd);
 // The seed thresholds and every pair's record (one block per query); with
 // `wl`, more blocks build the whole work list (ix.nl <= kFusedWorklistLeaves).
+// e0 / e1 (or NULL): timing events recorded by the kernel's own dispatch.
 hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s,
-                      const WorklistArgs* wl = nullptr);
+                      const WorklistArgs* wl = nullptr, hipEvent_t e0 = nullptr,
+                      hipEvent_t e1 = nullptr);
 hipError_t LaunchKthKeys(const uint32_t* vals, int sets, int kk, uint64_t* out, hipStream_t s);
 // The rank kernel (one block per query, <= kSelMax keys in LDS) for k' <=
 // kSelMax, the block kernel otherwise; both rescan overflowed lists first.
-hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s);
+hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s,
+                             hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 // Whether the final selection of these arguments fits the CU's 160 KiB LDS
 // (static + dynamic; the block kernel for k' > kSelMax holds the whole list).
 bool FinalSelectFits(const SelectArgs& a);

@@ -4574,14 +4574,18 @@ hipError_t LaunchLeafScores(const DeviceIndex& ix, int leaf, const int8_t* lut, 
   return hipGetLastError();
 }
 
-#define SMX_SEED_CASE(KV)                                                        \
-  case KV:                                                                       \
-    hipLaunchKernelGGL(seed_tau_kernel<KV>, dim3(nq + nwl), dim3(256), 0, s, a,            \
-                       wl ? *wl : WorklistArgs{}, nq);                                      \
+#define SMX_SEED_CASE(KV)                                                                   \
+  case KV:                                                                                  \
+    if (e0 && e1)                                                                           \
+      hipExtLaunchKernelGGL(seed_tau_kernel<KV>, dim3(nq + nwl), dim3(256), 0, s, e0, e1, 0, a, \
+                            wl ? *wl : WorklistArgs{}, nq);                                 \
+    else                                                                                    \
+      hipLaunchKernelGGL(seed_tau_kernel<KV>, dim3(nq + nwl), dim3(256), 0, s, a,            \
+                         wl ? *wl : WorklistArgs{}, nq);                                    \
     break;
 
 hipError_t LaunchSeed(const DeviceIndex& ix, const SeedArgs& a, int nq, hipStream_t s,
-                      const WorklistArgs* wl) {
+                      const WorklistArgs* wl, hipEvent_t e0, hipEvent_t e1) {
   if (wl && wl->nl > kFusedWorklistLeaves) return hipErrorInvalidValue;
   const int nwl = wl ? (wl->nl + kWlPosPerBlock - 1) / kWlPosPerBlock : 0;
   if (nq + nwl == 0) return hipSuccess;
@@ -4666,7 +4670,8 @@ bool FinalSelectFits(const SelectArgs& a) {
   return lds + static_lds <= 160 * 1024;
 }
 
-hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s) {
+hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s, hipEvent_t e0,
+                             hipEvent_t e1) {
   if (nq == 0) return hipSuccess;
   if (!FinalSelectFits(a)) return hipErrorInvalidValue;
   // the overflow flag is raised by the select kernels themselves; the
@@ -4680,12 +4685,18 @@ hipError_t LaunchFinalSelect(const SelectArgs& a, int nq, hipStream_t s) {
   while (kcap < a.cap) kcap <<= 1;
   const uint32_t selcap = std::max<uint32_t>(2048u, 2 * kkp2);
   if (a.kk <= kSelMax) {   // (shard mode too; the list is read from global memory)
-    hipLaunchKernelGGL(final_select_rank_kernel, dim3(nq), dim3(256), 0, s, a);
+    if (e0 && e1)
+      hipExtLaunchKernelGGL(final_select_rank_kernel, dim3(nq), dim3(256), 0, s, e0, e1, 0, a);
+    else
+      hipLaunchKernelGGL(final_select_rank_kernel, dim3(nq), dim3(256), 0, s, a);
     return hipGetLastError();
   }
   const size_t lds = size_t(kcap) * 8 + size_t(selcap) * 8 + size_t(kkp2) * 8 +
                      size_t(a.dim) * 4 + size_t(a.kk) * 8 + (kSelBins + 256) * 4;
-  hipLaunchKernelGGL(final_select_kernel, dim3(nq), dim3(256), lds, s, a);
+  if (e0 && e1)
+    hipExtLaunchKernelGGL(final_select_kernel, dim3(nq), dim3(256), lds, s, e0, e1, 0, a);
+  else
+    hipLaunchKernelGGL(final_select_kernel, dim3(nq), dim3(256), lds, s, a);
   return hipGetLastError();
 }
 

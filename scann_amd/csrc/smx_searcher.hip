@@ -722,6 +722,7 @@ int RunSearchChunk(smx_index* h, const float* queries, int nq, int L, int pre_nn
   // First pass: everything up to the stats copy.  Replayed as a captured
   // hipGraph when the call shape, buffers and stream repeat (one launch
   // instead of ~20, no per-kernel host overhead); eager otherwise.
+  bool seed_dispatch_ev = false;   // the seed timed by its own dispatch (fused work list)
   auto first_pass = [&]() -> int {
     Mark(h, 0, s);
     // front end: state reset, partition scores, top-L + ranks + LUTs
@@ -750,8 +751,10 @@ int RunSearchChunk(smx_index* h, const float* queries, int nq, int L, int pre_nn
           ix, cnt, w.work, w.leaf_item0, w.pos_unit0, w.gunits, uint32_t(nq), w.wave_start, h->grid,
           stats + 3, code_bytes, h->chunk_tiles, narrow, bd);
       Mark(h, 3, s);
-      SMX_HIP(smx::LaunchSeed(ix, sa, nq, s, &wla));
+      SMX_HIP(smx::LaunchSeed(ix, sa, nq, s, &wla, h->profiling ? h->ev[8] : nullptr,
+                              h->profiling ? h->ev[9] : nullptr));
       Mark(h, 4, s);
+      seed_dispatch_ev = h->profiling;
     } else if (h->serial_worklist) {
       // the work-list launches, then the seed, on one stream: beside the
       // seed's blocks (which fill every CU) the side-stream launches are
@@ -796,7 +799,8 @@ int RunSearchChunk(smx_index* h, const float* queries, int nq, int L, int pre_nn
     }
     SMX_HIP(smx::LaunchScan(ix, a, h->grid, variant, s, narrow, se0, se1));
     if (h->scan_log && !h->profiling) ++h->scan_logged;
-    SMX_HIP(smx::LaunchFinalSelect(sel, nq, s));
+    SMX_HIP(smx::LaunchFinalSelect(sel, nq, s, h->profiling ? h->ev[10] : nullptr,
+                                   h->profiling ? h->ev[11] : nullptr));
     Mark(h, 7, s);
     return SMX_OK;
   };
@@ -920,11 +924,14 @@ int RunSearchChunk(smx_index* h, const float* queries, int nq, int L, int pre_nn
     // stream) and the seed overlap, each timed from the fork
     t.partition_ms = Elapsed(h, 0, 1);
     t.lut_ms = 0.0f;
+    // the seed, scan and select kernels from events in their own dispatch
+    // packets (their execution, as rocprofv3 reports it); partition + top-L
+    // and the three-launch work list from event packets around the launches
     t.invert_ms = Elapsed(h, 1, 3);
-    t.seed_scan_ms = Elapsed(h, 1, 4);
+    t.seed_scan_ms = seed_dispatch_ev ? Elapsed(h, 8, 9) : Elapsed(h, 1, 4);
     t.seed_select_ms = 0.0f;
     t.scan_ms = Elapsed(h, 5, 6);
-    t.select_ms = Elapsed(h, 6, 7);
+    t.select_ms = Elapsed(h, 10, 11);
     t.total_ms = Elapsed(h, 0, 7);
   }
   unsigned long long cb;
