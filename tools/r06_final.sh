@@ -29,7 +29,9 @@ a)
   step smoke && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 &&
   step tests && timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 900 --timeout-method thread --durations=10 > $O/gpu_tests.log 2>&1 &&
   step fetch_glove && fetch glove && step fetch_sift && fetch sift &&
-  step alone_glove && alone glove && step alone_sift && alone sift && step done ;;
+  step alone_glove && alone glove && step alone_sift && alone sift &&
+  step diag_tests && SMX_LIB=scann_amd/lib/libscann_mi355x_diag.so timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 900 --timeout-method thread > $O/diag_tests.log 2>&1 &&
+  step done ;;
 b)
   step glove && timeout -k 10 600 python bench.py > $O/bench_glove.json 2> $O/bench_glove.err &&
   step glove_s20 && timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $O/bench_glove_s20.json 2> $O/bench_glove_s20.err &&
@@ -40,5 +42,10 @@ c)
   step soar && timeout -k 10 900 python bench.py --config soar100m > $O/bench_soar100m_shard.json 2> $O/bench_soar100m_shard.err &&
   step deep1b && timeout -k 10 1000 python bench.py --config deep1b > $O/bench_deep1b_shard.json 2> $O/bench_deep1b_shard.err && step done ;;
 d)
-  step alone_deep1b && alone deep1b && step done ;;
+  step alone_deep1b && alone deep1b &&
+  step stamps && timeout -k 10 300 python tools/phase_stamps.py 4 > $O/phases_glove.log 2>&1 &&
+  step pmc_scan && KREGEX=lut16_scan_kernel timeout -k 10 600 bash tools/pmc_kernel.sh $O/pmc_scan_glove &&
+  python tools/pmc_summary.py $O/pmc_scan_glove > $O/pmc_scan_glove.txt &&
+  step pmc_seed && KREGEX=seed_tau_kernel timeout -k 10 600 bash tools/pmc_kernel.sh $O/pmc_seed_glove &&
+  python tools/pmc_summary.py $O/pmc_seed_glove > $O/pmc_seed_glove.txt && step done ;;
 esac
