@@ -441,10 +441,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # rehearsal of the N-rank paths on a one-GPU box (never the measured
+    # configuration): SMX_BENCH_ONE_DEVICE=1 puts every rank on device 0,
+    # SMX_BENCH_BACKEND=gloo avoids RCCL's one-rank-per-GPU rule
+    if os.environ.get("SMX_BENCH_ONE_DEVICE") == "1":
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group(os.environ.get("SMX_BENCH_BACKEND") or
+                                ("nccl" if torch.cuda.is_available() else "gloo"))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
