@@ -584,7 +584,10 @@ def main():
                   "queries_per_gpu": e0_ - b0,
                   "parallelism": f"one {NQ}-query batch split over {world} GPU(s) by query_slice, "
                                  f"results all-gathered"
-                                 + (" (RCCL all_gather_into_tensor)" if world > 1 else "")
+                                 + ((" (RCCL all_gather_into_tensor)"
+                                     if dist.get_backend() == "nccl"
+                                     else f" ({dist.get_backend()} all_gather)")
+                                    if world > 1 else "")
                                  + f", {n_fl} batches in flight"}
         if rank == 0:
             # the split result == the whole batch searched on one GPU (rank 0's
