@@ -14,7 +14,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-LIB = os.path.join(ROOT, "scann_amd", "lib", "libscann_mi355x_time.so")
+LIB = os.environ.get("SMX_STAMP_LIB", os.path.join(ROOT, "scann_amd", "lib", "libscann_mi355x_time.so"))
 NAMES = {0: ("topl_wave", ["load", "rounds", "compact+rank", "out+rank atomics", "lut"]),
          1: ("seed_tau", ["lut+prefix", "score loop", "k'-th select"]),
          2: ("final_select", ["load+narrow", "rank", "gid gather", "dedupe", "exact", "out"])}
