@@ -79,3 +79,95 @@ def test_random_configuration_matches_oracle(oracle, case):
     np.testing.assert_array_equal(gc, oc, err_msg=str(p))
     np.testing.assert_array_equal(gi, oi, err_msg=str(p))
     np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32), err_msg=str(p))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(0, N_CASES, 3))
+def test_random_configuration_sharded_and_sub_batched(oracle, case):
+    """The same draws through the range-split path (W = 2..4 shards of the
+    leaves, their lists merged on the device; shard rows or dataset rows) and
+    through the device entry point with a leaf-slot budget that forces
+    sub-batches of ~1/3 of the batch: the oracle's whole-index results."""
+    import os
+    import torch
+    from scann_amd import _native
+    from scann_amd.distributed import NativeShardEngine
+    p = draw(case)
+    ix, q = build(p)
+    rng = np.random.default_rng(case)
+    oi, od, oc = oracle.search(ix, q, p["L"], p["pre"], p["final"], p["reorder"],
+                               oracle.MODE_IDEAL)
+    qd = torch.from_numpy(q).cuda()
+    nq = q.shape[0]
+    world = int(min(ix.num_leaves, rng.integers(2, 5)))
+    if world >= 2:
+        own = bool(rng.integers(2))
+        engines = [NativeShardEngine(ix.shard(r, world, own_rows=own), device=0)
+                   for r in range(world)]
+        k = engines[0].shard_width(p["L"], p["pre"], p["final"], p["reorder"])
+        entries = torch.empty((world, nq, k, 2), dtype=torch.int64, device="cuda")
+        for r, e in enumerate(engines):
+            e.search_shard(qd, p["L"], p["pre"], p["final"], p["reorder"], entries[r])
+        idx, dst, cnt = engines[0].merge(world, entries, nq, p["L"], p["pre"], p["final"],
+                                         p["reorder"])
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(cnt.cpu().numpy(), oc, err_msg=str(p))
+        np.testing.assert_array_equal(idx.cpu().numpy().astype(np.uint32), oi, err_msg=str(p))
+        np.testing.assert_array_equal(dst.cpu().numpy().view(np.uint32), od.view(np.uint32),
+                                      err_msg=str(p))
+    budget = str(max(1, ix.num_leaves * max(1, -(-nq // 3))))
+    old = os.environ.get("SMX_LEAF_SLOT_BUDGET")
+    os.environ["SMX_LEAF_SLOT_BUDGET"] = budget
+    try:
+        nat = _native.NativeIndex(ix)
+    finally:
+        if old is None:
+            os.environ.pop("SMX_LEAF_SLOT_BUDGET")
+        else:
+            os.environ["SMX_LEAF_SLOT_BUDGET"] = old
+    try:
+        f = p["final"]
+        di = torch.zeros((nq, f), dtype=torch.int32, device="cuda")
+        dd = torch.zeros((nq, f), dtype=torch.float32, device="cuda")
+        dc = torch.zeros(nq, dtype=torch.int32, device="cuda")
+        nat.search_batched_device(qd.data_ptr(), nq, p["L"], p["pre"], p["final"], p["reorder"],
+                                  di.data_ptr(), dd.data_ptr(), dc.data_ptr())
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(dc.cpu().numpy(), oc, err_msg=str(p))
+        np.testing.assert_array_equal(di.cpu().numpy().astype(np.uint32), oi, err_msg=str(p))
+        np.testing.assert_array_equal(dd.cpu().numpy().view(np.uint32), od.view(np.uint32),
+                                      err_msg=str(p))
+    finally:
+        nat.close()
+
+
+def draw_large(case):
+    """Batches of hundreds to thousands of queries over tens of thousands of
+    rows: many query tiles per leaf, 16- and 32-slot items, several segments
+    per workgroup and candidate lists past their first capacity."""
+    rng = np.random.default_rng(9100 + case)
+    d = int(rng.choice([32, 64, 96, 100, 128]))
+    metric = int(rng.integers(2))
+    p = dict(n=int(rng.integers(20000, 60000)), d=d, dpb=2, metric=metric,
+             leaves=int(rng.integers(40, 400)), residual=metric == 0 and bool(rng.integers(2)),
+             soar=bool(rng.random() < 0.3), nq=int(rng.choice([300, 1000, 2500])),
+             pre=int(rng.choice([10, 100, 250])), reorder=bool(rng.integers(2)),
+             seed=int(rng.integers(1, 1000)))
+    p["L"] = int(rng.integers(1, max(2, p["leaves"] // 4)))
+    p["final"] = int(min(p["pre"], 10))
+    return p
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(8))
+def test_random_large_batch_matches_oracle(oracle, case):
+    from scann_amd import _native
+    p = draw_large(case)
+    ix, q = build(p)
+    nat = _native.NativeIndex(ix)
+    gi, gd, gc = nat.search_batched(q, p["L"], p["pre"], p["final"], p["reorder"])
+    oi, od, oc = oracle.search(ix, q, p["L"], p["pre"], p["final"], p["reorder"],
+                               oracle.MODE_IDEAL)
+    np.testing.assert_array_equal(gc, oc, err_msg=str(p))
+    np.testing.assert_array_equal(gi, oi, err_msg=str(p))
+    np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32), err_msg=str(p))
