@@ -471,7 +471,10 @@ def main():
     # and select beside the other's scan) -- whole-job throughput, every
     # batch searched completely; the single-stream rate is reported beside it
     n_fl = max(1, args.in_flight)
-    streams = [torch.cuda.Stream(dev) for _ in range(n_fl)]
+    # (SMX_BENCH_STREAM_PRIORITY="-1,0,0": per-stream priorities, an A/B knob)
+    prio = [int(x) for x in os.environ.get("SMX_BENCH_STREAM_PRIORITY", "").split(",") if x]
+    streams = [torch.cuda.Stream(dev, priority=prio[i % len(prio)] if prio else 0)
+               for i in range(n_fl)]
     outs = [(torch.zeros((NQ, FINAL_NN), dtype=torch.int32, device=dev),
              torch.zeros((NQ, FINAL_NN), dtype=torch.float32, device=dev),
              torch.zeros(NQ, dtype=torch.int32, device=dev)) for _ in range(n_fl)]
