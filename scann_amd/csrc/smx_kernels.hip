@@ -1222,12 +1222,21 @@ __device__ __forceinline__ uint2 LeafQueryTiles(uint32_t c, uint32_t narrow) {
   if (narrow == kNarrowOnly) return make_uint2(0u, (c + kNarrowSlots - 1u) / kNarrowSlots);
   return make_uint2((c + kQueriesPerTile - 1u) / kQueriesPerTile, 0u);
 }
-// Per leaf: its items and units.
+// Per leaf: its items and units.  Every item also weighs kItemCost units
+// ahead of its first tile (its setup: the B fragments, the segment record, the
+// claim), so that shares of many small items take fewer tiles: the workgroups'
+// ends correlated with their segment counts (0.46, scan stamps).  Same-box
+// A/B of 0 / 2 / 4 / 6 / 10 (profiles/r06/ab/item_cost/): 4 took the scan
+// alone 66.8 -> 66.2 us (glove), 58.5 -> 57.1 us (SIFT), configs[4] even.
+#ifndef SMX_ITEM_COST
+#define SMX_ITEM_COST 4
+#endif
+constexpr uint32_t kItemCost = SMX_ITEM_COST;
 __device__ __forceinline__ uint32_t LeafUnits(uint32_t c, uint32_t n, uint32_t chunk_tiles,
                                               uint32_t narrow, uint32_t& items) {
   const uint2 qt = LeafQueryTiles(c, narrow);
   items = (qt.x + qt.y) * LeafChunks(n, chunk_tiles);
-  return (2u * qt.x + qt.y) * ((n + 31u) / 32u);
+  return (2u * qt.x + qt.y) * ((n + 31u) / 32u) + kItemCost * items;
 }
 
 // Phase 1 in two multi-block passes over the leaf positions in work order
@@ -1389,24 +1398,46 @@ __device__ void WaveStarts(const WorklistArgs& w, int p, const uint32_t* gunits,
     if (us >= ub) break;
     const uint32_t ue = U0 + uint32_t((uint64_t(span) * (k + 1)) / nw);
     const uint32_t off = us - ua;
-    uint32_t q, j, skip = 0;
-    if (off < 2u * tiles * qt.x) {   // in the 32-slot tiles (2 units each)
-      q = off / (2u * tiles);
-      const uint32_t ru = off - q * 2u * tiles;
-      j = (ru + 1u) / 2u;
-      skip = 2u * j - ru;
-      if (j == tiles) {   // (the leaf's next query tile, or the next leaf's first item)
-        ++q;
-        j = 0;
-      }
-    } else {                         // in the 16-slot tiles (one unit per tile)
-      const uint32_t o16 = off - 2u * tiles * qt.x;
-      q = qt.x + o16 / tiles;
-      j = o16 % tiles;
+    // the query tile, then the item (chunk) holding unit `off`: per item
+    // kItemCost units, then its tiles (2 units each in a 32-slot tile, 1 in a
+    // 16-slot one)
+    const uint32_t per32 = 2u * tiles + kItemCost * chunks;
+    uint32_t q, r, wt;
+    if (off < per32 * qt.x) {
+      q = off / per32;
+      r = off - q * per32;
+      wt = 2u;
+    } else {
+      const uint32_t per16 = tiles + kItemCost * chunks, o16 = off - per32 * qt.x;
+      q = qt.x + o16 / per16;
+      r = o16 - (q - qt.x) * per16;
+      wt = 1u;
     }
     uint32_t ch = 0;
-    if (q < qt.x + qt.y)
-      while (ChunkTiles(n, chunk_tiles, ch).y <= j) ++ch;
+    uint2 cr = ChunkTiles(n, chunk_tiles, 0);
+    while (r >= kItemCost + wt * (cr.y - cr.x)) {
+      r -= kItemCost + wt * (cr.y - cr.x);
+      cr = ChunkTiles(n, chunk_tiles, ++ch);
+    }
+    // the first tile whose first unit is at or after `off`, and the units
+    // between them (not the share's)
+    uint32_t j, skip;
+    if (r <= kItemCost) {
+      j = cr.x;
+      skip = kItemCost - r;
+    } else {
+      const uint32_t m = (r - kItemCost + wt - 1u) / wt;
+      j = cr.x + m;
+      skip = wt * m - (r - kItemCost);
+      if (j == cr.y) {   // the next item's first tile (the leaf's next query tile,
+        skip += kItemCost;   // or the next leaf's first item)
+        if (++ch == chunks) {
+          ch = 0;
+          ++q;
+        }
+        j = q < qt.x + qt.y ? ChunkTiles(n, chunk_tiles, ch).x : 0u;
+      }
+    }
     const uint32_t units = ue - us > skip ? ue - us - skip : 0u;
     SMX_CHECK(item0 + q * chunks + ch, w.bd.items + 1, "wave start item");
     SMX_GUARD(kGroups * k + g, w.bd.grid, "wave start")
@@ -2481,7 +2512,10 @@ struct SegDesc {
 // Wave 0 of a scan workgroup: the next segments of the share (item, first
 // tile, end tile, descriptor) into the LDS table, 64 items per step (a prefix
 // of their tiles), at most kMaxSegs; the share's remainder stays in s_sw /
-// s_su.
+// s_su.  sj: the share's first tile | kShareFirst until the first step (the
+// share starts at that tile's first unit: its item's kItemCost units are the
+// share before's).
+constexpr uint32_t kShareFirst = 0x80000000u;
 __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32_t& sj,
                                              uint32_t* s_item, uint32_t* s_end, uint32_t* s_next,
                                              SegDesc* s_desc, uint32_t& s_sw, uint32_t& s_su,
@@ -2491,9 +2525,11 @@ __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32
     const uint32_t idx = sw + uint32_t(lane);
     const WorkItem it = a.work[min(idx, a.num_items - 1)];
     const uint32_t wt = (it.leaf & kItemNarrow) ? 1u : 2u;   // units per tile
-    const uint32_t j0 = (lane == 0 && sj) ? sj : it.j0;
+    const bool first = lane == 0 && (sj & kShareFirst);
+    const uint32_t j0 = first ? (sj & ~kShareFirst) : it.j0;
+    const uint32_t ic = first ? 0u : kItemCost;                // the item's own units
     const uint32_t tt = it.jend > j0 ? it.jend - j0 : 0u;      // the item's tiles
-    const uint32_t t = min(tt * wt, su);                       // ... in units
+    const uint32_t t = min(ic + tt * wt, su);                  // ... in units
     uint32_t incl = t;
     for (int off = 1; off < 64; off <<= 1) {
       const uint32_t y = uint32_t(__shfl_up(int(incl), off));
@@ -2501,15 +2537,16 @@ __device__ __forceinline__ void ListSegments(const ScanArgs& a, int lane, uint32
     }
     const uint32_t excl = incl - t;
     const bool used = excl < su;   // a prefix of the lanes, lane 0 always
-    const bool take = used && tt > 0;
+    // the tiles whose first unit is inside the share
+    const uint32_t own = su - excl > ic ? min(tt, (su - excl - ic + wt - 1) / wt) : 0u;
+    const bool take = used && own > 0;
     if (take) SMX_CHECK(idx, a.bd.items, "listed item");
     const uint64_t bt = __ballot(take);
     if (take) {
       const uint32_t pos = nseg + uint32_t(__popcll(bt & ((1ull << lane) - 1ull)));
       s_item[pos] = idx;
       s_next[pos] = j0;
-      // the tiles whose first unit is inside the share
-      s_end[pos] = j0 + min(tt, (su - excl + wt - 1) / wt);
+      s_end[pos] = j0 + own;
       SegDesc dsc;
       dsc.tile_off = it.tile_off;
       dsc.member_off = it.member_off;
@@ -2611,7 +2648,7 @@ __global__ void __launch_bounds__(64 * ScanWaves<K>(), 1) lut16_scan_kernel(Scan
     s_sw = ws.x;
     s_su = ws.z;
   }
-  uint32_t sj = ws.y;   // the share's first tile inside its first item
+  uint32_t sj = ws.y | kShareFirst;   // the share's first tile inside its first item
   // The survivors of up to kStageSegs segments stay in the wave's stage and
   // go to the candidate lists together, when the stage is full and once at
   // the end: one list-slot atomic per (segment, query slot) with survivors,

@@ -9,9 +9,10 @@ import pytest
 import worklist_model as wm
 
 
+@pytest.mark.parametrize("alpha", [0, 1, 7])
 @pytest.mark.parametrize("small", [False, 2])
 @pytest.mark.parametrize("seed", range(10))
-def test_shares_cover_items_exactly_once(seed, small):
+def test_shares_cover_items_exactly_once(seed, small, alpha):
     rng = np.random.default_rng(seed)
     nl = int(rng.integers(1, 300))
     sizes = rng.integers(0, 3000, nl)
@@ -19,7 +20,7 @@ def test_shares_cover_items_exactly_once(seed, small):
     counts = rng.poisson(rng.uniform(0.5, 150), nl)
     counts[rng.random(nl) < 0.2] = 0                     # leaves no query visits
     wm.check([int(x) for x in sizes], [int(x) for x in counts], grid=int(rng.choice([64, 256, 3072])),
-             chunk_tiles=int(rng.choice([8, 16, 20, 40])), small=small)
+             chunk_tiles=int(rng.choice([8, 16, 20, 40])), small=small, alpha=alpha)
 
 
 @pytest.mark.parametrize("sizes,counts", [
@@ -32,7 +33,8 @@ def test_shares_cover_items_exactly_once(seed, small):
 def test_edge_shapes(sizes, counts):
     for small in (False, 2):
         for grid in (8, 256, 3072):
-            wm.check(sizes, counts, grid=grid, small=small)
+            for alpha in (0, 3, 40):
+                wm.check(sizes, counts, grid=grid, small=small, alpha=alpha)
 
 
 @pytest.mark.parametrize("seed", range(6))
@@ -69,7 +71,8 @@ def test_item_capacity_at_small_chunks(seed, chunk_tiles):
     sizes = [64 * 32] * nl if seed == 0 else [int(x) for x in rng.integers(0, 4000, nl)]
     counts = [48] * nl if seed == 0 else [int(x) for x in rng.poisson(rng.uniform(1, 60), nl)]
     for small in (False, 2):
-        wm.check(sizes, counts, grid=256, chunk_tiles=chunk_tiles, small=small)
+        for alpha in (0, 10):
+            wm.check(sizes, counts, grid=256, chunk_tiles=chunk_tiles, small=small, alpha=alpha)
     if seed == 0:
         wl = wm.build(sizes, counts, 256, 8, 2)
         assert len(wl["work"]) == 24 * nl

@@ -14,6 +14,7 @@ from __future__ import annotations
 import numpy as np
 
 GROUPS = 8
+ITEM_COST = 4   # smx_kernels.hip kItemCost
 
 
 def chunks_of(n, chunk_tiles):
@@ -50,11 +51,12 @@ def query_tiles(c, small=False):
     return (c + 31) // 32, 0
 
 
-def build(sizes, counts, grid, chunk_tiles, small=False):
+def build(sizes, counts, grid, chunk_tiles, small=False, alpha=ITEM_COST):
     """Items (leaf, n, j0, jend, query tile, weight) and the workgroups'
     shares (first item, first tile, units).  A unit is a 16-slot tile: a
-    32-slot item's tiles weigh 2, a 16-slot item's 1; a tile belongs to the
-    share holding its first unit."""
+    32-slot item's tiles weigh 2, a 16-slot item's 1, and every item adds
+    `alpha` units ahead of its first tile (kItemCost: its setup); a tile
+    belongs to the share holding its first unit."""
     nl = len(sizes)
     order = leaf_order(sizes)
     items_p, units_p = [], []
@@ -63,7 +65,7 @@ def build(sizes, counts, grid, chunk_tiles, small=False):
         c, n = counts[leaf], sizes[leaf]
         q32, q16 = query_tiles(c, small)
         items_p.append((q32 + q16) * chunks_of(n, chunk_tiles))
-        units_p.append((2 * q32 + q16) * ((n + 31) // 32))
+        units_p.append((2 * q32 + q16) * ((n + 31) // 32) + alpha * items_p[-1])
     ex_i = np.concatenate([[0], np.cumsum(items_p)[:-1]]).astype(int)
     ex_u = np.concatenate([[0], np.cumsum(units_p)[:-1]]).astype(int)
     total_w = int(sum(units_p))
@@ -118,23 +120,37 @@ def build(sizes, counts, grid, chunk_tiles, small=False):
                 break
             ue = U0 + (span * (k + 1)) // nw
             off = us - ua
-            if off < 2 * tiles * q32:
-                q, ru = divmod(off, 2 * tiles)
-                j = (ru + 1) // 2          # the first tile whose first unit is >= off
-                skip = 2 * j - ru
-                if j == tiles:
-                    q, j = q + 1, 0
-            else:                          # in the 16-slot tiles (1 unit each)
-                q16i, j = divmod(off - 2 * tiles * q32, tiles)
-                q, skip = q32 + q16i, 0
+            # the query tile, then the chunk (item) holding unit `off`
+            per32 = 2 * tiles + alpha * chunks
+            if off < per32 * q32:
+                q, r = divmod(off, per32)
+                wt = 2
+            else:
+                q16i, r = divmod(off - per32 * q32, tiles + alpha * chunks)
+                q, wt = q32 + q16i, 1
             ch = 0
-            if q < q32 + q16:
-                while chunk_tiles_range(n, chunk_tiles, ch)[1] <= j:
+            while True:
+                a0, a1 = chunk_tiles_range(n, chunk_tiles, ch)
+                if r < alpha + wt * (a1 - a0):
+                    break
+                r -= alpha + wt * (a1 - a0)
+                ch += 1
+            # the first tile whose first unit is >= off, and the units between
+            if r <= alpha:
+                j, skip = a0, alpha - r
+            else:
+                m = -(-(r - alpha) // wt)
+                j, skip = a0 + m, wt * m - (r - alpha)
+                if j == a1:                # the next item's first tile
+                    skip += alpha
                     ch += 1
+                    if ch == chunks:
+                        q, ch = q + 1, 0
+                    j = chunk_tiles_range(n, chunk_tiles, ch)[0] if q < q32 + q16 else 0
             wave_start[GROUPS * k + g] = (item0 + q * chunks + ch, j, max(0, ue - us - skip))
             k += 1
     return dict(order=order, work=work, slots=slots, wave_start=wave_start, gunits=gunits,
-                total_w=total_w, chunk_tiles=chunk_tiles)
+                total_w=total_w, chunk_tiles=chunk_tiles, alpha=alpha)
 
 
 def list_segments(wl, b, max_segs=512):
@@ -143,7 +159,9 @@ def list_segments(wl, b, max_segs=512):
     a partly taken item takes the tiles whose first unit is inside the share.
     Raises if a taken item is not a real one."""
     work = wl["work"]
+    alpha = wl.get("alpha", 0)
     sw, sj, su = wl["wave_start"][b]
+    first = True   # the share starts at a tile's first unit: no item cost
     segs = []
     while su > 0:
         used_lanes = 0
@@ -156,16 +174,18 @@ def list_segments(wl, b, max_segs=512):
                 raise AssertionError(f"share of workgroup {b} runs past the items (item {idx})")
             it = work[idx]
             w = it[5]
-            j0 = sj if (lane == 0 and sj) else it[2]
+            f = first and lane == 0
+            j0 = sj if f else it[2]
+            ae = 0 if f else alpha
             t = max(0, it[3] - j0)
             used_lanes += 1
-            take = min(t, -(-(su - excl) // w))
+            take = min(t, -(-(su - excl - ae) // w)) if su - excl > ae else 0
             if take > 0:
                 segs.append((idx, j0, j0 + take))
-            excl += min(t * w, su)
+            excl += min(ae + t * w, su)
         sw += used_lanes
         su -= min(su, excl)
-        sj = 0
+        sj, first = 0, False
     return segs
 
 
@@ -177,8 +197,8 @@ def max_items(sizes, pairs):
     return (pairs // 16 + len(sizes) + 1) * chunks
 
 
-def check(sizes, counts, grid=256, chunk_tiles=20, small=False):
-    wl = build(sizes, counts, grid, chunk_tiles, small)
+def check(sizes, counts, grid=256, chunk_tiles=20, small=False, alpha=ITEM_COST):
+    wl = build(sizes, counts, grid, chunk_tiles, small, alpha)
     cap = max_items(sizes, int(sum(counts)))
     assert len(wl["work"]) <= cap, f"{len(wl['work'])} items > MaxItems {cap}"
     assert all(w is not None for w in wl["wave_start"]), "a workgroup's share is not written"
@@ -204,5 +224,6 @@ def check(sizes, counts, grid=256, chunk_tiles=20, small=False):
         cover.setdefault((leaf, j0), []).extend(range(r0, r0 + ns))
     for (leaf, j0), ranks in cover.items():
         assert sorted(ranks) == list(range(counts[leaf])), (leaf, j0)
-    assert sum((j1 - j0) * w for (_, _, j0, j1, _, w) in wl["work"]) == wl["total_w"]
+    assert (sum((j1 - j0) * w for (_, _, j0, j1, _, w) in wl["work"])
+            + alpha * len(wl["work"])) == wl["total_w"]
     return wl
