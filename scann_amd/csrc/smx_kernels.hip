@@ -1504,7 +1504,10 @@ __global__ void __launch_bounds__(64) items_kernel(WorklistArgs w) {
 // scatter reads leaf_item0) and totals.  The seed blocks neither read nor
 // write anything these touch.
 constexpr int kWlPerThread = kFusedWorklistLeaves / 256;
-constexpr int kWlPosPerBlock = 4;
+#ifndef SMX_WL_POS
+#define SMX_WL_POS 4
+#endif
+constexpr int kWlPosPerBlock = SMX_WL_POS;
 
 __device__ void WorklistFusedBlock(const WorklistArgs& w, int b) {
   __shared__ uint32_t wsum[4], s_gunits[kGroups + 1], s_last_un[256];
